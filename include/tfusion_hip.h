@@ -1,0 +1,172 @@
+/*
+ * tfusion_hip.h -- C-ABI of libtfusion_hip.so, the MI355X (gfx950) implementation
+ * of the topfusion hot path: depth preprocessing, projective point-to-plane ICP,
+ * voxel-block-hash allocation, TSDF integration and raycasting.
+ *
+ * This is the drop-in boundary.  Plain pointers and sizes only; device pointers
+ * are HIP device pointers on the context's device.  Every entry point replaces a
+ * reference interface, cited as file:line relative to the 3d-scan/topfusion root.
+ * The C++ mirror of the reference API (include/tfusion/topfu.hpp etc.) is a thin layer over
+ * these functions; see INTEGRATION.md for the bindings.
+ *
+ * Error convention: every function returns a tf_status (0 = TF_OK).  The reference
+ * prints and exit()s on CUDA errors (tfusion/src/device_memory.cpp:7-11,
+ * tfusion/include/tfusion/cuda/CUDADefines.hpp:26-33); here the caller decides.
+ * ICP degeneracy is TF_ICP_FAIL and triggers the same reset as the reference
+ * (tfusion/src/topfu.cpp:263-264).
+ */
+#ifndef TFUSION_HIP_H
+#define TFUSION_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum tf_status {
+    TF_OK = 0,
+    TF_ICP_FAIL = 1,        /* estimateTransform returned false; scene was reset */
+    TF_INVALID_ARG = 2,
+    TF_OOM = 3,
+    TF_HIP_ERROR = 4,
+    TF_NO_DEVICE = 5
+} tf_status;
+
+/* TopFuParams (tfusion/include/tfusion/topfu.hpp:28-60) restricted to the fields the
+ * hot path reads, plus SceneParams (tfusion/include/tfusion/SceneParams.hpp:8-66)
+ * and the reference's compile-time capacities made run-time. */
+typedef struct tf_params {
+    int   cols, rows;
+    float fx, fy, cx, cy;               /* Intr */
+    float bilateral_sigma_depth;        /* m */
+    float bilateral_sigma_spatial;      /* px */
+    int   bilateral_kernel_size;        /* px (7) */
+    float icp_truncate_depth_dist;      /* m; <= 0 disables */
+    float icp_dist_thres;               /* m */
+    float icp_angle_thres;              /* rad */
+    int   icp_iter_num[4];              /* per level 0..3 */
+    float mu;                           /* TSDF truncation band (SceneParams::mu) */
+    int   maxW;
+    float voxelSize;                    /* m */
+    float viewFrustum_min, viewFrustum_max;
+    int   n_buckets;                    /* SDF_BUCKET_NUM, power of two (VoxelBlockHash.hpp:16) */
+    int   n_excess;                     /* SDF_EXCESS_LIST_SIZE (VoxelBlockHash.hpp:18) */
+    int   n_blocks;                     /* SDF_LOCAL_BLOCK_NUM (VoxelBlockHash.hpp:14) */
+    int   vis_capacity;                 /* visibleEntryIDs capacity (RenderState_VH.hpp:42) */
+    int   max_render_blocks;            /* MAX_RENDERING_BLOCKS (VisualisationEngine_Shared.hpp:5) */
+} tf_params;
+
+/* integer counters the reference keeps host-side (LocalVBA.hpp:26, VoxelBlockHash.hpp:69,
+ * RenderState_VH.hpp:33, VisualisationEngine_CUDA.cu:160) plus ICP bookkeeping */
+typedef struct tf_stats {
+    int lastFreeBlockId;
+    int lastFreeExcessListId;
+    int noVisibleEntries;
+    int noTotalBlocks;
+    int frame_counter;
+    int icp_iterations;                 /* iterations executed by the last estimateTransform */
+    int icp_ok;
+    int n_resets;
+} tf_stats;
+
+typedef struct tf_ctx tf_ctx;
+
+/* buffer ids for tf_download / tf_upload (state inspection for parity tests) */
+typedef enum tf_buffer {
+    TF_BUF_HASH = 0,          /* HashEntry[n_buckets+n_excess], 16 B each (VoxelBlockHash.hpp:32-44) */
+    TF_BUF_VBA = 1,           /* Voxel_s[n_blocks*512], 4 B each (VoxelTypes.hpp:69-92) */
+    TF_BUF_VISIBLE_IDS = 2,   /* int[vis_capacity] */
+    TF_BUF_VISIBLE_TYPE = 3,  /* uchar[n_buckets+n_excess] */
+    TF_BUF_RANGE = 4,         /* float2[rows*cols]  renderingRangeImage */
+    TF_BUF_RAYCAST = 5,       /* float4[rows*cols]  raycastResult */
+    TF_BUF_DISTS = 6,         /* float[rows*cols] */
+    TF_BUF_DEPTH = 7,         /* ushort[level]  filtered depth pyramid */
+    TF_BUF_CURR_POINTS = 8,   /* float4[level] */
+    TF_BUF_CURR_NORMALS = 9,
+    TF_BUF_PREV_POINTS = 10,
+    TF_BUF_PREV_NORMALS = 11,
+    TF_BUF_GREY = 12          /* uchar4[rows*cols] last renderImage output */
+} tf_buffer;
+
+/* ---- device ---------------------------------------------------------------- */
+/* cuda::getCudaEnabledDeviceCount / setDevice (tfusion/include/tfusion/topfu.hpp:20-21) */
+tf_status tf_device_count(int* count);
+tf_status tf_set_device(int device);
+const char* tf_status_string(tf_status s);
+
+/* ---- context (TopFu) -------------------------------------------------------- */
+/* TopFuParams::default_params (tfusion/src/topfu.cpp:12-53) */
+tf_status tf_default_params(tf_params* p);
+/* TopFu::TopFu (tfusion/src/topfu.cpp:55-84): allocates the scene, render state and
+ * ICP buffers on the current device and creates one HIP stream. */
+tf_status tf_create(const tf_params* p, tf_ctx** out);
+void      tf_destroy(tf_ctx* ctx);
+/* TopFu::reset (tfusion/src/topfu.cpp:141-152) */
+tf_status tf_reset(tf_ctx* ctx);
+/* TopFu::operator()(const cuda::Depth&) (tfusion/src/topfu.cpp:161-330).
+ * dev_depth: uint16 millimetres, rows x cols, row pitch in bytes.  Synchronous.
+ * Returns TF_OK (true) or TF_ICP_FAIL (false, scene reset).  pose_out (optional):
+ * getCameraPose() as a row-major 3x4 [R|t]. */
+tf_status tf_process_frame(tf_ctx* ctx, const uint16_t* dev_depth, size_t pitch_bytes,
+                           float pose_out[12], tf_stats* stats);
+/* same, host depth (cuda::Depth::upload, device_array.hpp; demo.cpp:100) */
+tf_status tf_process_frame_host(tf_ctx* ctx, const uint16_t* host_depth, size_t pitch_bytes,
+                                float pose_out[12], tf_stats* stats);
+/* Runs n frames (frame i at dev_frames + i*frame_stride_bytes, pitch cols*2) with the
+ * exact per-frame semantics of tf_process_frame, but without a host round trip per
+ * frame.  ok_out (optional, n ints) receives each frame's bool. */
+tf_status tf_process_frames(tf_ctx* ctx, const uint16_t* dev_frames, size_t frame_stride_bytes, int n,
+                            int* ok_out);
+/* TopFu::renderImage (tfusion/src/topfu.cpp:332-377): raycast + grey shading of the
+ * current pose into dev_rgba (uchar4, rows x cols, pitch bytes). */
+tf_status tf_render_image(tf_ctx* ctx, uint8_t* dev_rgba, size_t pitch_bytes);
+/* TopFu::getCameraPose (tfusion/src/topfu.cpp:154-159), time = -1 only */
+tf_status tf_get_pose(tf_ctx* ctx, float rt[12]);
+tf_status tf_get_stats(tf_ctx* ctx, tf_stats* stats);
+tf_status tf_get_params(tf_ctx* ctx, tf_params* p);
+/* HIP stream owned by the context (hipStream_t), for interop */
+void*     tf_get_stream(tf_ctx* ctx);
+
+/* ---- stage entry points (operate on context state; parity tests) ------------- */
+/* computeDists + depthBilateralFilter + depthTruncation + depthBuildPyramid +
+ * computePointNormals (topfu.cpp:166-197; imgproc.cpp:3-48) into the curr pyramid */
+tf_status tf_stage_preprocess(tf_ctx* ctx, const uint16_t* dev_depth, size_t pitch_bytes);
+/* same, host depth */
+tf_status tf_stage_preprocess_host(tf_ctx* ctx, const uint16_t* host_depth, size_t pitch_bytes);
+/* ProjectiveICP::estimateTransform(points overload) (projective_icp.cpp:169-213) on
+ * the context's curr/prev pyramids; affine_rt (out) row-major 3x4. */
+tf_status tf_stage_icp(tf_ctx* ctx, float affine_rt[12], int* ok, int* iterations);
+/* SceneReconstructionEngine_CUDA::AllocateSceneFromDepth
+ * (SceneReconstructionEngine_host.cu:75-195) with the context's dists */
+tf_status tf_stage_alloc(tf_ctx* ctx, const float pose_rt[12]);
+/* ::IntegrateIntoScene (SceneReconstructionEngine_host.cu:197-251) */
+tf_status tf_stage_integrate(tf_ctx* ctx, const float pose_rt[12]);
+/* VisualisationEngine_CUDA::CreateExpectedDepths (VisualisationEngine_CUDA.cu:119-173) */
+tf_status tf_stage_expected_depths(tf_ctx* ctx, const float pose_rt[12]);
+/* GenericRaycast (VisualisationEngine_CUDA.cu:175-218) into raycastResult */
+tf_status tf_stage_raycast(tf_ctx* ctx, const float invM_rt[12], int update_visible);
+/* renderICP_device + resizePointsNormals (VisualisationEngine_CUDA.cu:323-360,
+ * topfu.cpp:308-309): raycastResult -> prev points/normals pyramid */
+tf_status tf_stage_icp_maps(tf_ctx* ctx, const float invM_rt[12]);
+/* renderGrey_device (VisualisationHelper.hpp:105-118) from raycastResult */
+tf_status tf_stage_render_grey(tf_ctx* ctx, const float invM_rt[12]);
+/* ResetScene (SceneReconstructionEngine_host.cu:51-73) only */
+tf_status tf_stage_reset_scene(tf_ctx* ctx);
+/* swap curr <-> prev points/normals pyramids (topfu.cpp:205-207) */
+tf_status tf_stage_swap_pyramids(tf_ctx* ctx);
+
+/* ---- state transfer --------------------------------------------------------- */
+/* host <-> context buffer copies; level selects the pyramid level for TF_BUF_DEPTH..
+ * TF_BUF_PREV_NORMALS.  bytes must equal the buffer size (tf_buffer_bytes). */
+tf_status tf_buffer_bytes(tf_ctx* ctx, int which, int level, size_t* bytes);
+tf_status tf_download(tf_ctx* ctx, int which, int level, void* host, size_t bytes);
+tf_status tf_upload(tf_ctx* ctx, int which, int level, const void* host, size_t bytes);
+tf_status tf_set_pose(tf_ctx* ctx, const float rt[12]);
+tf_status tf_set_counters(tf_ctx* ctx, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

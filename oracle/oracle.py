@@ -1,0 +1,310 @@
+"""ctypes wrapper around the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product (topfusion_amd/).
+See oracle/tf_oracle.h for what is pinned and what is "parity unpinned".
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("cols", ctypes.c_int), ("rows", ctypes.c_int),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("bilateral_sigma_depth", ctypes.c_float), ("bilateral_sigma_spatial", ctypes.c_float),
+                ("bilateral_kernel_size", ctypes.c_int),
+                ("icp_truncate_depth_dist", ctypes.c_float), ("icp_dist_thres", ctypes.c_float),
+                ("icp_angle_thres", ctypes.c_float), ("icp_iter_num", ctypes.c_int * 4),
+                ("mu", ctypes.c_float), ("maxW", ctypes.c_int), ("voxelSize", ctypes.c_float),
+                ("viewFrustum_min", ctypes.c_float), ("viewFrustum_max", ctypes.c_float),
+                ("n_buckets", ctypes.c_int), ("n_excess", ctypes.c_int), ("n_blocks", ctypes.c_int),
+                ("vis_capacity", ctypes.c_int), ("max_render_blocks", ctypes.c_int)]
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries",
+                                            "noTotalBlocks", "frame_counter", "icp_iterations", "icp_ok",
+                                            "n_resets")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+HASH_DTYPE = np.dtype([("x", "<i2"), ("y", "<i2"), ("z", "<i2"), ("pad", "<i2"), ("offset", "<i4"), ("ptr", "<i4")])
+VOXEL_DTYPE = np.dtype([("sdf", "<i2"), ("w", "u1"), ("pad", "u1")])
+
+_lib = None
+
+
+def build():
+    """Compile the oracle with its Makefile (gcc, -ffp-contract=off)."""
+    subprocess.run(["make", "-s", "-C", _HERE, "liboracle.so"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = ctypes.CDLL(_LIB)
+        P = ctypes.c_void_p
+        L.tfo_default_params.argtypes = [ctypes.POINTER(Params)]
+        L.tfo_exp.argtypes = [ctypes.c_float]; L.tfo_exp.restype = ctypes.c_float
+        L.tfo_compute_dists.argtypes = [P, ctypes.c_int, ctypes.c_int, P]
+        L.tfo_bilateral.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float]
+        L.tfo_truncate.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_float]
+        L.tfo_pyr_down.argtypes = [P, ctypes.c_int, ctypes.c_int, P, ctypes.c_float]
+        L.tfo_points_normals.argtypes = [P, ctypes.c_int, ctypes.c_int] + [ctypes.c_float] * 4 + [P, P]
+        L.tfo_resize_points_normals.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, P]
+        L.tfo_icp_reduce.argtypes = [P, P, P, P, ctypes.c_int, ctypes.c_int] + [ctypes.c_float] * 6 + [P, P]
+        L.tfo_icp_step.argtypes = [P, P, ctypes.POINTER(ctypes.c_double)]; L.tfo_icp_step.restype = ctypes.c_int
+        L.tfo_rigid_mul.argtypes = [P, P, P]
+        L.tfo_rigid_inv.argtypes = [P, P]
+        L.tfo_matrix4_inv.argtypes = [P, P]; L.tfo_matrix4_inv.restype = ctypes.c_int
+        L.tfo_m4v.argtypes = [P, P, P]
+        L.tfo_tsdf_update.argtypes = [P, P, ctypes.c_float, ctypes.c_float, ctypes.c_int]
+        L.tfo_sincos.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.tfo_rodrigues.argtypes = [P, P]
+        L.tfo_create.argtypes = [ctypes.POINTER(Params)]; L.tfo_create.restype = P
+        L.tfo_destroy.argtypes = [P]
+        L.tfo_reset.argtypes = [P]
+        L.tfo_process_frame.argtypes = [P, P]; L.tfo_process_frame.restype = ctypes.c_int
+        L.tfo_get_counters.argtypes = [P, ctypes.POINTER(Counters)]
+        L.tfo_get_pose.argtypes = [P, P]
+        L.tfo_alloc.argtypes = [P, P, P]
+        L.tfo_integrate.argtypes = [P, P, P]
+        L.tfo_expected_depths.argtypes = [P, P]
+        L.tfo_raycast.argtypes = [P, P, ctypes.c_int]
+        L.tfo_render_icp.argtypes = [P, P, P, P]
+        L.tfo_render_grey.argtypes = [P, P, P]
+        L.tfo_render_image.argtypes = [P, P]
+        for name in ("tfo_hash", "tfo_vba", "tfo_visible_ids", "tfo_visible_type", "tfo_range_image",
+                     "tfo_raycast_result", "tfo_dists"):
+            getattr(L, name).argtypes = [P]; getattr(L, name).restype = P
+        for name in ("tfo_prev_points", "tfo_prev_normals", "tfo_curr_points", "tfo_curr_normals", "tfo_curr_depth"):
+            getattr(L, name).argtypes = [P, ctypes.c_int]; getattr(L, name).restype = P
+        _lib = L
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def default_params(**kw):
+    p = Params()
+    lib().tfo_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        if k == "icp_iter_num":
+            for i in range(4):
+                p.icp_iter_num[i] = int(v[i]) if i < len(v) else 0
+        else:
+            setattr(p, k, v)
+    return p
+
+
+# ---- stateless stages -------------------------------------------------------
+
+def compute_dists(depth):
+    H, W = depth.shape
+    out = np.empty((H, W), np.float32)
+    lib().tfo_compute_dists(ptr(np.ascontiguousarray(depth, np.uint16)), W, H, ptr(out))
+    return out
+
+
+def bilateral(depth, ksz=7, sigma_spatial=4.5, sigma_depth=0.04):
+    H, W = depth.shape
+    src = np.ascontiguousarray(depth, np.uint16)
+    out = np.empty_like(src)
+    lib().tfo_bilateral(ptr(src), ptr(out), W, H, ksz, sigma_spatial, sigma_depth)
+    return out
+
+
+def truncate(depth, max_dist=2.0):
+    H, W = depth.shape
+    out = np.ascontiguousarray(depth, np.uint16).copy()
+    lib().tfo_truncate(ptr(out), W, H, max_dist)
+    return out
+
+
+def pyr_down(depth, sigma_depth=0.04):
+    H, W = depth.shape
+    src = np.ascontiguousarray(depth, np.uint16)
+    out = np.empty((H // 2, W // 2), np.uint16)
+    lib().tfo_pyr_down(ptr(src), W, H, ptr(out), sigma_depth)
+    return out
+
+
+def points_normals(depth, fx, fy, cx, cy):
+    H, W = depth.shape
+    src = np.ascontiguousarray(depth, np.uint16)
+    pts = np.empty((H, W, 4), np.float32)
+    nrm = np.empty((H, W, 4), np.float32)
+    lib().tfo_points_normals(ptr(src), W, H, fx, fy, cx, cy, ptr(pts), ptr(nrm))
+    return pts, nrm
+
+
+def resize_points_normals(pts, nrm):
+    H, W = pts.shape[:2]
+    po = np.empty((H // 2, W // 2, 4), np.float32)
+    no = np.empty((H // 2, W // 2, 4), np.float32)
+    lib().tfo_resize_points_normals(ptr(np.ascontiguousarray(pts)), ptr(np.ascontiguousarray(nrm)), W, H, ptr(po), ptr(no))
+    return po, no
+
+
+def icp_reduce(vcurr, ncurr, vprev, nprev, fx, fy, cx, cy, min_cosine, dist2_thres, aff):
+    H, W = vcurr.shape[:2]
+    out = np.empty(27, np.float32)
+    a = np.ascontiguousarray(aff, np.float32).reshape(12)
+    lib().tfo_icp_reduce(ptr(vcurr), ptr(ncurr), ptr(vprev), ptr(nprev), W, H, fx, fy, cx, cy,
+                         min_cosine, dist2_thres, ptr(a), ptr(out))
+    return out
+
+
+def icp_step(sums27, affine):
+    a = np.ascontiguousarray(affine, np.float32).reshape(12).copy()
+    s = np.ascontiguousarray(sums27, np.float32)
+    det = ctypes.c_double()
+    ok = lib().tfo_icp_step(ptr(s), ptr(a), ctypes.byref(det))
+    return bool(ok), a, det.value
+
+
+def matrix4_inv(m):
+    m = np.ascontiguousarray(m, np.float32).reshape(16)
+    out = np.zeros(16, np.float32)
+    ok = lib().tfo_matrix4_inv(ptr(m), ptr(out))
+    return bool(ok), out
+
+
+def m4v(m, v):
+    out = np.zeros(4, np.float32)
+    lib().tfo_m4v(ptr(np.ascontiguousarray(m, np.float32)), ptr(np.ascontiguousarray(v, np.float32)), ptr(out))
+    return out
+
+
+def tsdf_update(sdf, w, eta, mu=0.02, maxW=100):
+    s = np.array([sdf], np.int16)
+    ww = np.array([w], np.uint8)
+    lib().tfo_tsdf_update(ptr(s), ptr(ww), eta, mu, maxW)
+    return int(s[0]), int(ww[0])
+
+
+# ---- stateful pipeline -------------------------------------------------------
+
+class Oracle:
+    """The reference TopFu pipeline restated on the CPU (oracle/tf_oracle.c)."""
+
+    def __init__(self, params=None, **kw):
+        self.params = params if params is not None else default_params(**kw)
+        self.ctx = lib().tfo_create(ctypes.byref(self.params))
+        self.W, self.H = self.params.cols, self.params.rows
+        self.n_total = self.params.n_buckets + self.params.n_excess
+
+    def __del__(self):
+        try:
+            if getattr(self, "ctx", None):
+                lib().tfo_destroy(self.ctx)
+                self.ctx = None
+        except Exception:
+            pass
+
+    def __call__(self, depth):
+        d = np.ascontiguousarray(depth, np.uint16)
+        assert d.shape == (self.H, self.W)
+        return bool(lib().tfo_process_frame(self.ctx, ptr(d)))
+
+    def reset(self):
+        lib().tfo_reset(self.ctx)
+
+    def counters(self):
+        c = Counters()
+        lib().tfo_get_counters(self.ctx, ctypes.byref(c))
+        return c.as_dict()
+
+    def pose(self):
+        rt = np.zeros(12, np.float32)
+        lib().tfo_get_pose(self.ctx, ptr(rt))
+        return rt.reshape(3, 4)
+
+    def _view(self, addr, dtype, count, shape=None):
+        buf = (ctypes.c_char * (np.dtype(dtype).itemsize * count)).from_address(addr)
+        a = np.frombuffer(buf, dtype=dtype, count=count)
+        return a.reshape(shape) if shape else a
+
+    def hash(self):
+        return self._view(lib().tfo_hash(self.ctx), HASH_DTYPE, self.n_total).copy()
+
+    def vba(self):
+        return self._view(lib().tfo_vba(self.ctx), VOXEL_DTYPE, self.params.n_blocks * 512).copy()
+
+    def visible_ids(self):
+        n = self.counters()["noVisibleEntries"]
+        return self._view(lib().tfo_visible_ids(self.ctx), np.int32, self.params.vis_capacity)[:n].copy()
+
+    def visible_type(self):
+        return self._view(lib().tfo_visible_type(self.ctx), np.uint8, self.n_total).copy()
+
+    def range_image(self):
+        return self._view(lib().tfo_range_image(self.ctx), np.float32, self.W * self.H * 2, (self.H, self.W, 2)).copy()
+
+    def raycast_result(self):
+        return self._view(lib().tfo_raycast_result(self.ctx), np.float32, self.W * self.H * 4, (self.H, self.W, 4)).copy()
+
+    def dists(self):
+        return self._view(lib().tfo_dists(self.ctx), np.float32, self.W * self.H, (self.H, self.W)).copy()
+
+    def level_shape(self, l):
+        return self.H >> l, self.W >> l
+
+    def prev_maps(self, l):
+        h, w = self.level_shape(l)
+        p = self._view(lib().tfo_prev_points(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
+        n = self._view(lib().tfo_prev_normals(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
+        return p, n
+
+    def curr_maps(self, l):
+        h, w = self.level_shape(l)
+        p = self._view(lib().tfo_curr_points(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
+        n = self._view(lib().tfo_curr_normals(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
+        return p, n
+
+    def curr_depth(self, l):
+        h, w = self.level_shape(l)
+        return self._view(lib().tfo_curr_depth(self.ctx, l), np.uint16, h * w, (h, w)).copy()
+
+    # stage-level
+    def alloc(self, pose_rt, dists):
+        lib().tfo_alloc(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
+                        ptr(np.ascontiguousarray(dists, np.float32)))
+
+    def integrate(self, pose_rt, dists):
+        lib().tfo_integrate(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
+                            ptr(np.ascontiguousarray(dists, np.float32)))
+
+    def expected_depths(self, pose_rt):
+        lib().tfo_expected_depths(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)))
+
+    def raycast(self, invM_rt, update_visible):
+        lib().tfo_raycast(self.ctx, ptr(np.ascontiguousarray(invM_rt, np.float32).reshape(12)), int(update_visible))
+
+    def render_icp(self, invM_rt):
+        pts = np.empty((self.H, self.W, 4), np.float32)
+        nrm = np.empty((self.H, self.W, 4), np.float32)
+        lib().tfo_render_icp(self.ctx, ptr(np.ascontiguousarray(invM_rt, np.float32).reshape(12)), ptr(pts), ptr(nrm))
+        return pts, nrm
+
+    def render_grey(self, invM_rt):
+        img = np.empty((self.H, self.W, 4), np.uint8)
+        lib().tfo_render_grey(self.ctx, ptr(np.ascontiguousarray(invM_rt, np.float32).reshape(12)), ptr(img))
+        return img
+
+    def render_image(self):
+        img = np.empty((self.H, self.W, 4), np.uint8)
+        lib().tfo_render_image(self.ctx, ptr(img))
+        return img

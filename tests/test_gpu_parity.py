@@ -1,0 +1,210 @@
+"""GPU parity: every stage of the HIP path against the CPU oracle, bit for bit.
+
+All comparisons are bit-exact (NaN == NaN): integer/index work (hash table, visible list,
+counters, allocation order, voxel weights) and the floating point work, because both
+sides implement the same canonical arithmetic.  The reference's
+CUDA build cannot be run anywhere available, so the oracle is the judge.
+"""
+import numpy as np
+import pytest
+
+from parity_util import assert_bit_exact, assert_struct_exact, hash_block_set
+from topfusion_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+I_RT = np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 0]], np.float32)
+
+
+def make_pair(oracle_mod, cols=640, rows=480, **kw):
+    from topfusion_amd import TopFu, default_params
+    fx, fy, cx, cy = synth.intrinsics(cols, rows)
+    args = dict(cols=cols, rows=rows, fx=fx, fy=fy, cx=cx, cy=cy, **kw)
+    return TopFu(default_params(**args)), oracle_mod.Oracle(oracle_mod.default_params(**args))
+
+
+def compare_scene(g, o, tag=""):
+    hg, ho = g.hash(), o.hash()
+    assert hash_block_set(hg) == hash_block_set(ho), f"{tag} allocated block sets differ"
+    assert_struct_exact(f"{tag} hash", hg, ho, ["x", "y", "z", "offset", "ptr"])
+    sg, so = g.stats(), o.counters()
+    for k in ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries"):
+        assert sg[k] == so[k], f"{tag} {k}: gpu {sg[k]} oracle {so[k]}"
+    assert_bit_exact(f"{tag} visible_ids", g.visible_ids(), o.visible_ids())
+    assert_bit_exact(f"{tag} visible_type", g.visible_type(), o.visible_type())
+    vg, vo = g.vba(), o.vba()
+    assert_struct_exact(f"{tag} vba", vg, vo, ["sdf", "w"])
+
+
+def test_preprocess(oracle_mod):
+    g, o = make_pair(oracle_mod)
+    d = synth.room_corner(noise_mm=2.0, holes=0.02, seed=3)
+    d[100:110, 200:260] = 2500          # > 2047 mm (dists -1) and > 2 m (truncated)
+    d[300, 300] = 65535
+    g.stage_preprocess(d)
+    assert_bit_exact("dists", g.dists(), oracle_mod.compute_dists(d))
+    d0 = oracle_mod.truncate(oracle_mod.bilateral(d), 2.0)
+    assert_bit_exact("depth0", g.curr_depth(0), d0)
+    d1 = oracle_mod.pyr_down(d0)
+    d2 = oracle_mod.pyr_down(d1)
+    assert_bit_exact("depth1", g.curr_depth(1), d1)
+    assert_bit_exact("depth2", g.curr_depth(2), d2)
+    p = g.params()
+    for l, dl in enumerate((d0, d1, d2)):
+        div = float(1 << l)
+        pts, nrm = oracle_mod.points_normals(dl, np.float32(p.fx) / np.float32(div), np.float32(p.fy) / np.float32(div),
+                                             np.float32(p.cx) / np.float32(div), np.float32(p.cy) / np.float32(div))
+        gp, gn = g.curr_maps(l)
+        assert_bit_exact(f"points L{l}", gp, pts)
+        assert_bit_exact(f"normals L{l}", gn, nrm)
+
+
+def test_frame0_alloc_integrate(oracle_mod):
+    g, o = make_pair(oracle_mod)
+    d = synth.room_corner()
+    assert g(d) is True
+    assert o(d) is True
+    compare_scene(g, o, "frame0")
+
+
+def test_stage_raycast_maps_grey(oracle_mod):
+    g, o = make_pair(oracle_mod)
+    d = synth.room_corner()
+    g(d)
+    o(d)
+    # CreateExpectedDepths / raycast / ICP maps / grey render at a slightly moved pose
+    R, t = synth.orbit_pose(3)
+    pose = np.zeros((3, 4), np.float32)
+    pose[:, :3] = R
+    pose[:, 3] = t
+    inv = np.zeros((3, 4), np.float32)
+    from oracle import oracle as O
+    a = np.ascontiguousarray(pose.reshape(12))
+    O.lib().tfo_rigid_inv(O.ptr(a), O.ptr(inv.reshape(12)))
+    g.stage_expected_depths(inv)
+    o.expected_depths(inv)
+    assert_bit_exact("range", g.range_image(), o.range_image())
+    assert g.stats()["noTotalBlocks"] == o.counters()["noTotalBlocks"]
+    g.stage_raycast(pose, 1)
+    o.raycast(pose, 1)
+    assert_bit_exact("raycast", g.raycast_result(), o.raycast_result())
+    assert_bit_exact("visible_type after raycast<true>", g.visible_type(), o.visible_type())
+    g.stage_icp_maps(pose)
+    op, on = o.render_icp(pose)
+    gp, gn = g.prev_maps(0)
+    assert_bit_exact("icp points L0", gp, op)
+    assert_bit_exact("icp normals L0", gn, on)
+    p1, n1 = oracle_mod.resize_points_normals(op, on)
+    p2, n2 = oracle_mod.resize_points_normals(p1, n1)
+    gp1, gn1 = g.prev_maps(1)
+    gp2, gn2 = g.prev_maps(2)
+    assert_bit_exact("icp points L1", gp1, p1)
+    assert_bit_exact("icp normals L1", gn1, n1)
+    assert_bit_exact("icp points L2", gp2, p2)
+    assert_bit_exact("icp normals L2", gn2, n2)
+    assert_bit_exact("grey", g.stage_render_grey(pose), o.render_grey(pose))
+
+
+def test_icp_stage(oracle_mod):
+    g, o = make_pair(oracle_mod)
+    seq = synth.orbit_sequence(2, seed=5)
+    # prev = frame-0 camera maps, curr = frame-1 maps (the reference's frame-1 situation)
+    g.stage_preprocess(seq[0])
+    g.stage_swap_pyramids()
+    g.stage_preprocess(seq[1])
+    ok, aff, iters = g.stage_icp()
+    o(seq[0])
+    p = g.params()
+    # oracle loop, exactly estimateTransform
+    affine = I_RT.copy().reshape(12)
+    oiters = 0
+    ook = True
+    for l, n_it in ((2, 4), (1, 5), (0, 10)):
+        div = np.float32(1 << l)
+        vc, nc = g.curr_maps(l)
+        vp, npv = o.prev_maps(l)
+        for _ in range(n_it):
+            s = oracle_mod.icp_reduce(vc, nc, vp, npv, np.float32(p.fx) / div, np.float32(p.fy) / div,
+                                      np.float32(p.cx) / div, np.float32(p.cy) / div,
+                                      _cosf(p.icp_angle_thres),
+                                      np.float32(p.icp_dist_thres) * np.float32(p.icp_dist_thres), affine)
+            oiters += 1
+            ok_i, affine, _ = oracle_mod.icp_step(s, affine)
+            if not ok_i:
+                ook = False
+                break
+        if not ook:
+            break
+    assert ok == ook
+    assert iters == oiters
+    assert_bit_exact("icp affine", aff.reshape(12), affine)
+
+
+def _cosf(x):
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.cosf.argtypes = [ctypes.c_float]
+    libm.cosf.restype = ctypes.c_float
+    return libm.cosf(x)
+
+
+@pytest.mark.parametrize("cols,rows,nframes", [(640, 480, 6), (320, 240, 16)])
+def test_sequence(oracle_mod, cols, rows, nframes):
+    """Whole TopFu::operator() frames: state identical after every frame."""
+    g, o = make_pair(oracle_mod, cols, rows)
+    seq = synth.orbit_sequence(nframes, cols, rows, seed=7)
+    for k in range(nframes):
+        okg = g(seq[k])
+        oko = o(seq[k])
+        assert okg == oko, f"frame {k}: ok gpu {okg} oracle {oko}"
+        sg, so = g.last_stats, o.counters()
+        for key in ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries", "icp_iterations", "frame_counter"):
+            assert sg[key] == so[key], f"frame {k} {key}: gpu {sg[key]} oracle {so[key]}"
+        if k > 0:
+            assert sg["noTotalBlocks"] == so["noTotalBlocks"], f"frame {k} noTotalBlocks"
+        assert_bit_exact(f"frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
+    compare_scene(g, o, "final")
+    assert_bit_exact("final raycast", g.raycast_result(), o.raycast_result())
+    for l in range(3):
+        gp, gn = g.prev_maps(l)
+        op, on = o.prev_maps(l)
+        assert_bit_exact(f"final prev points L{l}", gp, op)
+        assert_bit_exact(f"final prev normals L{l}", gn, on)
+
+
+def test_icp_failure_reset(oracle_mod):
+    """A frame without correspondences fails the det check -> reset (topfu.cpp:263-264)."""
+    g, o = make_pair(oracle_mod, 320, 240)
+    seq = synth.orbit_sequence(3, 320, 240, seed=9)
+    empty = np.zeros_like(seq[0])
+    frames = [seq[0], seq[1], empty, seq[2], seq[0]]
+    for k, f in enumerate(frames):
+        okg, oko = g(f), o(f)
+        assert okg == oko, f"frame {k}: gpu {okg} oracle {oko}"
+        sg, so = g.last_stats, o.counters()
+        for key in ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries", "icp_iterations", "frame_counter",
+                    "n_resets"):
+            assert sg[key] == so[key], f"frame {k} {key}: gpu {sg[key]} oracle {so[key]}"
+    compare_scene(g, o, "after reset")
+
+
+def test_small_hash_excess_chains(oracle_mod):
+    """Tiny bucket array: heavy collisions exercise excess chains and ordered excess slots."""
+    g, o = make_pair(oracle_mod, 320, 240, n_buckets=4096, n_excess=8192, n_blocks=16384, vis_capacity=65536)
+    seq = synth.orbit_sequence(4, 320, 240, seed=11)
+    for k in range(4):
+        assert g(seq[k]) == o(seq[k])
+    compare_scene(g, o, "excess")
+    assert (g.hash()["offset"] > 0).sum() > 0
+
+
+def test_capacity_exhaustion(oracle_mod):
+    """VBA smaller than the request count: the serial-order fallback must match."""
+    g, o = make_pair(oracle_mod, 320, 240, n_buckets=4096, n_excess=256, n_blocks=600, vis_capacity=65536)
+    seq = synth.orbit_sequence(3, 320, 240, seed=13)
+    for k in range(3):
+        assert g(seq[k]) == o(seq[k])
+        sg, so = g.last_stats, o.counters()
+        assert sg["lastFreeBlockId"] == so["lastFreeBlockId"]
+        assert sg["lastFreeExcessListId"] == so["lastFreeExcessListId"]
+    compare_scene(g, o, "exhausted")

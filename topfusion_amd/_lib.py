@@ -1,0 +1,133 @@
+"""ctypes binding of libtfusion_hip.so (the C-ABI declared in include/tfusion_hip.h).
+
+The shared library is built in-tree by topfusion_amd/csrc/Makefile (hipcc, gfx950).
+There is no CPU fallback: if the library is missing, loading fails loudly.
+"""
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtfusion_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tfusion_hip.h")
+
+TF_OK, TF_ICP_FAIL, TF_INVALID_ARG, TF_OOM, TF_HIP_ERROR, TF_NO_DEVICE = range(6)
+
+(TF_BUF_HASH, TF_BUF_VBA, TF_BUF_VISIBLE_IDS, TF_BUF_VISIBLE_TYPE, TF_BUF_RANGE, TF_BUF_RAYCAST, TF_BUF_DISTS,
+ TF_BUF_DEPTH, TF_BUF_CURR_POINTS, TF_BUF_CURR_NORMALS, TF_BUF_PREV_POINTS, TF_BUF_PREV_NORMALS, TF_BUF_GREY) = range(13)
+
+
+class TfParams(ctypes.Structure):
+    """tf_params (include/tfusion_hip.h) == TopFuParams + SceneParams + capacities."""
+    _fields_ = [("cols", ctypes.c_int), ("rows", ctypes.c_int),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("bilateral_sigma_depth", ctypes.c_float), ("bilateral_sigma_spatial", ctypes.c_float),
+                ("bilateral_kernel_size", ctypes.c_int),
+                ("icp_truncate_depth_dist", ctypes.c_float), ("icp_dist_thres", ctypes.c_float),
+                ("icp_angle_thres", ctypes.c_float), ("icp_iter_num", ctypes.c_int * 4),
+                ("mu", ctypes.c_float), ("maxW", ctypes.c_int), ("voxelSize", ctypes.c_float),
+                ("viewFrustum_min", ctypes.c_float), ("viewFrustum_max", ctypes.c_float),
+                ("n_buckets", ctypes.c_int), ("n_excess", ctypes.c_int), ("n_blocks", ctypes.c_int),
+                ("vis_capacity", ctypes.c_int), ("max_render_blocks", ctypes.c_int)]
+
+
+class TfStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries",
+                                            "noTotalBlocks", "frame_counter", "icp_iterations", "icp_ok",
+                                            "n_resets")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class TfError(RuntimeError):
+    def __init__(self, status, where):
+        self.status = status
+        super().__init__(f"{where}: tf_status {status} ({status_string(status)})")
+
+
+_lib = None
+
+
+def header_functions():
+    """Names of every function declared in include/tfusion_hip.h."""
+    src = open(HEADER_PATH).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tf_[a-z0-9_]+)\s*\(", src)))
+
+
+def load():
+    """Load libtfusion_hip.so (no fallback: raises if it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `make -C topfusion_amd/csrc` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    S = ctypes.c_size_t
+    sig = {
+        "tf_device_count": ([ctypes.POINTER(I)], I),
+        "tf_set_device": ([I], I),
+        "tf_status_string": ([I], ctypes.c_char_p),
+        "tf_default_params": ([ctypes.POINTER(TfParams)], I),
+        "tf_create": ([ctypes.POINTER(TfParams), ctypes.POINTER(P)], I),
+        "tf_destroy": ([P], None),
+        "tf_reset": ([P], I),
+        "tf_process_frame": ([P, P, S, P, ctypes.POINTER(TfStats)], I),
+        "tf_process_frame_host": ([P, P, S, P, ctypes.POINTER(TfStats)], I),
+        "tf_process_frames": ([P, P, S, I, P], I),
+        "tf_render_image": ([P, P, S], I),
+        "tf_get_pose": ([P, P], I),
+        "tf_get_stats": ([P, ctypes.POINTER(TfStats)], I),
+        "tf_get_params": ([P, ctypes.POINTER(TfParams)], I),
+        "tf_get_stream": ([P], P),
+        "tf_stage_preprocess": ([P, P, S], I),
+        "tf_stage_preprocess_host": ([P, P, S], I),
+        "tf_stage_icp": ([P, P, ctypes.POINTER(I), ctypes.POINTER(I)], I),
+        "tf_stage_alloc": ([P, P], I),
+        "tf_stage_integrate": ([P, P], I),
+        "tf_stage_expected_depths": ([P, P], I),
+        "tf_stage_raycast": ([P, P, I], I),
+        "tf_stage_icp_maps": ([P, P], I),
+        "tf_stage_render_grey": ([P, P], I),
+        "tf_stage_reset_scene": ([P], I),
+        "tf_stage_swap_pyramids": ([P], I),
+        "tf_buffer_bytes": ([P, I, I, ctypes.POINTER(S)], I),
+        "tf_download": ([P, I, I, P, S], I),
+        "tf_upload": ([P, I, I, P, S], I),
+        "tf_set_pose": ([P, P], I),
+        "tf_set_counters": ([P, I, I, I], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def status_string(s):
+    try:
+        return load().tf_status_string(int(s)).decode()
+    except Exception:
+        return str(s)
+
+
+def check(status, where, allow=(TF_OK,)):
+    if status not in allow:
+        raise TfError(status, where)
+    return status
+
+
+def default_params(**kw):
+    p = TfParams()
+    check(load().tf_default_params(ctypes.byref(p)), "tf_default_params")
+    for k, v in kw.items():
+        if k == "icp_iter_num":
+            for i in range(4):
+                p.icp_iter_num[i] = int(v[i]) if i < len(v) else 0
+        else:
+            setattr(p, k, v)
+    return p

@@ -1,0 +1,581 @@
+// tf_capi.hip -- context management, frame orchestration and the C-ABI of libtfusion_hip.
+//
+// TopFu::operator() (tfusion/src/topfu.cpp:161-330) becomes a fixed sequence of kernels on
+// the context's stream with ONE host synchronisation at the end of the frame (the
+// reference has ~27).  ICP, pose algebra and every counter live on the device
+// (TfDevState); the host only reads the frame's bool + counters back.
+#include "tf_internal.h"
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <new>
+
+#define TF_CHECK(expr)                                   \
+    do {                                                 \
+        hipError_t e_ = (expr);                          \
+        if (e_ != hipSuccess) return tf_from_hip(e_);    \
+    } while (0)
+
+static tf_status tf_from_hip(hipError_t e)
+{
+    if (e == hipSuccess) return TF_OK;
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return TF_OOM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return TF_NO_DEVICE;
+    return TF_HIP_ERROR;
+}
+
+extern "C" const char* tf_status_string(tf_status s)
+{
+    switch (s) {
+    case TF_OK: return "ok";
+    case TF_ICP_FAIL: return "icp failed (scene reset)";
+    case TF_INVALID_ARG: return "invalid argument";
+    case TF_OOM: return "out of device memory";
+    case TF_HIP_ERROR: return "HIP error";
+    case TF_NO_DEVICE: return "no HIP device";
+    }
+    return "unknown";
+}
+
+extern "C" tf_status tf_device_count(int* count)
+{
+    if (!count) return TF_INVALID_ARG;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e == hipErrorNoDevice) { *count = 0; return TF_OK; }
+    if (e != hipSuccess) { *count = 0; return tf_from_hip(e); }
+    *count = n;
+    return TF_OK;
+}
+
+extern "C" tf_status tf_set_device(int device) { return tf_from_hip(hipSetDevice(device)); }
+
+extern "C" tf_status tf_default_params(tf_params* p)
+{   // TopFuParams::default_params (topfu.cpp:12-53) + SceneParams(0.02, 100, 0.005, 0.2, 3.0) (:50)
+    if (!p) return TF_INVALID_ARG;
+    memset(p, 0, sizeof(*p));
+    p->cols = 640; p->rows = 480;
+    p->fx = 504.261f; p->fy = 503.905f; p->cx = 352.457f; p->cy = 272.202f;
+    p->bilateral_sigma_depth = 0.04f;
+    p->bilateral_sigma_spatial = 4.5f;
+    p->bilateral_kernel_size = 7;
+    p->icp_truncate_depth_dist = 2.0f;
+    p->icp_dist_thres = 0.1f;
+    p->icp_angle_thres = 30.f * 0.017453293f;
+    p->icp_iter_num[0] = 10; p->icp_iter_num[1] = 5; p->icp_iter_num[2] = 4; p->icp_iter_num[3] = 0;
+    p->mu = 0.02f; p->maxW = 100; p->voxelSize = 0.005f;
+    p->viewFrustum_min = 0.2f; p->viewFrustum_max = 3.0f;
+    p->n_buckets = 0x100000; p->n_excess = 0x20000; p->n_blocks = 0x10000;
+    p->vis_capacity = 0x40000;
+    p->max_render_blocks = 65536 * 4;
+    return TF_OK;
+}
+
+static bool params_valid(const tf_params* p)
+{
+    if (p->cols <= 0 || p->rows <= 0 || (p->cols % 4) || (p->rows % 4)) return false;
+    if (p->n_buckets <= 0 || (p->n_buckets & (p->n_buckets - 1))) return false;
+    if (p->n_excess <= 0 || p->n_blocks <= 0 || p->vis_capacity <= 0 || p->max_render_blocks <= 0) return false;
+    if ((p->n_buckets + p->n_excess) % 16) return false;
+    if (p->bilateral_kernel_size < 1 || p->bilateral_kernel_size > 7) return false;
+    if (p->voxelSize <= 0 || p->mu <= 0) return false;
+    // steps per pixel ceil(2*|e-s|) with |e-s| ~ 2*mu/(8*voxel) must fit the 6-bit key field
+    if (4.0f * p->mu / (8.0f * p->voxelSize) + 2.0f > 60.0f) return false;
+    if ((double)p->cols * p->rows * 64.0 > 2147483000.0) return false;
+    return true;
+}
+
+static void ctx_free(tf_ctx* c)
+{
+    if (!c) return;
+    void* bufs[] = { c->hash, c->excessList, c->vba, c->allocList, c->allocType, c->winnerKey, c->allocCounts,
+                     c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->raycast, c->grey,
+                     c->blockBox, c->blockZ, c->blockTiles, c->blockKeep, c->depth_in, c->dists, c->icp_partial, c->st };
+    for (void* b : bufs) if (b) (void)hipFree(b);
+    for (int l = 0; l < TF_LEVELS; ++l) {
+        if (c->depth_pyr[l]) (void)hipFree(c->depth_pyr[l]);
+        if (c->curr_pts[l]) (void)hipFree(c->curr_pts[l]);
+        if (c->curr_nrm[l]) (void)hipFree(c->curr_nrm[l]);
+        if (c->prev_pts[l]) (void)hipFree(c->prev_pts[l]);
+        if (c->prev_nrm[l]) (void)hipFree(c->prev_nrm[l]);
+    }
+    if (c->st_host) (void)hipHostFree(c->st_host);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+template <class T>
+static hipError_t dalloc(T** p, size_t bytes)
+{
+    return hipMalloc((void**)p, bytes < 16 ? 16 : bytes);
+}
+
+static tf_status sync_state(tf_ctx* c)
+{
+    TF_CHECK(hipMemcpyAsync(c->st_host, c->st, sizeof(TfDevState), hipMemcpyDeviceToHost, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+// TopFu::reset (topfu.cpp:141-152): pose history -> [I], ResetScene.  The render state
+// (visible list / types / range image) is deliberately left as is, like the reference.
+static tf_status ctx_reset(tf_ctx* c)
+{
+    if (c->frame_counter) c->n_resets++;
+    c->frame_counter = 0;
+    float I[12] = { 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0 };
+    TF_CHECK(hipMemcpyAsync(c->st->pose, I, sizeof(I), hipMemcpyHostToDevice, c->stream));
+    TF_CHECK(tfk_reset_scene(c));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
+{
+    if (!pin || !out) return TF_INVALID_ARG;
+    *out = nullptr;
+    if (!params_valid(pin)) return TF_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return TF_NO_DEVICE;
+    tf_ctx* c = new (std::nothrow) tf_ctx;
+    if (!c) return TF_OOM;
+    memset((void*)c, 0, sizeof(*c));
+    c->p = *pin;
+    hipError_t e = hipGetDevice(&c->device);
+    if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    c->W = pin->cols; c->H = pin->rows;
+    c->n_total = pin->n_buckets + pin->n_excess;
+    for (int l = 0, w = c->W, h = c->H; l < TF_LEVELS; ++l, w /= 2, h /= 2) { c->lw[l] = w; c->lh[l] = h; }
+    c->alloc_chunks = (c->n_total + 4095) / 4096;
+    c->vis_chunks = c->alloc_chunks;
+    const size_t npx = (size_t)c->W * c->H;
+    const size_t ntot_pad = (size_t)c->alloc_chunks * 4096;
+    c->icp_max_cta = ((c->W + 31) / 32) * ((c->H + 7) / 8);
+    // ComputeIcpHelper ctor (projective_icp.cpp:11-15), evaluated on the host like the reference
+    c->min_cosine = cosf(pin->icp_angle_thres);
+    c->dist2_thres = pin->icp_dist_thres * pin->icp_dist_thres;
+#define ALLOC(ptr, bytes) do { e = dalloc(&(ptr), (bytes)); if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); } } while (0)
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    ALLOC(c->hash, sizeof(TfHashEntry) * (size_t)c->n_total);
+    ALLOC(c->excessList, sizeof(int) * (size_t)pin->n_excess);
+    ALLOC(c->vba, sizeof(TfVoxel) * (size_t)pin->n_blocks * TF_BLK3);
+    ALLOC(c->allocList, sizeof(int) * (size_t)pin->n_blocks);
+    ALLOC(c->allocType, ntot_pad);
+    ALLOC(c->winnerKey, sizeof(int) * ntot_pad);
+    ALLOC(c->allocCounts, sizeof(int) * 2 * (size_t)c->alloc_chunks);
+    ALLOC(c->requestList, sizeof(int) * (size_t)c->n_total);
+    ALLOC(c->visCounts, sizeof(int) * (size_t)c->vis_chunks);
+    ALLOC(c->visibleIds, sizeof(int) * (size_t)pin->vis_capacity);
+    ALLOC(c->visType, ntot_pad);
+    ALLOC(c->range, sizeof(float) * 2 * npx);
+    ALLOC(c->raycast, sizeof(float) * 4 * npx);
+    ALLOC(c->grey, sizeof(uchar4) * npx);
+    ALLOC(c->blockBox, sizeof(int4) * (size_t)pin->vis_capacity);
+    ALLOC(c->blockZ, sizeof(float2) * (size_t)pin->vis_capacity);
+    ALLOC(c->blockTiles, sizeof(int) * (size_t)pin->vis_capacity);
+    ALLOC(c->blockKeep, (size_t)pin->vis_capacity);
+    ALLOC(c->depth_in, sizeof(uint16_t) * npx);
+    ALLOC(c->dists, sizeof(float) * npx);
+    for (int l = 0; l < TF_LEVELS; ++l) {
+        size_t n = (size_t)c->lw[l] * c->lh[l];
+        ALLOC(c->depth_pyr[l], sizeof(uint16_t) * n);
+        ALLOC(c->curr_pts[l], sizeof(float4) * n);
+        ALLOC(c->curr_nrm[l], sizeof(float4) * n);
+        ALLOC(c->prev_pts[l], sizeof(float4) * n);
+        ALLOC(c->prev_nrm[l], sizeof(float4) * n);
+    }
+    ALLOC(c->icp_partial, sizeof(float) * 28 * (size_t)c->icp_max_cta);
+    ALLOC(c->st, sizeof(TfDevState));
+#undef ALLOC
+    e = hipHostMalloc((void**)&c->st_host, sizeof(TfDevState), hipHostMallocDefault);
+    if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    // initial device state
+    TfDevState s0;
+    memset(&s0, 0, sizeof(s0));
+    for (int i = 0; i < 12; ++i) s0.pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+    s0.icp_ok = 1;
+    e = hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->allocType, 0, ntot_pad, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->winnerKey, 0xff, sizeof(int) * ntot_pad, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->visType, 0, ntot_pad, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->visibleIds, 0, sizeof(int) * (size_t)pin->vis_capacity, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->raycast, 0, sizeof(float) * 4 * npx, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->grey, 0, sizeof(uchar4) * npx, c->stream);
+    for (int l = 0; l < TF_LEVELS && e == hipSuccess; ++l) {
+        size_t n = (size_t)c->lw[l] * c->lh[l];
+        e = hipMemsetAsync(c->prev_pts[l], 0, sizeof(float4) * n, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(c->prev_nrm[l], 0, sizeof(float4) * n, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(c->curr_pts[l], 0, sizeof(float4) * n, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(c->curr_nrm[l], 0, sizeof(float4) * n, c->stream);
+    }
+    if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    {   // RenderState ctor: renderingRangeImage = (viewFrustum_min, viewFrustum_max) (RenderState.hpp:56-76)
+        float2* tmp = (float2*)malloc(sizeof(float2) * npx);
+        if (!tmp) { ctx_free(c); return TF_OOM; }
+        for (size_t i = 0; i < npx; ++i) tmp[i] = make_float2(pin->viewFrustum_min, pin->viewFrustum_max);
+        e = hipMemcpy(c->range, tmp, sizeof(float2) * npx, hipMemcpyHostToDevice);
+        free(tmp);
+        if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    }
+    e = tfk_reset_scene(c);                              // topfu.cpp:75
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    *out = c;
+    return TF_OK;
+}
+
+extern "C" void tf_destroy(tf_ctx* c)
+{
+    if (!c) return;
+    (void)hipStreamSynchronize(c->stream);
+    ctx_free(c);
+}
+
+extern "C" tf_status tf_reset(tf_ctx* c)
+{
+    if (!c) return TF_INVALID_ARG;
+    return ctx_reset(c);
+}
+
+static hipError_t clear_abort(tf_ctx* c)
+{
+    return hipMemsetAsync(&c->st->abort, 0, sizeof(int), c->stream);
+}
+
+static void swap_pyramids(tf_ctx* c)
+{
+    for (int l = 0; l < TF_LEVELS; ++l) {
+        float4* t = c->curr_pts[l]; c->curr_pts[l] = c->prev_pts[l]; c->prev_pts[l] = t;
+        t = c->curr_nrm[l]; c->curr_nrm[l] = c->prev_nrm[l]; c->prev_nrm[l] = t;
+    }
+}
+
+// enqueue one TopFu::operator() frame; returns whether the frame took the tracking path
+static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, bool* tracked)
+{
+    TF_CHECK(clear_abort(c));
+    TF_CHECK(tfk_preprocess(c, depth, pitch));                       // topfu.cpp:166-197
+    if (c->frame_counter == 0) {                                     // topfu.cpp:200-209
+        TF_CHECK(tfk_frame0_matrices(c));
+        TF_CHECK(tfk_alloc(c));
+        TF_CHECK(tfk_integrate(c));
+        swap_pyramids(c);
+        *tracked = false;
+        return TF_OK;
+    }
+    TF_CHECK(tfk_icp(c, 1));                                         // topfu.cpp:242-243
+    TF_CHECK(tfk_alloc(c));                                          // topfu.cpp:281
+    TF_CHECK(tfk_integrate(c));                                      // topfu.cpp:282
+    TF_CHECK(tfk_raycast(c, 0));                                     // renderImage, topfu.cpp:284-285
+    TF_CHECK(tfk_render_grey(c));
+    TF_CHECK(tfk_expected_depths(c));                                // topfu.cpp:306
+    TF_CHECK(tfk_raycast(c, 1));                                     // CreateICPMaps, topfu.cpp:307
+    TF_CHECK(tfk_icp_maps(c));                                       // + resizePointsNormals :308-309
+    *tracked = true;
+    return TF_OK;
+}
+
+static tf_status finish_frame(tf_ctx* c, bool tracked)
+{
+    tf_status s = sync_state(c);
+    if (s != TF_OK) return s;
+    if (tracked && !c->st_host->icp_ok) {                            // topfu.cpp:263-264
+        s = ctx_reset(c);
+        if (s != TF_OK) return s;
+        return TF_ICP_FAIL;
+    }
+    c->frame_counter++;
+    return TF_OK;
+}
+
+static void fill_stats(tf_ctx* c, tf_stats* st)
+{
+    if (!st) return;
+    const TfDevState* d = c->st_host;
+    st->lastFreeBlockId = d->lastFreeBlockId;
+    st->lastFreeExcessListId = d->lastFreeExcessListId;
+    st->noVisibleEntries = d->noVisibleEntries;
+    st->noTotalBlocks = d->noTotalBlocks;
+    st->frame_counter = c->frame_counter;
+    st->icp_iterations = d->icp_iters;
+    st->icp_ok = d->icp_ok;
+    st->n_resets = c->n_resets;
+}
+
+extern "C" tf_status tf_process_frame(tf_ctx* c, const uint16_t* dev_depth, size_t pitch, float pose_out[12],
+                                      tf_stats* stats)
+{
+    if (!c || !dev_depth) return TF_INVALID_ARG;
+    if (pitch == 0) pitch = (size_t)c->W * 2;
+    bool tracked = false;
+    tf_status s = enqueue_frame(c, dev_depth, pitch, &tracked);
+    if (s != TF_OK) return s;
+    s = finish_frame(c, tracked);
+    if (s != TF_OK && s != TF_ICP_FAIL) return s;
+    if (s == TF_ICP_FAIL) {
+        tf_status s2 = sync_state(c);
+        if (s2 != TF_OK) return s2;
+        c->st_host->icp_ok = 0;
+    }
+    if (pose_out) memcpy(pose_out, c->st_host->pose, sizeof(float) * 12);
+    fill_stats(c, stats);
+    return s;
+}
+
+extern "C" tf_status tf_process_frame_host(tf_ctx* c, const uint16_t* host_depth, size_t pitch, float pose_out[12],
+                                           tf_stats* stats)
+{
+    if (!c || !host_depth) return TF_INVALID_ARG;
+    if (pitch == 0) pitch = (size_t)c->W * 2;
+    TF_CHECK(hipMemcpy2DAsync(c->depth_in, (size_t)c->W * 2, host_depth, pitch, (size_t)c->W * 2, c->H,
+                              hipMemcpyHostToDevice, c->stream));
+    return tf_process_frame(c, c->depth_in, (size_t)c->W * 2, pose_out, stats);
+}
+
+extern "C" tf_status tf_process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t stride, int n, int* ok_out)
+{
+    if (!c || !dev_frames || n < 0) return TF_INVALID_ARG;
+    for (int i = 0; i < n; ++i) {
+        const uint16_t* f = (const uint16_t*)((const char*)dev_frames + (size_t)i * stride);
+        tf_status s = tf_process_frame(c, f, (size_t)c->W * 2, nullptr, nullptr);
+        if (s != TF_OK && s != TF_ICP_FAIL) return s;
+        if (ok_out) ok_out[i] = (s == TF_OK);
+    }
+    return TF_OK;
+}
+
+extern "C" tf_status tf_render_image(tf_ctx* c, uint8_t* dev_rgba, size_t pitch)
+{   // TopFu::renderImage: raycast from poses_.back() with the current range image + grey
+    if (!c) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));
+    TF_CHECK(hipMemcpyAsync(c->st->pose_in, c->st->pose, sizeof(float) * 12, hipMemcpyDeviceToDevice, c->stream));
+    TF_CHECK(tfk_pose_from_input(c, 0));
+    TF_CHECK(tfk_raycast(c, 0));
+    TF_CHECK(tfk_render_grey(c));
+    if (dev_rgba) {
+        if (pitch == 0) pitch = (size_t)c->W * 4;
+        TF_CHECK(hipMemcpy2DAsync(dev_rgba, pitch, c->grey, (size_t)c->W * 4, (size_t)c->W * 4, c->H,
+                                  hipMemcpyDeviceToDevice, c->stream));
+    }
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_get_pose(tf_ctx* c, float rt[12])
+{
+    if (!c || !rt) return TF_INVALID_ARG;
+    tf_status s = sync_state(c);
+    if (s != TF_OK) return s;
+    memcpy(rt, c->st_host->pose, sizeof(float) * 12);
+    return TF_OK;
+}
+
+extern "C" tf_status tf_get_stats(tf_ctx* c, tf_stats* stats)
+{
+    if (!c || !stats) return TF_INVALID_ARG;
+    tf_status s = sync_state(c);
+    if (s != TF_OK) return s;
+    fill_stats(c, stats);
+    return TF_OK;
+}
+
+extern "C" tf_status tf_get_params(tf_ctx* c, tf_params* p)
+{
+    if (!c || !p) return TF_INVALID_ARG;
+    *p = c->p;
+    return TF_OK;
+}
+
+extern "C" void* tf_get_stream(tf_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+// ---- stage entry points ---------------------------------------------------------------
+static tf_status set_pose_in(tf_ctx* c, const float* rt, int mode)
+{
+    TF_CHECK(clear_abort(c));
+    TF_CHECK(hipMemcpyAsync(c->st->pose_in, rt, sizeof(float) * 12, hipMemcpyHostToDevice, c->stream));
+    TF_CHECK(tfk_pose_from_input(c, mode));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_preprocess(tf_ctx* c, const uint16_t* dev_depth, size_t pitch)
+{
+    if (!c || !dev_depth) return TF_INVALID_ARG;
+    if (pitch == 0) pitch = (size_t)c->W * 2;
+    TF_CHECK(clear_abort(c));
+    TF_CHECK(tfk_preprocess(c, dev_depth, pitch));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_preprocess_host(tf_ctx* c, const uint16_t* host_depth, size_t pitch)
+{
+    if (!c || !host_depth) return TF_INVALID_ARG;
+    if (pitch == 0) pitch = (size_t)c->W * 2;
+    TF_CHECK(hipMemcpy2DAsync(c->depth_in, (size_t)c->W * 2, host_depth, pitch, (size_t)c->W * 2, c->H,
+                              hipMemcpyHostToDevice, c->stream));
+    return tf_stage_preprocess(c, c->depth_in, (size_t)c->W * 2);
+}
+
+extern "C" tf_status tf_stage_icp(tf_ctx* c, float affine_rt[12], int* ok, int* iterations)
+{
+    if (!c) return TF_INVALID_ARG;
+    TF_CHECK(tfk_icp(c, 0));
+    tf_status s = sync_state(c);
+    if (s != TF_OK) return s;
+    if (affine_rt) memcpy(affine_rt, c->st_host->affine, sizeof(float) * 12);
+    if (ok) *ok = c->st_host->icp_ok;
+    if (iterations) *iterations = c->st_host->icp_iters;
+    TF_CHECK(clear_abort(c));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_alloc(tf_ctx* c, const float pose_rt[12])
+{
+    if (!c || !pose_rt) return TF_INVALID_ARG;
+    tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
+    if (s != TF_OK) return s;
+    TF_CHECK(tfk_alloc(c));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_integrate(tf_ctx* c, const float pose_rt[12])
+{
+    if (!c || !pose_rt) return TF_INVALID_ARG;
+    tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
+    if (s != TF_OK) return s;
+    TF_CHECK(tfk_integrate(c));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_expected_depths(tf_ctx* c, const float pose_rt[12])
+{
+    if (!c || !pose_rt) return TF_INVALID_ARG;
+    tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
+    if (s != TF_OK) return s;
+    TF_CHECK(tfk_expected_depths(c));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_raycast(tf_ctx* c, const float invM_rt[12], int update_visible)
+{
+    if (!c || !invM_rt) return TF_INVALID_ARG;
+    tf_status s = set_pose_in(c, invM_rt, 0);
+    if (s != TF_OK) return s;
+    TF_CHECK(tfk_raycast(c, update_visible));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_icp_maps(tf_ctx* c, const float invM_rt[12])
+{
+    if (!c || !invM_rt) return TF_INVALID_ARG;
+    tf_status s = set_pose_in(c, invM_rt, 0);
+    if (s != TF_OK) return s;
+    TF_CHECK(tfk_icp_maps(c));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
+{
+    if (!c || !invM_rt) return TF_INVALID_ARG;
+    tf_status s = set_pose_in(c, invM_rt, 0);
+    if (s != TF_OK) return s;
+    TF_CHECK(tfk_render_grey(c));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_reset_scene(tf_ctx* c)
+{
+    if (!c) return TF_INVALID_ARG;
+    TF_CHECK(tfk_reset_scene(c));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_stage_swap_pyramids(tf_ctx* c)
+{
+    if (!c) return TF_INVALID_ARG;
+    swap_pyramids(c);
+    return TF_OK;
+}
+
+// ---- state transfer -------------------------------------------------------------------
+static void* buffer_ptr(tf_ctx* c, int which, int level, size_t* bytes)
+{
+    const size_t npx = (size_t)c->W * c->H;
+    if (level < 0 || level >= TF_LEVELS) level = 0;
+    const size_t nl = (size_t)c->lw[level] * c->lh[level];
+    switch (which) {
+    case TF_BUF_HASH: *bytes = sizeof(TfHashEntry) * (size_t)c->n_total; return c->hash;
+    case TF_BUF_VBA: *bytes = sizeof(TfVoxel) * (size_t)c->p.n_blocks * TF_BLK3; return c->vba;
+    case TF_BUF_VISIBLE_IDS: *bytes = sizeof(int) * (size_t)c->p.vis_capacity; return c->visibleIds;
+    case TF_BUF_VISIBLE_TYPE: *bytes = (size_t)c->n_total; return c->visType;
+    case TF_BUF_RANGE: *bytes = sizeof(float) * 2 * npx; return c->range;
+    case TF_BUF_RAYCAST: *bytes = sizeof(float) * 4 * npx; return c->raycast;
+    case TF_BUF_DISTS: *bytes = sizeof(float) * npx; return c->dists;
+    case TF_BUF_DEPTH: *bytes = sizeof(uint16_t) * nl; return c->depth_pyr[level];
+    case TF_BUF_CURR_POINTS: *bytes = sizeof(float4) * nl; return c->curr_pts[level];
+    case TF_BUF_CURR_NORMALS: *bytes = sizeof(float4) * nl; return c->curr_nrm[level];
+    case TF_BUF_PREV_POINTS: *bytes = sizeof(float4) * nl; return c->prev_pts[level];
+    case TF_BUF_PREV_NORMALS: *bytes = sizeof(float4) * nl; return c->prev_nrm[level];
+    case TF_BUF_GREY: *bytes = sizeof(uchar4) * npx; return c->grey;
+    }
+    *bytes = 0;
+    return nullptr;
+}
+
+extern "C" tf_status tf_buffer_bytes(tf_ctx* c, int which, int level, size_t* bytes)
+{
+    if (!c || !bytes) return TF_INVALID_ARG;
+    return buffer_ptr(c, which, level, bytes) ? TF_OK : TF_INVALID_ARG;
+}
+
+extern "C" tf_status tf_download(tf_ctx* c, int which, int level, void* host, size_t bytes)
+{
+    if (!c || !host) return TF_INVALID_ARG;
+    size_t n;
+    void* p = buffer_ptr(c, which, level, &n);
+    if (!p || n != bytes) return TF_INVALID_ARG;
+    TF_CHECK(hipMemcpyAsync(host, p, n, hipMemcpyDeviceToHost, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host, size_t bytes)
+{
+    if (!c || !host) return TF_INVALID_ARG;
+    size_t n;
+    void* p = buffer_ptr(c, which, level, &n);
+    if (!p || n != bytes) return TF_INVALID_ARG;
+    TF_CHECK(hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_set_pose(tf_ctx* c, const float rt[12])
+{
+    if (!c || !rt) return TF_INVALID_ARG;
+    TF_CHECK(hipMemcpyAsync(c->st->pose, rt, sizeof(float) * 12, hipMemcpyHostToDevice, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_set_counters(tf_ctx* c, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries)
+{
+    if (!c) return TF_INVALID_ARG;
+    tf_status s = sync_state(c);
+    if (s != TF_OK) return s;
+    c->st_host->lastFreeBlockId = lastFreeBlockId;
+    c->st_host->lastFreeExcessListId = lastFreeExcessListId;
+    c->st_host->noVisibleEntries = noVisibleEntries;
+    TF_CHECK(hipMemcpyAsync(c->st, c->st_host, sizeof(TfDevState), hipMemcpyHostToDevice, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}

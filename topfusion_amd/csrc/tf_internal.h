@@ -1,0 +1,207 @@
+// tf_internal.h -- shared definitions of libtfusion_hip (gfx950).
+//
+// Numerics are "canonical" (see DESIGN.md §Numerics): every kernel is compiled with
+// -ffp-contract=off and IEEE-correct f32 division/sqrt, fmaf() is written exactly where
+// the reference writes __fmaf_rn, and the reference's fast intrinsics (__expf, rsqrt,
+// __fdividef) are replaced by fixed IEEE sequences, so each stage is bit-reproducible
+// against the CPU oracle (oracle/tf_oracle.c, test infrastructure only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/tfusion_hip.h"
+
+#define TF_BLK 8        // SDF_BLOCK_SIZE (VoxelBlockHash.hpp:10)
+#define TF_BLK3 512     // SDF_BLOCK_SIZE3
+#define TF_FAR_AWAY 999999.9f   // VisualisationEngine_Shared.hpp:18
+#define TF_VERY_CLOSE 0.05f     // VisualisationEngine_Shared.hpp:22
+#define TF_SUBSAMPLE 8          // minmaximg_subsample (VisualisationEngine_Shared.hpp:7)
+#define TF_RB_SIZE 16           // renderingBlockSizeX/Y (VisualisationEngine_Shared.hpp:25-26)
+#define TF_LEVELS 3
+
+// HashEntry, VoxelBlockHash.hpp:32-44 (16 B; one dwordx4 probe)
+struct __attribute__((aligned(16))) TfHashEntry {
+    short x, y, z, pad;
+    int offset;
+    int ptr;
+};
+// Voxel_s, VoxelTypes.hpp:69-92 (4 B)
+struct __attribute__((aligned(4))) TfVoxel {
+    short sdf;
+    unsigned char w;
+    unsigned char pad;
+};
+
+// Per-context device state: everything the frame's kernels exchange, so that a frame is a
+// fixed kernel sequence with no host round trip (graph-capturable).
+struct TfDevState {
+    float pose[12];          // poses_.back(), camera->world, row-major [R|t]
+    float affine[12];        // ICP working transform
+    float pose_in[12];       // explicit pose for stage entry points
+    float M_alloc[16];       // Matrix4f of the world->camera pose (column-major m[4c+r])
+    float invM_alloc[16];    // Matrix4::inv(M_alloc) (SceneReconstructionEngine_host.cu:102-103)
+    float M_ray[16];         // Matrix4f(pose) camera->world, raycast invM
+    float sums[27];          // last ICP A|b
+    int icp_ok;              // estimateTransform result
+    int icp_iters;           // iterations executed
+    int abort;               // set by ICP failure: remaining kernels of the frame no-op
+    int lastFreeBlockId;     // LocalVBA::lastFreeBlockId
+    int lastFreeExcessListId;
+    int noVisibleEntries;
+    int noTotalBlocks;
+    int alloc_exhausted;     // capacity exhausted this frame -> serial allocation
+    unsigned tiles_total;    // rendering tiles requested (before the MAX cap)
+    int pad_[3];
+};
+
+// ---------------------------------------------------------------------------------------
+// canonical device math
+// ---------------------------------------------------------------------------------------
+// replacement for __expf (imgproc.cu:40): 2^(x log2 e), exact range reduction + Horner
+__device__ __forceinline__ float tf_exp(float x)
+{
+    float t = x * 1.44269504088896341f;
+    if (!(t > -125.0f)) return 0.0f;
+    if (t >= 128.0f) return __builtin_inff();
+    float k = rintf(t);
+    float f = t - k;
+    float p = 1.5403530393381606e-4f;
+    p = fmaf(p, f, 1.3333558146428443e-3f);
+    p = fmaf(p, f, 9.6181291076284772e-3f);
+    p = fmaf(p, f, 5.5504108664821580e-2f);
+    p = fmaf(p, f, 2.4022650695910071e-1f);
+    p = fmaf(p, f, 6.9314718055994531e-1f);
+    p = fmaf(p, f, 1.0f);
+    return ldexpf(p, (int)k);
+}
+
+struct tf3 { float x, y, z; };
+__device__ __forceinline__ tf3 mk3(float x, float y, float z) { tf3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ tf3 sub3(tf3 a, tf3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+// dot with __fmaf_rn (src/cuda/device.hpp:26-29)
+__device__ __forceinline__ float kdot(tf3 a, tf3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
+__device__ __forceinline__ tf3 kcross(tf3 a, tf3 b)
+{
+    return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+// normalized(): v * rsqrt(dot(v,v)) (device.hpp:100-103), rsqrt -> 1/sqrtf
+__device__ __forceinline__ tf3 knormalized(tf3 v)
+{
+    float s = 1.0f / sqrtf(kdot(v, v));
+    return mk3(v.x * s, v.y * s, v.z * s);
+}
+
+// Matrix4f * Vector4f (Matrix.hpp:126-133), column-major m[4c+r]
+__device__ __forceinline__ void tf_m4v(const float* m, float v0, float v1, float v2, float v3, float* r)
+{
+    r[0] = m[0] * v0 + m[4] * v1 + m[8] * v2 + m[12] * v3;
+    r[1] = m[1] * v0 + m[5] * v1 + m[9] * v2 + m[13] * v3;
+    r[2] = m[2] * v0 + m[6] * v1 + m[10] * v2 + m[14] * v3;
+    r[3] = m[3] * v0 + m[7] * v1 + m[11] * v2 + m[15] * v3;
+}
+__device__ __forceinline__ void tf_m4v3(const float* m, float v0, float v1, float v2, float v3, float* r)
+{
+    r[0] = m[0] * v0 + m[4] * v1 + m[8] * v2 + m[12] * v3;
+    r[1] = m[1] * v0 + m[5] * v1 + m[9] * v2 + m[13] * v3;
+    r[2] = m[2] * v0 + m[6] * v1 + m[10] * v2 + m[14] * v3;
+}
+
+// Matrix4f(pose(0,0), pose(1,0), ...) (topfu.cpp:246-249): m[4c+r] = P[r][c]
+__device__ __forceinline__ void tf_rt_to_m4(const float* rt, float* m)
+{
+    for (int c = 0; c < 4; ++c) {
+        for (int r = 0; r < 3; ++r) m[4 * c + r] = rt[r * 4 + c];
+        m[4 * c + 3] = (c == 3) ? 1.0f : 0.0f;
+    }
+}
+
+// hashIndex (RepresentationAccess.hpp:5-7)
+__device__ __forceinline__ int tf_hash_index(int x, int y, int z, unsigned mask)
+{
+    return (int)((((unsigned)x * 73856093u) ^ ((unsigned)y * 19349669u) ^ ((unsigned)z * 83492791u)) & mask);
+}
+
+__device__ __forceinline__ float tf_qnan() { return __int_as_float(0x7fffffff); }
+
+// wave64 butterfly sum that reproduces the reference's halving tree bit for bit
+// (temp_utils.hpp:503-523 for lanes 0..63 after the cross-wave steps)
+__device__ __forceinline__ float tf_wave_tree64(float b)
+{
+    b = b + __shfl_xor(b, 32, 64);
+    b = b + __shfl_xor(b, 16, 64);
+    b = b + __shfl_xor(b, 8, 64);
+    b = b + __shfl_xor(b, 4, 64);
+    b = b + __shfl_xor(b, 2, 64);
+    b = b + __shfl_xor(b, 1, 64);
+    return b;
+}
+
+// ---------------------------------------------------------------------------------------
+// host-side context
+// ---------------------------------------------------------------------------------------
+struct tf_ctx {
+    tf_params p;
+    int device;
+    hipStream_t stream;
+    int n_total;
+    int W, H;
+    int lw[TF_LEVELS], lh[TF_LEVELS];
+    // scene (Scene<Voxel_s,VoxelBlockHash>, scene.hpp:13-44)
+    TfHashEntry* hash;
+    int* excessList;
+    TfVoxel* vba;
+    int* allocList;
+    // SceneReconstructionEngine temporaries
+    unsigned char* allocType;
+    int* winnerKey;          // per-entry last-writer key (pixel*64+step), replaces blockCoords races
+    int* allocCounts;        // per-chunk counts (2 ints per chunk)
+    int* requestList;        // ordered request indices
+    int* visCounts;
+    // RenderState_VH
+    int* visibleIds;
+    unsigned char* visType;
+    float* range;            // float2
+    float* raycast;          // float4
+    uchar4* grey;
+    // expected-depths scratch
+    int4* blockBox;          // per visible entry: ulx, uly, lrx, lry (ulx < 0 -> invalid)
+    float2* blockZ;
+    int* blockTiles;
+    unsigned char* blockKeep;
+    // frame buffers
+    uint16_t* depth_in;      // staging for host uploads / pitched input
+    float* dists;
+    uint16_t* depth_pyr[TF_LEVELS];
+    float4* curr_pts[TF_LEVELS];
+    float4* curr_nrm[TF_LEVELS];
+    float4* prev_pts[TF_LEVELS];
+    float4* prev_nrm[TF_LEVELS];
+    // ICP
+    float* icp_partial;      // [27][max CTAs]
+    int icp_max_cta;
+    float min_cosine, dist2_thres;
+    // device state
+    TfDevState* st;
+    TfDevState* st_host;     // pinned mirror
+    int frame_counter;       // host mirror of TopFu::frame_counter_
+    int n_resets;
+    int alloc_chunks;        // N_tot / 4096
+    int vis_chunks;
+};
+
+// ---------------------------------------------------------------------------------------
+// launchers (one per kernel family); all enqueue on ctx->stream
+// ---------------------------------------------------------------------------------------
+hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch);
+hipError_t tfk_icp(tf_ctx* c, int pose_update);
+hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / raycast matrices
+hipError_t tfk_reset_scene(tf_ctx* c);
+hipError_t tfk_alloc(tf_ctx* c);
+hipError_t tfk_integrate(tf_ctx* c);
+hipError_t tfk_raycast(tf_ctx* c, int update_visible);
+hipError_t tfk_render_grey(tf_ctx* c);
+hipError_t tfk_icp_maps(tf_ctx* c);
+hipError_t tfk_expected_depths(tf_ctx* c);
+hipError_t tfk_frame0_matrices(tf_ctx* c);
+
+enum { TF_POSE_ALLOC = 1, TF_POSE_RAY = 2, TF_POSE_ALLOC_NOINV = 4 };

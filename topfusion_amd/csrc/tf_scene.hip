@@ -1,0 +1,534 @@
+// tf_scene.hip -- voxel-block hash allocation, visible list and TSDF integration
+//  for gfx950.
+//
+// The reference resolves its data races by "last writer wins" and hands out blocks in
+// atomicSub order (SceneReconstructionEngine.hpp:287-292, SceneReconstructionEngine_host.cu:
+// 350-479).  Here every decision is deterministic and equal to the serial order:
+//   * allocation requests: per-entry atomicMax of key = pixel*64 + step (raster order,
+//     last writer wins); the winning block position is recomputed from the key;
+//   * block / excess slots: ordered by hash index through a two-pass chunked scan
+//     (exact serial semantics, including capacity exhaustion, via a one-wave fallback);
+//   * visible list: ordered compaction by hash index.
+#include "tf_internal.h"
+
+#define CHUNK 4096          // hash entries per workgroup in the scan passes (256 thr x 16)
+
+// byte i (0..15) of a 16-byte group held as two 64-bit words (no dynamic register indexing)
+__device__ __forceinline__ unsigned byte16(unsigned long long lo, unsigned long long hi, int i)
+{
+    return (unsigned)(((i < 8) ? (lo >> (8 * i)) : (hi >> (8 * (i - 8)))) & 0xffull);
+}
+__device__ __forceinline__ void load16(const unsigned char* p, unsigned long long* lo, unsigned long long* hi)
+{
+    uint4 v = *(const uint4*)p;
+    *lo = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+    *hi = (unsigned long long)v.z | ((unsigned long long)v.w << 32);
+}
+
+// ---------------------------------------------------------------------------------------
+// ResetScene (SceneReconstructionEngine_host.cu:51-73)
+// ---------------------------------------------------------------------------------------
+__global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_blocks, TfHashEntry* hash,
+                              int n_total, int* excessList, int n_excess, TfDevState* st)
+{
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    uint4 vfill = make_uint4(32767u, 32767u, 32767u, 32767u);   // Voxel_s(): sdf 32767, w 0
+    uint4* v4 = (uint4*)vba;
+    for (size_t i = tid; i < n_vox / 4; i += stride) v4[i] = vfill;
+    for (size_t i = tid; i < (size_t)n_blocks; i += stride) allocList[i] = (int)i;
+    TfHashEntry e; e.x = e.y = e.z = e.pad = 0; e.offset = 0; e.ptr = -2;
+    for (size_t i = tid; i < (size_t)n_total; i += stride) hash[i] = e;
+    for (size_t i = tid; i < (size_t)n_excess; i += stride) excessList[i] = (int)i;
+    if (tid == 0) {
+        st->lastFreeBlockId = n_blocks - 1;
+        st->lastFreeExcessListId = n_excess - 1;
+    }
+}
+
+hipError_t tfk_reset_scene(tf_ctx* c)
+{
+    hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, c->vba, (size_t)c->p.n_blocks * TF_BLK3,
+                       c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// buildHashAllocAndVisibleTypePP (SceneReconstructionEngine.hpp:206-298)
+// ---------------------------------------------------------------------------------------
+struct AllocArgs {
+    const float* dists;
+    int W, H;
+    float invfx, invfy, cx, cy;        // invProjParams_d (SceneReconstructionEngine_host.cu:110-113)
+    float mu, oneOverVoxelSize;        // 1/(voxelSize*8)
+    float vf_min, vf_max;
+    unsigned mask;
+    int n_buckets;
+};
+
+// ray segment [d-mu, d+mu] of pixel (x,y) in block units; false if the pixel is skipped
+__device__ __forceinline__ bool alloc_segment(const AllocArgs& a, const float* invM, int x, int y,
+                                              float* point, float* dir, int* noSteps)
+{
+    float depth_measure = a.dists[x + y * a.W];
+    if (depth_measure <= 0 || (depth_measure - a.mu) < 0 || (depth_measure - a.mu) < a.vf_min ||
+        (depth_measure + a.mu) > a.vf_max) return false;
+    float pcz = depth_measure;
+    float pcx = pcz * (((float)x - a.cx) * a.invfx);
+    float pcy = pcz * (((float)y - a.cy) * a.invfy);
+    float norm = sqrtf(pcx * pcx + pcy * pcy + pcz * pcz);
+    float r[3], pe[3];
+    float s1 = 1.0f - a.mu / norm;
+    tf_m4v3(invM, pcx * s1, pcy * s1, pcz * s1, 1.0f, r);
+    point[0] = r[0] * a.oneOverVoxelSize; point[1] = r[1] * a.oneOverVoxelSize; point[2] = r[2] * a.oneOverVoxelSize;
+    float s2 = 1.0f + a.mu / norm;
+    tf_m4v3(invM, pcx * s2, pcy * s2, pcz * s2, 1.0f, r);
+    pe[0] = r[0] * a.oneOverVoxelSize; pe[1] = r[1] * a.oneOverVoxelSize; pe[2] = r[2] * a.oneOverVoxelSize;
+    dir[0] = pe[0] - point[0]; dir[1] = pe[1] - point[1]; dir[2] = pe[2] - point[2];
+    norm = sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
+    int n = (int)ceilf(2.0f * norm);
+    float dv = (float)(n - 1);
+    dir[0] /= dv; dir[1] /= dv; dir[2] /= dv;
+    *noSteps = n;
+    return true;
+}
+
+__global__ void __launch_bounds__(256)
+k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+                 unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType, int* __restrict__ winnerKey)
+{
+    if (st->abort) return;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.W || y >= a.H) return;
+    float point[3], dir[3]; int noSteps;
+    if (!alloc_segment(a, st->invM_alloc, x, y, point, dir, &noSteps)) return;
+    const int key0 = (y * a.W + x) * 64;
+    for (int i = 0; i < noSteps; i++) {
+        int bx = (short)floorf(point[0]), by = (short)floorf(point[1]), bz = (short)floorf(point[2]);
+        int hashIdx = tf_hash_index(bx, by, bz, a.mask);
+        TfHashEntry e = hash[hashIdx];
+        bool found = false;
+        if (e.x == bx && e.y == by && e.z == bz && e.ptr >= -1) {
+            visType[hashIdx] = (e.ptr == -1) ? 2 : 1;
+            found = true;
+        }
+        if (!found) {
+            bool isExcess = false;
+            if (e.ptr >= -1) {
+                while (e.offset >= 1) {
+                    hashIdx = a.n_buckets + e.offset - 1;
+                    e = hash[hashIdx];
+                    if (e.x == bx && e.y == by && e.z == bz && e.ptr >= -1) {
+                        visType[hashIdx] = (e.ptr == -1) ? 2 : 1;
+                        found = true;
+                        break;
+                    }
+                }
+                isExcess = true;
+            }
+            if (!found) {
+                allocType[hashIdx] = isExcess ? 2 : 1;
+                if (!isExcess) visType[hashIdx] = 1;
+                atomicMax(&winnerKey[hashIdx], key0 + i);   // raster-order last writer
+            }
+        }
+        point[0] += dir[0]; point[1] += dir[1]; point[2] += dir[2];
+    }
+}
+
+// recompute the block position written by request `key` (blockCoords in the reference)
+__device__ __forceinline__ void alloc_block_from_key(const AllocArgs& a, const float* invM, int key, short* pos)
+{
+    int pix = key >> 6, step = key & 63;
+    int x = pix % a.W, y = pix / a.W;
+    float point[3], dir[3]; int noSteps;
+    alloc_segment(a, invM, x, y, point, dir, &noSteps);
+    for (int i = 0; i < step; ++i) { point[0] += dir[0]; point[1] += dir[1]; point[2] += dir[2]; }
+    pos[0] = (short)floorf(point[0]); pos[1] = (short)floorf(point[1]); pos[2] = (short)floorf(point[2]);
+}
+
+// setToType3 (SceneReconstructionEngine_host.cu:343-348) over the previous visible list
+__global__ void k_set_type3(const TfDevState* __restrict__ st, const int* __restrict__ visibleIds,
+                            unsigned char* __restrict__ visType)
+{
+    if (st->abort) return;
+    const int n = st->noVisibleEntries;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        visType[visibleIds[i]] = 3;
+}
+
+// ---------------------------------------------------------------------------------------
+// block scan helpers (256 threads)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int wave_incl_scan(int v)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int n = __shfl_up(v, o, 64);
+        if (lane >= o) v += n;
+    }
+    return v;
+}
+
+// exclusive scan of v over the 256-thread block; *total receives the block sum
+__device__ __forceinline__ int block_excl_scan(int v, int* total)
+{
+    __shared__ int wsum[4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int inc = wave_incl_scan(v);
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int w = 0; w < 4; ++w) { int s = wsum[w]; if (w < wave) off += s; tot += s; }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+__device__ __forceinline__ int block_sum(int v)
+{
+    int tot;
+    block_excl_scan(v, &tot);
+    return tot;
+}
+
+// ---------------------------------------------------------------------------------------
+// allocateVoxelBlocksList_device (SceneReconstructionEngine_host.cu:350-415), ordered
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_alloc_count(const TfDevState* __restrict__ st, const unsigned char* __restrict__ allocType, int n_total, int* counts)
+{
+    if (st->abort) return;
+    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
+    int c12 = 0, c2 = 0;
+    if (base < n_total) {
+        unsigned long long lo, hi;
+        load16(allocType + base, &lo, &hi);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { unsigned t = byte16(lo, hi, i); c12 += t != 0; c2 += t == 2; }
+    }
+    int t12 = block_sum(c12);
+    int t2 = block_sum(c2);
+    if (threadIdx.x == 0) { counts[2 * blockIdx.x] = t12; counts[2 * blockIdx.x + 1] = t2; }
+}
+
+__global__ void __launch_bounds__(256)
+k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int* __restrict__ counts,
+              unsigned char* __restrict__ allocType, int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
+              unsigned char* __restrict__ visType, const int* __restrict__ allocList,
+              const int* __restrict__ excessList, int* __restrict__ requestList, int n_total)
+{
+    if (st->abort) return;
+    // prefix and totals over the per-chunk counts
+    int p12 = 0, p2 = 0, a12 = 0, a2 = 0;
+    for (int h = threadIdx.x; h < n_chunks; h += 256) {
+        int c12 = counts[2 * h], c2 = counts[2 * h + 1];
+        a12 += c12; a2 += c2;
+        if (h < (int)blockIdx.x) { p12 += c12; p2 += c2; }
+    }
+    p12 = block_sum(p12); p2 = block_sum(p2); a12 = block_sum(a12); a2 = block_sum(a2);
+    const int v0 = st->lastFreeBlockId, e0 = st->lastFreeExcessListId;
+    const bool exhausted = (a12 > v0 + 1) || (a2 > e0 + 1);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->alloc_exhausted = exhausted ? 1 : 0;
+        st->pad_[0] = a12; st->pad_[1] = a2;
+    }
+    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
+    unsigned long long lo = 0, hi = 0;
+    int l12 = 0, l2 = 0;
+    if (base < n_total) {
+        load16(allocType + base, &lo, &hi);
+        for (int i = 0; i < 16; ++i) { unsigned t = byte16(lo, hi, i); l12 += t != 0; l2 += t == 2; }
+    }
+    int tmp;
+    int r12 = p12 + block_excl_scan(l12, &tmp);
+    int r2 = p2 + block_excl_scan(l2, &tmp);
+    if (l12 == 0) return;
+    const float* invM = st->invM_alloc;
+    for (int i = 0; i < 16; ++i) {
+        int t = (int)byte16(lo, hi, i);
+        if (!t) continue;
+        int idx = base + i;
+        requestList[r12] = idx;
+        if (!exhausted) {
+            short pos[3];
+            alloc_block_from_key(a, invM, winnerKey[idx], pos);
+            TfHashEntry e; e.x = pos[0]; e.y = pos[1]; e.z = pos[2]; e.pad = 0; e.offset = 0;
+            e.ptr = allocList[v0 - r12];
+            if (t == 1) {
+                hash[idx] = e;
+            } else {
+                int exlOffset = excessList[e0 - r2];
+                hash[idx].offset = exlOffset + 1;
+                hash[a.n_buckets + exlOffset] = e;
+                visType[a.n_buckets + exlOffset] = 1;
+            }
+            allocType[idx] = 0;
+            winnerKey[idx] = -1;
+        }
+        r12++;
+        if (t == 2) r2++;
+    }
+}
+
+// counter update; on capacity exhaustion the exact serial semantics in index order
+__global__ void k_alloc_finish(AllocArgs a, TfDevState* __restrict__ st, unsigned char* __restrict__ allocType,
+                               int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
+                               unsigned char* __restrict__ visType, const int* __restrict__ allocList,
+                               const int* __restrict__ excessList, const int* __restrict__ requestList)
+{
+    if (st->abort) return;
+    const int total12 = st->pad_[0], total2 = st->pad_[1];
+    if (!st->alloc_exhausted) {
+        st->lastFreeBlockId -= total12;
+        st->lastFreeExcessListId -= total2;
+        return;
+    }
+    int v = st->lastFreeBlockId, e = st->lastFreeExcessListId;
+    for (int r = 0; r < total12; ++r) {
+        int idx = requestList[r];
+        int t = allocType[idx];
+        if (t == 1) {
+            int vbaIdx = v--;
+            if (vbaIdx >= 0) {
+                short pos[3];
+                alloc_block_from_key(a, st->invM_alloc, winnerKey[idx], pos);
+                TfHashEntry he; he.x = pos[0]; he.y = pos[1]; he.z = pos[2]; he.pad = 0; he.offset = 0;
+                he.ptr = allocList[vbaIdx];
+                hash[idx] = he;
+            } else {
+                visType[idx] = 0;
+                v++;
+            }
+        } else if (t == 2) {
+            int vbaIdx = v--, exlIdx = e--;
+            if (vbaIdx >= 0 && exlIdx >= 0) {
+                short pos[3];
+                alloc_block_from_key(a, st->invM_alloc, winnerKey[idx], pos);
+                TfHashEntry he; he.x = pos[0]; he.y = pos[1]; he.z = pos[2]; he.pad = 0; he.offset = 0;
+                he.ptr = allocList[vbaIdx];
+                int exlOffset = excessList[exlIdx];
+                hash[idx].offset = exlOffset + 1;
+                hash[a.n_buckets + exlOffset] = he;
+                visType[a.n_buckets + exlOffset] = 1;
+            } else {
+                v++; e++;
+            }
+        }
+        allocType[idx] = 0;
+        winnerKey[idx] = -1;
+    }
+    st->lastFreeBlockId = v;
+    st->lastFreeExcessListId = e;
+}
+
+// ---------------------------------------------------------------------------------------
+// buildVisibleList_device<false> (SceneReconstructionEngine_host.cu:434-479) with
+// checkBlockVisibility<false> (SceneReconstructionEngine.hpp:300-375), ordered compaction
+// ---------------------------------------------------------------------------------------
+struct VisArgs {
+    float fx, fy, cx, cy;
+    float factor;                 // (float)SDF_BLOCK_SIZE * voxelSize
+    int W, H;
+    int n_total, cap;
+};
+
+__device__ __forceinline__ bool vis_point(const float* M, const float* pt, const VisArgs& v)
+{
+    float b[4];
+    tf_m4v(M, pt[0], pt[1], pt[2], pt[3], b);
+    if (b[2] < 1e-10f) return false;
+    float bx = v.fx * b[0] / b[2] + v.cx;
+    float by = v.fy * b[1] / b[2] + v.cy;
+    return bx >= 0 && bx < (float)v.W && by >= 0 && by < (float)v.H;
+}
+
+__device__ bool vis_block(const TfHashEntry& e, const float* M, const VisArgs& v)
+{
+    const float f = v.factor;
+    float pt[4] = { (float)e.x * f, (float)e.y * f, (float)e.z * f, 1.0f };
+    if (vis_point(M, pt, v)) return true;
+    pt[2] += f; if (vis_point(M, pt, v)) return true;                     // 0 0 1
+    pt[1] += f; if (vis_point(M, pt, v)) return true;                     // 0 1 1
+    pt[0] += f; if (vis_point(M, pt, v)) return true;                     // 1 1 1
+    pt[2] -= f; if (vis_point(M, pt, v)) return true;                     // 1 1 0
+    pt[1] -= f; if (vis_point(M, pt, v)) return true;                     // 1 0 0
+    pt[0] -= f; pt[1] += f; if (vis_point(M, pt, v)) return true;         // 0 1 0
+    pt[0] += f; pt[1] -= f; pt[2] += f; if (vis_point(M, pt, v)) return true;  // 1 0 1
+    return false;
+}
+
+__global__ void __launch_bounds__(256)
+k_vis_count(VisArgs v, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+            unsigned char* __restrict__ visType, int* __restrict__ counts)
+{
+    if (st->abort) return;
+    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
+    int cnt = 0;
+    if (base < v.n_total) {
+        unsigned long long lo, hi;
+        load16(visType + base, &lo, &hi);
+        bool dirty = false;
+        for (int i = 0; i < 16; ++i) {
+            unsigned t = byte16(lo, hi, i);
+            if (t == 3) {
+                if (!vis_block(hash[base + i], st->M_alloc, v)) {
+                    if (i < 8) lo &= ~(0xffull << (8 * i)); else hi &= ~(0xffull << (8 * (i - 8)));
+                    t = 0;
+                    dirty = true;
+                }
+            }
+            cnt += t > 0;
+        }
+        if (dirty) *(uint4*)(visType + base) = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
+    }
+    int tot = block_sum(cnt);
+    if (threadIdx.x == 0) counts[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(256)
+k_vis_apply(VisArgs v, TfDevState* __restrict__ st, int n_chunks, const int* __restrict__ counts,
+            const unsigned char* __restrict__ visType, int* __restrict__ visibleIds)
+{
+    if (st->abort) return;
+    int pre = 0, all = 0;
+    for (int h = threadIdx.x; h < n_chunks; h += 256) {
+        int c = counts[h];
+        all += c;
+        if (h < (int)blockIdx.x) pre += c;
+    }
+    pre = block_sum(pre); all = block_sum(all);
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->noVisibleEntries = all < v.cap ? all : v.cap;
+    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
+    unsigned long long lo = 0, hi = 0;
+    int cnt = 0;
+    if (base < v.n_total) {
+        load16(visType + base, &lo, &hi);
+        for (int i = 0; i < 16; ++i) cnt += byte16(lo, hi, i) > 0;
+    }
+    int tmp;
+    int r = pre + block_excl_scan(cnt, &tmp);
+    if (!cnt) return;
+    for (int i = 0; i < 16; ++i) {
+        if (byte16(lo, hi, i) > 0) {
+            if (r < v.cap) visibleIds[r] = base + i;
+            r++;
+        }
+    }
+}
+
+static AllocArgs make_alloc_args(tf_ctx* c)
+{
+    AllocArgs a;
+    a.dists = c->dists; a.W = c->W; a.H = c->H;
+    a.invfx = 1.0f / c->p.fx; a.invfy = 1.0f / c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy;
+    a.mu = c->p.mu;
+    a.oneOverVoxelSize = 1.0f / (c->p.voxelSize * (float)TF_BLK);      // SceneReconstructionEngine_host.cu:138
+    a.vf_min = c->p.viewFrustum_min; a.vf_max = c->p.viewFrustum_max;
+    a.mask = (unsigned)(c->p.n_buckets - 1);
+    a.n_buckets = c->p.n_buckets;
+    return a;
+}
+
+// AllocateSceneFromDepth (SceneReconstructionEngine_host.cu:75-195) with the matrices
+// already in st->M_alloc / st->invM_alloc
+hipError_t tfk_alloc(tf_ctx* c)
+{
+    AllocArgs a = make_alloc_args(c);
+    hipLaunchKernelGGL(k_set_type3, dim3(256), dim3(256), 0, c->stream, c->st, c->visibleIds, c->visType);
+    hipLaunchKernelGGL(k_alloc_requests, dim3((c->W + 15) / 16, (c->H + 15) / 16), dim3(256), 0, c->stream,
+                       a, c->st, c->hash, c->allocType, c->visType, c->winnerKey);
+    hipLaunchKernelGGL(k_alloc_count, dim3(c->alloc_chunks), dim3(256), 0, c->stream, c->st, c->allocType, c->n_total,
+                       c->allocCounts);
+    hipLaunchKernelGGL(k_alloc_apply, dim3(c->alloc_chunks), dim3(256), 0, c->stream, a, c->st, c->alloc_chunks,
+                       c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
+                       c->requestList, c->n_total);
+    hipLaunchKernelGGL(k_alloc_finish, dim3(1), dim3(1), 0, c->stream, a, c->st, c->allocType, c->winnerKey, c->hash,
+                       c->visType, c->allocList, c->excessList, c->requestList);
+    VisArgs v;
+    v.fx = c->p.fx; v.fy = c->p.fy; v.cx = c->p.cx; v.cy = c->p.cy;
+    v.factor = (float)TF_BLK * c->p.voxelSize;
+    v.W = c->W; v.H = c->H; v.n_total = c->n_total; v.cap = c->p.vis_capacity;
+    hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
+                       c->visCounts);
+    hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
+                       c->visCounts, c->visType, c->visibleIds);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// integrateIntoScene_device<Voxel_s,false> (SceneReconstructionEngine_host.cu:297-329) +
+// computeUpdatedVoxelDepthInfo (SceneReconstructionEngine.hpp:23-71).
+// 128 lanes per 8^3 block, 4 consecutive voxels (16 B) per lane; blocks grid-strided.
+// ---------------------------------------------------------------------------------------
+struct IntegArgs {
+    const float* dists;
+    int W, H;
+    float fx, fy, cx, cy;
+    float voxelSize, mu;
+    int maxW;
+};
+
+__device__ __forceinline__ unsigned integ_voxel(unsigned vox, float px, float py, float pz, const float* M,
+                                                const IntegArgs& a)
+{
+    float pc[3];
+    tf_m4v3(M, px, py, pz, 1.0f, pc);
+    if (pc[2] <= 0) return vox;
+    float ix = a.fx * pc[0] / pc[2] + a.cx;
+    float iy = a.fy * pc[1] / pc[2] + a.cy;
+    if ((ix < 1) || (ix > (float)(a.W - 2)) || (iy < 1) || (iy > (float)(a.H - 2))) return vox;
+    float depth_measure = a.dists[(int)(ix + 0.5f) + (int)(iy + 0.5f) * a.W];
+    if (depth_measure <= 0.0f) return vox;
+    float eta = depth_measure - pc[2];
+    if (eta < -a.mu) return vox;
+    short sdf = (short)(vox & 0xffff);
+    int oldW = (vox >> 16) & 0xff;
+    float oldF = (float)sdf / 32767.0f;
+    float newF = eta / a.mu;
+    newF = (1.0f < newF) ? 1.0f : newF;
+    newF = (float)oldW * oldF + 1.0f * newF;
+    int newW = oldW + 1;
+    newF /= (float)newW;
+    newW = (newW < a.maxW) ? newW : a.maxW;
+    short nsdf = (short)(newF * 32767.0f);
+    return ((unsigned)(unsigned short)nsdf) | ((unsigned)(newW & 0xff) << 16) | (vox & 0xff000000u);
+}
+
+__global__ void __launch_bounds__(256)
+k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba)
+{
+    if (st->abort) return;
+    const int n = st->noVisibleEntries;
+    float M[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) M[i] = st->M_alloc[i];
+    const int half = threadIdx.x >> 7, t = threadIdx.x & 127;
+    const int lin = t * 4;                       // first voxel of this lane: x in {0,4}
+    const int vx = lin & 7, vy = (lin >> 3) & 7, vz = lin >> 6;
+    for (int i = blockIdx.x * 2 + half; i < n; i += gridDim.x * 2) {
+        TfHashEntry e = hash[visibleIds[i]];
+        if (e.ptr < 0) continue;
+        const int gx = e.x * TF_BLK, gy = e.y * TF_BLK, gz = e.z * TF_BLK;
+        uint4* p = (uint4*)(vba + (size_t)e.ptr * TF_BLK3 + lin);
+        uint4 v = *p;
+        const float py = (float)(gy + vy) * a.voxelSize, pz = (float)(gz + vz) * a.voxelSize;
+        v.x = integ_voxel(v.x, (float)(gx + vx + 0) * a.voxelSize, py, pz, M, a);
+        v.y = integ_voxel(v.y, (float)(gx + vx + 1) * a.voxelSize, py, pz, M, a);
+        v.z = integ_voxel(v.z, (float)(gx + vx + 2) * a.voxelSize, py, pz, M, a);
+        v.w = integ_voxel(v.w, (float)(gx + vx + 3) * a.voxelSize, py, pz, M, a);
+        *p = v;
+    }
+}
+
+hipError_t tfk_integrate(tf_ctx* c)
+{
+    IntegArgs a;
+    a.dists = c->dists; a.W = c->W; a.H = c->H;
+    a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy;
+    a.voxelSize = c->p.voxelSize; a.mu = c->p.mu; a.maxW = c->p.maxW;
+    hipLaunchKernelGGL(k_integrate, dim3(2048), dim3(256), 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba);
+    return hipGetLastError();
+}

@@ -1,0 +1,218 @@
+"""Python mirror of the reference's pipeline API (tfusion/include/tfusion/topfu.hpp:28-110)
+over the C-ABI of libtfusion_hip.so.
+
+    params = TopFuParams.default_params()     # topfu.cpp:12-53
+    topfu = TopFu(params)                     # topfu.cpp:55-84
+    ok = topfu(depth)                         # operator(), topfu.cpp:161-330
+    img = topfu.renderImage()                 # topfu.cpp:332-377
+    pose = topfu.getCameraPose()              # topfu.cpp:154-159
+    topfu.reset()                             # topfu.cpp:141-152
+
+`depth` is a uint16 (rows, cols) numpy array (host; uploaded like cuda::Depth::upload)
+or a device pointer (int) to uint16 millimetres on the context's device.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+HASH_DTYPE = np.dtype([("x", "<i2"), ("y", "<i2"), ("z", "<i2"), ("pad", "<i2"), ("offset", "<i4"), ("ptr", "<i4")])
+VOXEL_DTYPE = np.dtype([("sdf", "<i2"), ("w", "u1"), ("pad", "u1")])
+
+
+class TopFuParams:
+    """TopFuParams: construct with default_params() and override attributes."""
+
+    @staticmethod
+    def default_params(**kw):
+        return L.default_params(**kw)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _rt(m):
+    a = np.ascontiguousarray(np.asarray(m, np.float32)[:3, :4] if np.ndim(m) == 2 else np.asarray(m, np.float32))
+    return a.reshape(12)
+
+
+class TopFu:
+    """tfusion::TopFu on one MI355X (one HIP stream per instance)."""
+
+    def __init__(self, params=None, device=None, **kw):
+        lib = L.load()
+        if device is not None:
+            L.check(lib.tf_set_device(int(device)), "tf_set_device")
+        self.params_ = params if params is not None else L.default_params(**kw)
+        h = ctypes.c_void_p()
+        L.check(lib.tf_create(ctypes.byref(self.params_), ctypes.byref(h)), "tf_create")
+        self._h = h
+        self.W, self.H = self.params_.cols, self.params_.rows
+        self.n_total = self.params_.n_buckets + self.params_.n_excess
+        self.last_stats = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.load().tf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def params(self):
+        return self.params_
+
+    # -- TopFu API ----------------------------------------------------------------------
+    def __call__(self, depth, pitch=0):
+        """TopFu::operator(): returns the frame's bool (False = ICP failed, scene reset)."""
+        lib = L.load()
+        stats = L.TfStats()
+        pose = np.zeros(12, np.float32)
+        if isinstance(depth, int):
+            s = lib.tf_process_frame(self._h, ctypes.c_void_p(depth), pitch, _ptr(pose), ctypes.byref(stats))
+        else:
+            d = np.ascontiguousarray(depth, np.uint16)
+            assert d.shape == (self.H, self.W), d.shape
+            s = lib.tf_process_frame_host(self._h, _ptr(d), self.W * 2, _ptr(pose), ctypes.byref(stats))
+        L.check(s, "tf_process_frame", allow=(L.TF_OK, L.TF_ICP_FAIL))
+        self.last_stats = stats.as_dict()
+        return s == L.TF_OK
+
+    def process_frames(self, dev_frames, n, stride=None):
+        """Runs n device-resident frames; returns the per-frame bools."""
+        ok = np.zeros(n, np.int32)
+        stride = stride if stride is not None else self.W * self.H * 2
+        L.check(L.load().tf_process_frames(self._h, ctypes.c_void_p(dev_frames), stride, n, _ptr(ok)),
+                "tf_process_frames")
+        return ok.astype(bool)
+
+    def renderImage(self):
+        """TopFu::renderImage -> uint8 (rows, cols, 4) grey image (host copy)."""
+        L.check(L.load().tf_render_image(self._h, None, 0), "tf_render_image")
+        return self.download(L.TF_BUF_GREY).view(np.uint8).reshape(self.H, self.W, 4)
+
+    def getCameraPose(self):
+        rt = np.zeros(12, np.float32)
+        L.check(L.load().tf_get_pose(self._h, _ptr(rt)), "tf_get_pose")
+        m = np.eye(4, dtype=np.float32)
+        m[:3, :4] = rt.reshape(3, 4)
+        return m
+
+    def reset(self):
+        L.check(L.load().tf_reset(self._h), "tf_reset")
+
+    def stats(self):
+        s = L.TfStats()
+        L.check(L.load().tf_get_stats(self._h, ctypes.byref(s)), "tf_get_stats")
+        return s.as_dict()
+
+    def stream(self):
+        return L.load().tf_get_stream(self._h)
+
+    # -- stage entry points (parity tests) ------------------------------------------------
+    def stage_preprocess(self, depth):
+        """computeDists + bilateral + truncation + pyramid + vertex/normal maps (host depth)."""
+        d = np.ascontiguousarray(depth, np.uint16)
+        assert d.shape == (self.H, self.W), d.shape
+        L.check(L.load().tf_stage_preprocess_host(self._h, _ptr(d), self.W * 2), "tf_stage_preprocess_host")
+
+    def stage_icp(self):
+        aff = np.zeros(12, np.float32)
+        ok = ctypes.c_int()
+        it = ctypes.c_int()
+        L.check(L.load().tf_stage_icp(self._h, _ptr(aff), ctypes.byref(ok), ctypes.byref(it)), "tf_stage_icp")
+        return bool(ok.value), aff.reshape(3, 4), it.value
+
+    def stage_alloc(self, pose_rt):
+        L.check(L.load().tf_stage_alloc(self._h, _ptr(_rt(pose_rt))), "tf_stage_alloc")
+
+    def stage_integrate(self, pose_rt):
+        L.check(L.load().tf_stage_integrate(self._h, _ptr(_rt(pose_rt))), "tf_stage_integrate")
+
+    def stage_expected_depths(self, pose_rt):
+        L.check(L.load().tf_stage_expected_depths(self._h, _ptr(_rt(pose_rt))), "tf_stage_expected_depths")
+
+    def stage_raycast(self, invM_rt, update_visible):
+        L.check(L.load().tf_stage_raycast(self._h, _ptr(_rt(invM_rt)), int(update_visible)), "tf_stage_raycast")
+
+    def stage_icp_maps(self, invM_rt):
+        L.check(L.load().tf_stage_icp_maps(self._h, _ptr(_rt(invM_rt))), "tf_stage_icp_maps")
+
+    def stage_render_grey(self, invM_rt):
+        L.check(L.load().tf_stage_render_grey(self._h, _ptr(_rt(invM_rt))), "tf_stage_render_grey")
+        return self.download(L.TF_BUF_GREY).view(np.uint8).reshape(self.H, self.W, 4)
+
+    def stage_reset_scene(self):
+        L.check(L.load().tf_stage_reset_scene(self._h), "tf_stage_reset_scene")
+
+    def stage_swap_pyramids(self):
+        L.check(L.load().tf_stage_swap_pyramids(self._h), "tf_stage_swap_pyramids")
+
+    # -- state transfer ------------------------------------------------------------------
+    def nbytes(self, which, level=0):
+        n = ctypes.c_size_t()
+        L.check(L.load().tf_buffer_bytes(self._h, which, level, ctypes.byref(n)), "tf_buffer_bytes")
+        return n.value
+
+    def download(self, which, level=0):
+        n = self.nbytes(which, level)
+        buf = np.empty(n, np.uint8)
+        L.check(L.load().tf_download(self._h, which, level, _ptr(buf), n), "tf_download")
+        return buf
+
+    def upload(self, which, arr, level=0):
+        a = np.ascontiguousarray(arr)
+        n = self.nbytes(which, level)
+        assert a.nbytes == n, (a.nbytes, n)
+        L.check(L.load().tf_upload(self._h, which, level, _ptr(a), n), "tf_upload")
+
+    def set_pose(self, rt):
+        L.check(L.load().tf_set_pose(self._h, _ptr(_rt(rt))), "tf_set_pose")
+
+    def set_counters(self, lastFreeBlockId, lastFreeExcessListId, noVisibleEntries):
+        L.check(L.load().tf_set_counters(self._h, lastFreeBlockId, lastFreeExcessListId, noVisibleEntries),
+                "tf_set_counters")
+
+    # typed views
+    def hash(self):
+        return self.download(L.TF_BUF_HASH).view(HASH_DTYPE)
+
+    def vba(self):
+        return self.download(L.TF_BUF_VBA).view(VOXEL_DTYPE)
+
+    def visible_ids(self):
+        n = self.stats()["noVisibleEntries"]
+        return self.download(L.TF_BUF_VISIBLE_IDS).view(np.int32)[:n]
+
+    def visible_type(self):
+        return self.download(L.TF_BUF_VISIBLE_TYPE)
+
+    def range_image(self):
+        return self.download(L.TF_BUF_RANGE).view(np.float32).reshape(self.H, self.W, 2)
+
+    def raycast_result(self):
+        return self.download(L.TF_BUF_RAYCAST).view(np.float32).reshape(self.H, self.W, 4)
+
+    def dists(self):
+        return self.download(L.TF_BUF_DISTS).view(np.float32).reshape(self.H, self.W)
+
+    def level_shape(self, l):
+        return self.H >> l, self.W >> l
+
+    def curr_depth(self, l):
+        return self.download(L.TF_BUF_DEPTH, l).view(np.uint16).reshape(self.level_shape(l))
+
+    def curr_maps(self, l):
+        h, w = self.level_shape(l)
+        return (self.download(L.TF_BUF_CURR_POINTS, l).view(np.float32).reshape(h, w, 4),
+                self.download(L.TF_BUF_CURR_NORMALS, l).view(np.float32).reshape(h, w, 4))
+
+    def prev_maps(self, l):
+        h, w = self.level_shape(l)
+        return (self.download(L.TF_BUF_PREV_POINTS, l).view(np.float32).reshape(h, w, 4),
+                self.download(L.TF_BUF_PREV_NORMALS, l).view(np.float32).reshape(h, w, 4))
