@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: fused frames/sec @640x480, 5 mm voxel hash
+(ICP + integrate ms/frame reported alongside), on the C2 workload of SURVEY.md §8d.
+
+A "step" is one TopFu::operator() frame (tfusion/src/topfu.cpp:161-330): preprocessing,
+3-level projective ICP (19 iterations), hash allocation, TSDF integration, the grey
+renderImage raycast, CreateExpectedDepths and the CreateICPMaps raycast.  Frames come from
+the synthetic 640x480 orbit sequence (topfusion_amd/synth.py, seed 7 + rank), uploaded
+to HBM before the timed region.  One process per GPU; each rank tracks its own
+independent stream (replicas, weak scaling) and the per-rank frame counts / times are
+combined with one RCCL all-reduce.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--cols", type=int, default=640)
+    ap.add_argument("--rows", type=int, default=480)
+    ap.add_argument("--voxel", type=float, default=0.005)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample length")
+    ap.add_argument("--no-profile", action="store_true", help="disable the per-stage HIP-event timing")
+    return ap.parse_args()
+
+
+def stage_bytes(stage, p, nvis, W, H):
+    """Algorithmic HBM bytes of ONE launch of a stage."""
+    if stage in ("raycast_render", "raycast_icp"):
+        return W * H * 16 + nvis * (2048 + 16)          # ray output float4 + every visible block once
+    if stage == "integrate":
+        return nvis * (4096 + 20) + W * H * 4           # voxel R+W + entry/id + depth image
+    if stage == "grey":
+        return W * H * (16 + 4) + nvis * (2048 + 16)
+    if stage == "icp":
+        tot = 0
+        for l in range(3):
+            tot += p.icp_iter_num[l] * (W >> l) * (H >> l) * 64
+        return tot
+    return None
+
+
+def cpu_baseline(frames, params_kw, seconds):
+    """Oracle (serial C restatement of the reference, 1 thread) on a bounded prefix of the same stream."""
+    from oracle import oracle as O
+    o = O.Oracle(O.default_params(**params_kw))
+    t0 = time.perf_counter()
+    n = 0
+    while n < len(frames):
+        o(frames[n])
+        n += 1
+        if time.perf_counter() - t0 >= seconds and n >= 3:
+            break
+    dt = time.perf_counter() - t0
+    return n / dt, n, dt
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    from topfusion_amd import TopFu, default_params, synth
+
+    W, H = args.cols, args.rows
+    fx, fy, cx, cy = synth.intrinsics(W, H)
+    pkw = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=args.voxel)
+    n_frames = args.warmup + args.steps
+    frames = synth.orbit_sequence(n_frames, W, H, seed=7 + rank)
+    dev = torch.from_numpy(frames.view(np.int16)).to(f"cuda:{local_rank}")
+    frame_bytes = W * H * 2
+    base = dev.data_ptr()
+
+    tf = TopFu(default_params(**pkw), device=local_rank)
+    torch.cuda.synchronize()
+    ok_w = tf.process_frames(base, args.warmup) if args.warmup > 0 else np.zeros(0, bool)
+    if not args.no_profile:
+        tf.profile(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ok = tf.process_frames(base + args.warmup * frame_bytes, args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = tf.profile_read() if not args.no_profile else {}
+    st = tf.stats()
+
+    # one RCCL all-reduce: [elapsed (max), frames (sum), fps (sum)]
+    red = torch.tensor([elapsed, float(args.steps), args.steps / elapsed], dtype=torch.float64,
+                       device=f"cuda:{local_rank}")
+    if world > 1:
+        mx = red[0:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = red[1:3].clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed_max, total_frames = float(mx[0]), float(sm[0])
+    else:
+        elapsed_max, total_frames = elapsed, float(args.steps)
+
+    if rank == 0:
+        value = total_frames / elapsed_max
+        ms_per_step = elapsed_max / args.steps * 1000.0
+        per_stage = {k: (v[0] / v[1] if v[1] else None) for k, v in prof.items()}
+        icp_integ = None
+        if prof and prof["icp"][1]:
+            icp_integ = per_stage["icp"] + per_stage["alloc"] + per_stage["integrate"]
+        # dominant single-kernel stage by measured time
+        roof = None
+        if prof:
+            cands = {k: per_stage[k] for k in ("raycast_render", "raycast_icp", "integrate", "grey") if per_stage[k]}
+            if cands:
+                dom = max(cands, key=cands.get)
+                nvis = st["noVisibleEntries"]
+                b = stage_bytes(dom, tf.params(), nvis, W, H)
+                ach = b / (cands[dom] * 1e-3) / 1e9
+                traffic = None
+                pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+                if os.path.exists(pmc_path):
+                    try:
+                        traffic = json.load(open(pmc_path)).get(dom, {}).get("bytes_per_launch")
+                    except Exception:
+                        traffic = None
+                roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic, "kernel": dom,
+                        "algorithmic_bytes_per_launch": b, "avg_launch_ms": round(cands[dom], 5)}
+        cpu = None
+        if not args.no_cpu_baseline:
+            v, n, dt = cpu_baseline(frames, pkw, args.cpu_seconds)
+            cpu = {"value": round(v, 4), "unit": "frames/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle (serial C restatement) on frames 0..{n - 1} of the same C2 stream, "
+                             f"{W}x{H}, {dt:.1f} s, 1 thread, host CPU of the GPU box"}
+        out = {
+            "metric": "fused frames/sec @640x480, 5 mm voxel hash; ICP+integrate ms/frame",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"C2 orbit, {W}x{H}, {args.voxel * 1000:g} mm voxels, 8^3 blocks, "
+                                   "3-level ICP (10/5/4) + alloc + integrate + renderImage + expected depths + "
+                                   "ICP-map raycast; one independent stream per GPU",
+                       "cols": W, "rows": H, "voxel_m": args.voxel, "parallelism": f"replicas{world}"},
+            "icp_integrate_ms_per_frame": None if icp_integ is None else round(icp_integ, 4),
+            "stage_ms_per_frame": {k: (None if v is None else round(v, 4)) for k, v in per_stage.items()},
+            "frames_ok": int(ok.sum()), "resets": int(st["n_resets"]),
+            "visible_blocks_last": st["noVisibleEntries"],
+            "allocated_blocks": tf.params().n_blocks - 1 - st["lastFreeBlockId"],
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    tf.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -164,6 +164,25 @@ tf_status tf_buffer_bytes(tf_ctx* ctx, int which, int level, size_t* bytes);
 tf_status tf_download(tf_ctx* ctx, int which, int level, void* host, size_t bytes);
 tf_status tf_upload(tf_ctx* ctx, int which, int level, const void* host, size_t bytes);
 tf_status tf_set_pose(tf_ctx* ctx, const float rt[12]);
+
+/* ---- per-stage timing (SampledScopeTime, tfusion/include/tfusion/types.hpp:91-104) --
+ * When enabled, every frame records HIP events around each stage on the context stream;
+ * durations accumulate until tf_profile_reset.  Stage ids: */
+typedef enum tf_stage_id {
+    TF_STAGE_PREPROCESS = 0,      /* dists + bilateral + pyramid + vertex/normal maps */
+    TF_STAGE_ICP = 1,             /* estimateTransform, all iterations */
+    TF_STAGE_ALLOC = 2,           /* AllocateSceneFromDepth */
+    TF_STAGE_INTEGRATE = 3,       /* IntegrateIntoScene (k_integrate only) */
+    TF_STAGE_RAYCAST_RENDER = 4,  /* renderImage raycast (k_raycast) */
+    TF_STAGE_GREY = 5,            /* renderGrey */
+    TF_STAGE_EXPECTED_DEPTHS = 6, /* CreateExpectedDepths */
+    TF_STAGE_RAYCAST_ICP = 7,     /* CreateICPMaps raycast<true> (k_raycast) */
+    TF_STAGE_ICP_MAPS = 8         /* renderICP + resizePointsNormals */
+} tf_stage_id;
+tf_status tf_profile_enable(tf_ctx* ctx, int enable);
+tf_status tf_profile_reset(tf_ctx* ctx);
+/* ms[i] = accumulated milliseconds, counts[i] = frames measured, for i < n (n <= 9) */
+tf_status tf_profile_read(tf_ctx* ctx, double* ms, long long* counts, int n);
 tf_status tf_set_counters(tf_ctx* ctx, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries);
 
 #ifdef __cplusplus

@@ -13,6 +13,9 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tfusion_hip.h")
 
 TF_OK, TF_ICP_FAIL, TF_INVALID_ARG, TF_OOM, TF_HIP_ERROR, TF_NO_DEVICE = range(6)
 
+STAGE_NAMES = ("preprocess", "icp", "alloc", "integrate", "raycast_render", "grey", "expected_depths",
+               "raycast_icp", "icp_maps")
+
 (TF_BUF_HASH, TF_BUF_VBA, TF_BUF_VISIBLE_IDS, TF_BUF_VISIBLE_TYPE, TF_BUF_RANGE, TF_BUF_RAYCAST, TF_BUF_DISTS,
  TF_BUF_DEPTH, TF_BUF_CURR_POINTS, TF_BUF_CURR_NORMALS, TF_BUF_PREV_POINTS, TF_BUF_PREV_NORMALS, TF_BUF_GREY) = range(13)
 
@@ -99,6 +102,9 @@ def load():
         "tf_upload": ([P, I, I, P, S], I),
         "tf_set_pose": ([P, P], I),
         "tf_set_counters": ([P, I, I, I], I),
+        "tf_profile_enable": ([P, I], I),
+        "tf_profile_reset": ([P], I),
+        "tf_profile_read": ([P, P, P, I], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

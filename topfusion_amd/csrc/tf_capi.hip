@@ -101,6 +101,7 @@ static void ctx_free(tf_ctx* c)
         if (c->prev_nrm[l]) (void)hipFree(c->prev_nrm[l]);
     }
     if (c->st_host) (void)hipHostFree(c->st_host);
+    for (int i = 0; i < 2 * TF_NUM_STAGES; ++i) if (c->prof_ev[i]) (void)hipEventDestroy(c->prof_ev[i]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -252,27 +253,52 @@ static void swap_pyramids(tf_ctx* c)
     }
 }
 
+// ---- per-stage event timing -----------------------------------------------------------
+#define STAGE(id, expr)                                                                     \
+    do {                                                                                    \
+        if (c->prof_enabled) TF_CHECK(hipEventRecord(c->prof_ev[2 * (id)], c->stream));    \
+        TF_CHECK(expr);                                                                     \
+        if (c->prof_enabled) {                                                              \
+            TF_CHECK(hipEventRecord(c->prof_ev[2 * (id) + 1], c->stream));                  \
+            c->prof_pending[id] = 1;                                                        \
+        }                                                                                   \
+    } while (0)
+
+static void prof_collect(tf_ctx* c)
+{
+    if (!c->prof_enabled) return;
+    for (int i = 0; i < TF_NUM_STAGES; ++i) {
+        if (!c->prof_pending[i]) continue;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, c->prof_ev[2 * i], c->prof_ev[2 * i + 1]) == hipSuccess) {
+            c->prof_ms[i] += ms;
+            c->prof_count[i] += 1;
+        }
+        c->prof_pending[i] = 0;
+    }
+}
+
 // enqueue one TopFu::operator() frame; returns whether the frame took the tracking path
 static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, bool* tracked)
 {
     TF_CHECK(clear_abort(c));
-    TF_CHECK(tfk_preprocess(c, depth, pitch));                       // topfu.cpp:166-197
+    STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch));     // topfu.cpp:166-197
     if (c->frame_counter == 0) {                                     // topfu.cpp:200-209
         TF_CHECK(tfk_frame0_matrices(c));
-        TF_CHECK(tfk_alloc(c));
-        TF_CHECK(tfk_integrate(c));
+        STAGE(TF_STAGE_ALLOC, tfk_alloc(c));
+        STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c));
         swap_pyramids(c);
         *tracked = false;
         return TF_OK;
     }
-    TF_CHECK(tfk_icp(c, 1));                                         // topfu.cpp:242-243
-    TF_CHECK(tfk_alloc(c));                                          // topfu.cpp:281
-    TF_CHECK(tfk_integrate(c));                                      // topfu.cpp:282
-    TF_CHECK(tfk_raycast(c, 0));                                     // renderImage, topfu.cpp:284-285
-    TF_CHECK(tfk_render_grey(c));
-    TF_CHECK(tfk_expected_depths(c));                                // topfu.cpp:306
-    TF_CHECK(tfk_raycast(c, 1));                                     // CreateICPMaps, topfu.cpp:307
-    TF_CHECK(tfk_icp_maps(c));                                       // + resizePointsNormals :308-309
+    STAGE(TF_STAGE_ICP, tfk_icp(c, 1));                              // topfu.cpp:242-243
+    STAGE(TF_STAGE_ALLOC, tfk_alloc(c));                             // topfu.cpp:281
+    STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c));                     // topfu.cpp:282
+    STAGE(TF_STAGE_RAYCAST_RENDER, tfk_raycast(c, 0));               // renderImage, topfu.cpp:284-285
+    STAGE(TF_STAGE_GREY, tfk_render_grey(c));
+    STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c));         // topfu.cpp:306
+    STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));                  // CreateICPMaps, topfu.cpp:307
+    STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps(c));                       // + resizePointsNormals :308-309
     *tracked = true;
     return TF_OK;
 }
@@ -281,12 +307,40 @@ static tf_status finish_frame(tf_ctx* c, bool tracked)
 {
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
+    prof_collect(c);
     if (tracked && !c->st_host->icp_ok) {                            // topfu.cpp:263-264
         s = ctx_reset(c);
         if (s != TF_OK) return s;
         return TF_ICP_FAIL;
     }
     c->frame_counter++;
+    return TF_OK;
+}
+
+extern "C" tf_status tf_profile_enable(tf_ctx* c, int enable)
+{
+    if (!c) return TF_INVALID_ARG;
+    if (enable && !c->prof_ev[0]) {
+        for (int i = 0; i < 2 * TF_NUM_STAGES; ++i) TF_CHECK(hipEventCreate(&c->prof_ev[i]));
+    }
+    c->prof_enabled = enable ? 1 : 0;
+    return TF_OK;
+}
+
+extern "C" tf_status tf_profile_reset(tf_ctx* c)
+{
+    if (!c) return TF_INVALID_ARG;
+    for (int i = 0; i < TF_NUM_STAGES; ++i) { c->prof_ms[i] = 0; c->prof_count[i] = 0; c->prof_pending[i] = 0; }
+    return TF_OK;
+}
+
+extern "C" tf_status tf_profile_read(tf_ctx* c, double* ms, long long* counts, int n)
+{
+    if (!c || n < 0 || n > TF_NUM_STAGES) return TF_INVALID_ARG;
+    for (int i = 0; i < n; ++i) {
+        if (ms) ms[i] = c->prof_ms[i];
+        if (counts) counts[i] = c->prof_count[i];
+    }
     return TF_OK;
 }
 

@@ -18,6 +18,7 @@
 #define TF_SUBSAMPLE 8          // minmaximg_subsample (VisualisationEngine_Shared.hpp:7)
 #define TF_RB_SIZE 16           // renderingBlockSizeX/Y (VisualisationEngine_Shared.hpp:25-26)
 #define TF_LEVELS 3
+#define TF_NUM_STAGES 9     // tf_stage_id in include/tfusion_hip.h
 
 // HashEntry, VoxelBlockHash.hpp:32-44 (16 B; one dwordx4 probe)
 struct __attribute__((aligned(16))) TfHashEntry {
@@ -187,6 +188,12 @@ struct tf_ctx {
     int n_resets;
     int alloc_chunks;        // N_tot / 4096
     int vis_chunks;
+    // per-stage HIP-event timing on the context stream (tf_profile_*)
+    int prof_enabled;
+    hipEvent_t prof_ev[2 * TF_NUM_STAGES];
+    int prof_pending[TF_NUM_STAGES];
+    double prof_ms[TF_NUM_STAGES];
+    long long prof_count[TF_NUM_STAGES];
 };
 
 // ---------------------------------------------------------------------------------------

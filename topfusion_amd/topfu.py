@@ -114,6 +114,18 @@ class TopFu:
     def stream(self):
         return L.load().tf_get_stream(self._h)
 
+    # -- per-stage HIP-event timing ----------------------------------------------------
+    def profile(self, enable=True):
+        L.check(L.load().tf_profile_enable(self._h, int(enable)), "tf_profile_enable")
+        L.check(L.load().tf_profile_reset(self._h), "tf_profile_reset")
+
+    def profile_read(self):
+        n = len(L.STAGE_NAMES)
+        ms = np.zeros(n, np.float64)
+        cnt = np.zeros(n, np.int64)
+        L.check(L.load().tf_profile_read(self._h, _ptr(ms), _ptr(cnt), n), "tf_profile_read")
+        return {name: (float(ms[i]), int(cnt[i])) for i, name in enumerate(L.STAGE_NAMES)}
+
     # -- stage entry points (parity tests) ------------------------------------------------
     def stage_preprocess(self, depth):
         """computeDists + bilateral + truncation + pyramid + vertex/normal maps (host depth)."""
