@@ -72,6 +72,20 @@ def cpu_baseline(frames, params_kw, seconds):
     return n / dt, n, dt
 
 
+def combine_ranks(elapsed, frames, device, world):
+    """Whole-job numbers from per-rank ones: the slowest rank's time (MAX) and the frames of all
+    ranks (SUM); one small all-reduce per op over RCCL (gloo in the CPU tests)."""
+    if world <= 1:
+        return float(elapsed), float(frames)
+    import torch
+    import torch.distributed as dist
+    mx = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    sm = torch.tensor([float(frames)], dtype=torch.float64, device=device)
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    return float(mx[0]), float(sm[0])
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -112,17 +126,7 @@ def main():
     prof = tf.profile_read() if not args.no_profile else {}
     st = tf.stats()
 
-    # one RCCL all-reduce: [elapsed (max), frames (sum), fps (sum)]
-    red = torch.tensor([elapsed, float(args.steps), args.steps / elapsed], dtype=torch.float64,
-                       device=f"cuda:{local_rank}")
-    if world > 1:
-        mx = red[0:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = red[1:3].clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed_max, total_frames = float(mx[0]), float(sm[0])
-    else:
-        elapsed_max, total_frames = elapsed, float(args.steps)
+    elapsed_max, total_frames = combine_ranks(elapsed, args.steps, f"cuda:{local_rank}", world)
 
     if rank == 0:
         value = total_frames / elapsed_max

@@ -71,6 +71,8 @@ def lib():
         L.tfo_tsdf_update.argtypes = [P, P, ctypes.c_float, ctypes.c_float, ctypes.c_int]
         L.tfo_sincos.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.tfo_rodrigues.argtypes = [P, P]
+        L.tfo_point_conv.argtypes = [P, P]
+        L.tfo_hash_index.argtypes = [ctypes.c_int] * 4; L.tfo_hash_index.restype = ctypes.c_int
         L.tfo_create.argtypes = [ctypes.POINTER(Params)]; L.tfo_create.restype = P
         L.tfo_destroy.argtypes = [P]
         L.tfo_reset.argtypes = [P]
@@ -308,3 +310,38 @@ class Oracle:
         img = np.empty((self.H, self.W, 4), np.uint8)
         lib().tfo_render_image(self.ctx, ptr(img))
         return img
+
+
+def point_conv(p):
+    out = np.zeros(13, np.float32)
+    lib().tfo_point_conv(ptr(np.ascontiguousarray(p, np.float32)), ptr(out))
+    return out
+
+
+def sincos(th):
+    s, c = ctypes.c_double(), ctypes.c_double()
+    lib().tfo_sincos(float(th), ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+def rodrigues(r):
+    R = np.zeros(9, np.float32)
+    lib().tfo_rodrigues(ptr(np.ascontiguousarray(r, np.float32)), ptr(R))
+    return R.reshape(3, 3)
+
+
+def rigid_mul(a, b):
+    out = np.zeros(12, np.float32)
+    lib().tfo_rigid_mul(ptr(np.ascontiguousarray(a, np.float32).reshape(12)),
+                        ptr(np.ascontiguousarray(b, np.float32).reshape(12)), ptr(out))
+    return out.reshape(3, 4)
+
+
+def rigid_inv(a):
+    out = np.zeros(12, np.float32)
+    lib().tfo_rigid_inv(ptr(np.ascontiguousarray(a, np.float32).reshape(12)), ptr(out))
+    return out.reshape(3, 4)
+
+
+def hash_index(x, y, z, n_buckets=0x100000):
+    return int(lib().tfo_hash_index(int(x), int(y), int(z), int(n_buckets)))

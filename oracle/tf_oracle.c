@@ -1293,3 +1293,25 @@ float* tfo_curr_points(tfo_ctx* c, int l) { return c->curr_pts[l]; }
 float* tfo_curr_normals(tfo_ctx* c, int l) { return c->curr_nrm[l]; }
 uint16_t* tfo_curr_depth(tfo_ctx* c, int l) { return c->depth_pyr[l]; }
 float* tfo_dists(tfo_ctx* c) { return c->dists; }
+
+/* The point conversions used above, exposed for pinning against the reference's own
+ * Vector3f::toShortFloor / toIntFloor(residual) / toIntRound and length()
+ * (Vector.hpp:210-240, 814-824; golden tests/golden/ref_pin_round.bin).
+ * out = {short floor xyz, int floor xyz, residual xyz, round xyz, length}. */
+void tfo_point_conv(const float p[3], float out[13])
+{
+    for (int i = 0; i < 3; ++i) {
+        out[i] = (float)(int16_t)floorf(p[i]);
+        out[3 + i] = (float)(int)floorf(p[i]);
+        out[6 + i] = p[i] - floorf(p[i]);
+        out[9 + i] = (float)iround(p[i]);
+    }
+    out[12] = sqrtf(((0.0f + p[0] * p[0]) + p[1] * p[1]) + p[2] * p[2]);
+}
+
+/* hashIndex (RepresentationAccess.hpp:5-7) for a table of n_buckets (power of two) */
+int tfo_hash_index(int x, int y, int z, int n_buckets)
+{
+    return (int)((((uint32_t)x * 73856093u) ^ ((uint32_t)y * 19349669u) ^ ((uint32_t)z * 83492791u)) &
+                 (uint32_t)(n_buckets - 1));
+}

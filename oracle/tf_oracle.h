@@ -113,6 +113,8 @@ void tfo_sincos(double th, double* s, double* c);
 void tfo_m4v(const float m[16], const float v[4], float r[4]);
 void tfo_tsdf_update(int16_t* sdf, uint8_t* w, float eta, float mu, int maxW);
 void tfo_rodrigues(const float r[3], float R[9]);
+void tfo_point_conv(const float p[3], float out[13]);     /* floor/round/length conversions */
+int  tfo_hash_index(int x, int y, int z, int n_buckets);
 
 /* ---- stateful pipeline (TopFu) ---- */
 typedef struct tfo_ctx tfo_ctx;

@@ -1,0 +1,99 @@
+"""CPU tests of the drop-in boundary: libtfusion_hip.so loads in a GPU-less container,
+exports every function include/tfusion_hip.h declares, its structs match the ctypes mirror
+byte for byte, and the host-only entry points behave (no compute calls without a GPU)."""
+import ctypes
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+from topfusion_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_function():
+    L = _lib.load()
+    names = _lib.header_functions()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_ctypes_signatures_cover_header():
+    """Every declared function has a ctypes signature in topfusion_amd/_lib.py."""
+    src = open(_lib.__file__).read()
+    for n in _lib.header_functions():
+        if n == "tf_debug_icp_ts":
+            continue
+        assert f'"{n}"' in src, n
+
+
+def _c_layout(struct, fields):
+    prog = "#include <stdio.h>\n#include <stddef.h>\n#include \"tfusion_hip.h\"\nint main(void){\n"
+    prog += f'printf("%zu\\n", sizeof({struct}));\n'
+    for f in fields:
+        prog += f'printf("%zu\\n", offsetof({struct}, {f}));\n'
+    prog += "return 0;}\n"
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(prog)
+        exe = os.path.join(d, "l")
+        subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    return [int(v) for v in out]
+
+
+@pytest.mark.parametrize("cls,cname", [(_lib.TfParams, "tf_params"), (_lib.TfStats, "tf_stats")])
+def test_struct_layout_matches_header(cls, cname):
+    fields = [f for f, _ in cls._fields_]
+    got = _c_layout(cname, fields)
+    assert got[0] == ctypes.sizeof(cls)
+    for f, off in zip(fields, got[1:]):
+        assert getattr(cls, f).offset == off, f
+
+
+def test_default_params_match_reference_defaults():
+    """TopFuParams::default_params (topfu.cpp:12-53) via the C-ABI and via the oracle."""
+    from oracle import oracle as O
+    p = _lib.default_params()
+    q = O.default_params()
+    for f, _ in _lib.TfParams._fields_:
+        a, b = getattr(p, f), getattr(q, f)
+        if f == "icp_iter_num":
+            assert list(a) == list(b) == [10, 5, 4, 0]
+        else:
+            assert a == b, f
+    assert (p.cols, p.rows) == (640, 480)
+    assert p.voxelSize == pytest.approx(0.005) and p.mu == pytest.approx(0.02) and p.maxW == 100
+
+
+def test_status_strings_and_invalid_args():
+    L = _lib.load()
+    assert L.tf_status_string(_lib.TF_OK) == b"ok"
+    assert L.tf_status_string(_lib.TF_ICP_FAIL).startswith(b"icp failed")
+    assert L.tf_default_params(None) == _lib.TF_INVALID_ARG
+    ctx = ctypes.c_void_p()
+    assert L.tf_create(None, ctypes.byref(ctx)) == _lib.TF_INVALID_ARG
+    bad = _lib.default_params(n_buckets=1000)          # not a power of two
+    assert L.tf_create(ctypes.byref(bad), ctypes.byref(ctx)) == _lib.TF_INVALID_ARG
+
+
+def test_no_silent_cpu_fallback(monkeypatch):
+    """The product fails loudly when the HIP library is missing."""
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libtfusion_hip.so")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.load()
+
+
+def test_product_does_not_import_oracle():
+    """Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may touch oracle/."""
+    pkg = os.path.join(ROOT, "topfusion_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".hip", ".h", ".cpp", ".hpp")):
+                src = open(os.path.join(dp, f), errors="ignore").read()
+                bad = ("import oracle", "from oracle", "tf_oracle.h", "liboracle", "tfo_")
+                assert not any(b in src for b in bad), f

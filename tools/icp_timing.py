@@ -1,0 +1,24 @@
+"""Per-phase ICP iteration timing (debug build, `make -C topfusion_amd/csrc timing`).
+Run on the GPU box: TFUSION_HIP_LIB=tools/_build/libtfusion_hip_timing.so python tools/icp_timing.py"""
+import ctypes, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch
+from topfusion_amd import TopFu, default_params, synth
+from topfusion_amd import _lib
+W, H = 640, 480
+fx, fy, cx, cy = synth.intrinsics(W, H)
+frames = synth.orbit_sequence(60, W, H, seed=7)
+dev = torch.from_numpy(frames.view(np.int16)).cuda()
+tf = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy), device=0)
+tf.process_frames(dev.data_ptr(), 60)
+torch.cuda.synchronize()
+L = _lib.load()
+ts = (ctypes.c_ulonglong * 16)()
+L.tf_debug_icp_ts(ts)
+n = ts[0]
+names = {1: "ticket won", 2: "final tree loads+LDS", 3: "tree+unpack", 4: "det", 5: "solve", 6: "rodrigues+compose+store"}
+print("launches", n)
+for k in range(1, 7):
+    print(f"{names[k]:28s} cumulative {ts[k] / n * 10 / 1000:8.3f} us (from last-WG entry)")

@@ -8,7 +8,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtfusion_hip.so")
+LIB_PATH = os.environ.get("TFUSION_HIP_LIB") or os.path.join(_HERE, "libtfusion_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tfusion_hip.h")
 
 TF_OK, TF_ICP_FAIL, TF_INVALID_ARG, TF_OOM, TF_HIP_ERROR, TF_NO_DEVICE = range(6)

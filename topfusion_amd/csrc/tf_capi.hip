@@ -91,7 +91,7 @@ static void ctx_free(tf_ctx* c)
     if (!c) return;
     void* bufs[] = { c->hash, c->excessList, c->vba, c->allocList, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->raycast, c->grey,
-                     c->blockBox, c->blockZ, c->blockTiles, c->blockKeep, c->depth_in, c->dists, c->icp_partial, c->st };
+                     c->blockBox, c->blockZ, c->blockTiles, c->blockKeep, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->st };
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (int l = 0; l < TF_LEVELS; ++l) {
         if (c->depth_pyr[l]) (void)hipFree(c->depth_pyr[l]);
@@ -187,7 +187,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         ALLOC(c->prev_pts[l], sizeof(float4) * n);
         ALLOC(c->prev_nrm[l], sizeof(float4) * n);
     }
-    ALLOC(c->icp_partial, sizeof(float) * 28 * (size_t)c->icp_max_cta);
+    ALLOC(c->icp_partial, sizeof(float) * 28 * 256);
+    ALLOC(c->icp_ticket, 64);
     ALLOC(c->st, sizeof(TfDevState));
 #undef ALLOC
     e = hipHostMalloc((void**)&c->st_host, sizeof(TfDevState), hipHostMallocDefault);
@@ -198,6 +199,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     for (int i = 0; i < 12; ++i) s0.pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
     s0.icp_ok = 1;
     e = hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->icp_ticket, 0, 64, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->allocType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->winnerKey, 0xff, sizeof(int) * ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->visType, 0, ntot_pad, c->stream);

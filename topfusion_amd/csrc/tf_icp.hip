@@ -1,19 +1,40 @@
 // tf_icp.hip -- projective point-to-plane ICP for gfx950.
 //
-// One iteration = two launches and no host round trip (the reference syncs to the host
-// and solves with OpenCV 19 times per frame, projective_icp.cpp:187-210):
-//   k_icp_partial : find_coresp + row build (proj_icp.cu:80-117,359-377) and the 27
-//                   products reduced per reference CTA.  A wave64 owns one 32x8 reference
-//                   CTA (4 pixels per lane: tids l, l+64, l+128, l+192) and reproduces the
-//                   reference's 256-wide halving tree (temp_utils.hpp:503-523) with two
-//                   in-register adds + a 6-step xor butterfly: no LDS, no barriers.
-//   k_icp_solve   : icp_final_reduce_kernel (proj_icp.cu:382-403) in the same order,
-//                   then det check (cv::determinant), 6x6 solve, Rodrigues and
-//                   affine = Tinc * affine on the device.
+// ONE launch per ICP iteration and no host round trip (the reference syncs to the host and
+// solves with OpenCV 19 times per frame, projective_icp.cpp:187-210).  k_icp_iter:
+//   * find_coresp + row build (proj_icp.cu:80-117,359-377).  A wave64 owns one 32x8
+//     reference CTA, 4 pixels per lane (reference tids l, l+64, l+128, l+192), and reproduces
+//     the reference's 256-wide halving tree (temp_utils.hpp:503-523) bit for bit: two adds
+//     in registers, then a *transposed* xor butterfly that halves the live sums at every
+//     step (32 lane exchanges for all 27 sums instead of 27 x 6).
+//   * workgroup w owns reference CTAs w, w+256, w+512, ... so it produces exactly the
+//     column sum that thread w of icp_final_reduce_kernel computes (proj_icp.cu:389-391),
+//     in the same order; no [27 x #CTA] partial buffer.
+//   * the last workgroup to finish (agent-scope ticket, write-through sc1 stores/loads,
+//     MI355X_MICROARCH.md "Valid forms" row 1) runs the final 256-wide tree, the det check
+//     (cv::determinant), the 6x6 solve, Rodrigues and affine = Tinc * affine with one wave
+//     holding the 6x7 system one element per lane.
 // A failed det check sets state->abort; every later ICP / scene kernel of the frame no-ops.
 #include "tf_internal.h"
 
-#define ICP_PART_STRIDE 28   // 27 sums padded to 7 float4
+#define ICP_T_STRIDE 28        // 27 column sums per workgroup, padded
+#define ICP_NWG 256            // = FINAL_REDUCE_CTA_SIZE (proj_icp.cu:25-26)
+#define ICP_WAVES 5
+#define ICP_MAX_SLOTS 40       // reference CTAs per workgroup (40*256 CTAs = 2560x1024 pixels)
+
+#ifdef TF_ICP_TIMING
+// debug build only: per-phase wall clock of the last workgroup (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_icp_ts[16];
+#define ICP_TS0() const unsigned long long ts0_ = __builtin_amdgcn_s_memrealtime()
+#define ICP_TS(k) do { if (threadIdx.x == 0) g_icp_ts[k] += __builtin_amdgcn_s_memrealtime() - ts0_; } while (0)
+extern "C" int tf_debug_icp_ts(unsigned long long* out)
+{
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_ts), sizeof(g_icp_ts), 0, hipMemcpyDeviceToHost);
+}
+#else
+#define ICP_TS0()
+#define ICP_TS(k)
+#endif
 
 struct IcpLevel {
     const float4* vcurr; const float4* ncurr; const float4* vprev; const float4* nprev;
@@ -54,95 +75,19 @@ __device__ __forceinline__ bool icp_row(const IcpLevel& L, const float* aff, int
     return true;
 }
 
-__global__ void __launch_bounds__(256)
-k_icp_partial(IcpLevel L, const TfDevState* __restrict__ st, float* __restrict__ partial)
+// One exchange step of the transposed butterfly: lanes with (lane & OFF) keep the upper half
+// of the N live sums, the others the lower half; each kept sum is completed with the
+// partner lane's copy, so every sum sees the same pairings as a full xor butterfly.
+template <int N, int OFF>
+__device__ __forceinline__ void tstep(float* v, int lane)
 {
-    if (st->abort) return;
-    const int lane = threadIdx.x & 63;
-    const int cta = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (cta >= L.nct) return;                       // whole wave exits together
-    float aff[12];
+    const bool hi = (lane & OFF) != 0;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) aff[i] = st->affine[i];
-    const int bx = cta % L.gx, by = cta / L.gx;
-    float r[4][7];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        int t = lane + 64 * j;
-        int x = bx * 32 + (t & 31), y = by * 8 + (t >> 5);
-        if (!icp_row(L, aff, x, y, r[j]))
-#pragma unroll
-            for (int k = 0; k < 7; ++k) r[j][k] = 0.f;
+    for (int j = 0; j < N / 2; ++j) {
+        float send = hi ? v[j] : v[j + N / 2];
+        float keep = hi ? v[j + N / 2] : v[j];
+        v[j] = keep + __shfl_xor(send, OFF, 64);
     }
-    float mine = 0.f;
-    int k = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int b = a; b < 7; ++b, ++k) {
-            // step 128: v[t]+v[t+128]; step 64: + (v[t+64]+v[t+192]); then 32..1
-            float a0 = r[0][a] * r[0][b] + r[2][a] * r[2][b];
-            float a1 = r[1][a] * r[1][b] + r[3][a] * r[3][b];
-            float s = tf_wave_tree64(a0 + a1);
-            if (lane == k) mine = s;
-        }
-    if (lane < 27) partial[cta * ICP_PART_STRIDE + lane] = mine;
-}
-
-// ---- 6x6 algebra (one thread; double where OpenCV's replacement is double) ----------------
-// cv::determinant(Matx66f): LU with partial pivoting in float, eps = 10*FLT_EPSILON
-__device__ double icp_det6(const float* Ain)
-{
-    float A[36];
-    for (int i = 0; i < 36; ++i) A[i] = Ain[i];
-    int p = 1;
-    const float eps = 1.19209290e-07f * 10;
-    for (int i = 0; i < 6; i++) {
-        int k = i;
-        for (int j = i + 1; j < 6; j++)
-            if (fabsf(A[j * 6 + i]) > fabsf(A[k * 6 + i])) k = j;
-        if (fabsf(A[k * 6 + i]) < eps) return 0.0;
-        if (k != i) {
-            for (int j = i; j < 6; j++) { float t = A[i * 6 + j]; A[i * 6 + j] = A[k * 6 + j]; A[k * 6 + j] = t; }
-            p = -p;
-        }
-        float d = -1 / A[i * 6 + i];
-        for (int j = i + 1; j < 6; j++) {
-            float alpha = A[j * 6 + i] * d;
-            for (int c = i + 1; c < 6; c++) A[j * 6 + c] += alpha * A[i * 6 + c];
-        }
-    }
-    double det = p;
-    for (int i = 0; i < 6; i++) det *= A[i * 6 + i];
-    return det;
-}
-
-// cv::solve(A, b, DECOMP_SVD) replacement: Gaussian elimination, partial pivoting, double
-__device__ void icp_solve6(const float* Af, const float* bf, float* x)
-{
-    double A[36], b[6], xs[6];
-    for (int i = 0; i < 36; ++i) A[i] = Af[i];
-    for (int i = 0; i < 6; ++i) b[i] = bf[i];
-    for (int i = 0; i < 6; ++i) {
-        int k = i;
-        for (int j = i + 1; j < 6; ++j) if (fabs(A[j * 6 + i]) > fabs(A[k * 6 + i])) k = j;
-        if (k != i) {
-            for (int j = 0; j < 6; ++j) { double t = A[i * 6 + j]; A[i * 6 + j] = A[k * 6 + j]; A[k * 6 + j] = t; }
-            double t = b[i]; b[i] = b[k]; b[k] = t;
-        }
-        double piv = A[i * 6 + i];
-        for (int j = i + 1; j < 6; ++j) {
-            double l = A[j * 6 + i] / piv;
-            for (int c = i; c < 6; ++c) A[j * 6 + c] = A[j * 6 + c] - l * A[i * 6 + c];
-            b[j] = b[j] - l * b[i];
-        }
-    }
-    for (int i = 5; i >= 0; --i) {
-        double s = b[i];
-        for (int c = i + 1; c < 6; ++c) s = s - A[i * 6 + c] * xs[c];
-        xs[i] = s / A[i * 6 + i];
-    }
-    for (int i = 0; i < 6; ++i) x[i] = (float)xs[i];
 }
 
 __constant__ double c_inv_sin[14] = { 0.0, 1.0/6.0, 1.0/20.0, 1.0/42.0, 1.0/72.0, 1.0/110.0, 1.0/156.0,
@@ -267,69 +212,255 @@ __device__ void tf_set_pose_matrices(TfDevState* st, const float* pose, int allo
     tf_rt_to_m4(pose, st->M_ray);
 }
 
-__global__ void __launch_bounds__(256)
-k_icp_solve(const float* __restrict__ partial, int nct, TfDevState* __restrict__ st, int last_iter)
+
+// ---- 6x6 algebra, register resident: every lane runs the same fully unrolled code on
+// uniform data (static indices only; pivot rows selected by uniform branches) ------------------
+// cv::determinant(Matx66f): LU with partial pivoting in float (eps 10*FLT_EPSILON), pivot
+// product in double -- the operations of the serial LU (see oracle/tf_oracle.c:cv_det6)
+__device__ __forceinline__ double icp_det6_reg(const float (&A0)[6][6])
 {
-    if (st->abort) return;
-    __shared__ float red[27][256];
-    __shared__ float sums[27];
-    const int t = threadIdx.x;
-    // icp_final_reduce_kernel (proj_icp.cu:382-403): per row k, thread t sums t, t+256, ...
-    float s[27];
+    float A[6][6];
 #pragma unroll
-    for (int k = 0; k < 27; ++k) s[k] = 0.f;
-    for (int j = t; j < nct; j += 256) {
-        const float4* p4 = (const float4*)(partial + (size_t)j * ICP_PART_STRIDE);
-        float v[28];
-#pragma unroll
-        for (int q = 0; q < 7; ++q) { float4 f = p4[q]; v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w; }
-#pragma unroll
-        for (int k = 0; k < 27; ++k) s[k] += v[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 27; ++k) red[k][t] = s[k];
-    __syncthreads();
-    const int wave = t >> 6, lane = t & 63;
-    for (int k = wave; k < 27; k += 4) {
-        float a0 = red[k][lane] + red[k][lane + 128];
-        float a1 = red[k][lane + 64] + red[k][lane + 192];
-        float r = tf_wave_tree64(a0 + a1);
-        if (lane == 0) sums[k] = r;
-    }
-    __syncthreads();
-    if (t != 0) return;
-    // StreamHelper::get unpacking (projective_icp.cpp:51-61)
-    float A[36], b[6];
-    int shift = 0;
     for (int i = 0; i < 6; ++i)
-        for (int j = i; j < 7; ++j) {
-            float value = sums[shift++];
-            if (j == 6) b[i] = value;
-            else A[j * 6 + i] = A[i * 6 + j] = value;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) A[i][j] = A0[i][j];
+    const float eps = 1.19209290e-07f * 10;
+    int p = 1;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        float best = fabsf(A[i][i]);
+        int k = i;
+#pragma unroll
+        for (int j = i + 1; j < 6; j++) { float v = fabsf(A[j][i]); if (v > best) { best = v; k = j; } }
+        if (best < eps) return 0.0;
+        if (k != i) {
+#pragma unroll
+            for (int r = i + 1; r < 6; ++r)
+                if (r == k) {
+#pragma unroll
+                    for (int c = i; c < 6; ++c) { float t = A[i][c]; A[i][c] = A[r][c]; A[r][c] = t; }
+                }
+            p = -p;
         }
-    for (int k = 0; k < 27; ++k) st->sums[k] = sums[k];
-    st->icp_iters += 1;
-    double det = icp_det6(A);
-    if (fabs(det) < 1e-15 || isnan(det)) {          // projective_icp.cpp:197-203
-        st->icp_ok = 0;
-        st->abort = 1;
+        float d = -1 / A[i][i];
+#pragma unroll
+        for (int j = i + 1; j < 6; j++) {
+            float alpha = A[j][i] * d;
+#pragma unroll
+            for (int c = i + 1; c < 6; c++) A[j][c] += alpha * A[i][c];
+        }
+    }
+    double det = p;
+#pragma unroll
+    for (int i = 0; i < 6; i++) det *= A[i][i];
+    return det;
+}
+
+// cv::solve(A, b, DECOMP_SVD) replacement: Gaussian elimination with partial pivoting in
+// double, back substitution in the serial order (oracle/tf_oracle.c:solve6)
+__device__ __forceinline__ void icp_solve6_reg(const float (&Af)[6][6], const float (&bf)[6], float (&x)[6])
+{
+    double A[6][6], b[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        b[i] = bf[i];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) A[i][j] = Af[i][j];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double best = fabs(A[i][i]);
+        int k = i;
+#pragma unroll
+        for (int j = i + 1; j < 6; ++j) { double v = fabs(A[j][i]); if (v > best) { best = v; k = j; } }
+        if (k != i) {
+#pragma unroll
+            for (int r = i + 1; r < 6; ++r)
+                if (r == k) {
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) { double t = A[i][c]; A[i][c] = A[r][c]; A[r][c] = t; }
+                    double t = b[i]; b[i] = b[r]; b[r] = t;
+                }
+        }
+        double piv = A[i][i];
+#pragma unroll
+        for (int j = i + 1; j < 6; ++j) {
+            double l = A[j][i] / piv;
+#pragma unroll
+            for (int c = i; c < 6; ++c) A[j][c] = A[j][c] - l * A[i][c];
+            b[j] = b[j] - l * b[i];
+        }
+    }
+    double xs[6];
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        double sacc = b[i];
+#pragma unroll
+        for (int c = i + 1; c < 6; ++c) sacc = sacc - A[i][c] * xs[c];
+        xs[i] = sacc / A[i][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] = (float)xs[i];
+}
+
+__global__ void __launch_bounds__(64 * ICP_WAVES)
+k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsigned* __restrict__ ticket,
+           int nwg, int slots, int last_iter)
+{
+    __shared__ float red[ICP_MAX_SLOTS][ICP_T_STRIDE];
+    __shared__ float tv[27][ICP_NWG];
+    __shared__ int is_last;
+    if (st->abort) return;
+    ICP_TS0();
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    float aff[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) aff[i] = st->affine[i];
+    for (int s = wave; s < slots; s += ICP_WAVES) {
+        const int cta = blockIdx.x + ICP_NWG * s;
+        if (cta >= L.nct) break;
+        const int bx = cta % L.gx, by = cta / L.gx;
+        float r[4][7];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int t = lane + 64 * j;
+            if (!icp_row(L, aff, bx * 32 + (t & 31), by * 8 + (t >> 5), r[j]))
+#pragma unroll
+                for (int k = 0; k < 7; ++k) r[j][k] = 0.f;
+        }
+        // steps 128 and 64 of the halving tree in registers (partial_reduce order, proj_icp.cu:137-356)
+        float v[32];
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = a; b < 7; ++b, ++k) {
+                float a0 = r[0][a] * r[0][b] + r[2][a] * r[2][b];
+                float a1 = r[1][a] * r[1][b] + r[3][a] * r[3][b];
+                v[k] = a0 + a1;
+            }
+#pragma unroll
+        for (int j = 27; j < 32; ++j) v[j] = 0.f;
+        // steps 32..2 transposed, step 1 plain: lane l ends with sum (l >> 1)
+        tstep<32, 32>(v, lane);
+        tstep<16, 16>(v, lane);
+        tstep<8, 8>(v, lane);
+        tstep<4, 4>(v, lane);
+        tstep<2, 2>(v, lane);
+        float tot = v[0] + __shfl_xor(v[0], 1, 64);
+        const int sidx = lane >> 1;
+        if (!(lane & 1) && sidx < 27) red[s][sidx] = tot;
+    }
+    __syncthreads();
+    // column sum of icp_final_reduce_kernel thread blockIdx.x: 0 + P[w] + P[w+256] + ...
+    if (tid < 27) {
+        float sum = 0.f;
+        for (int s = 0; s < slots; ++s) {
+            if (blockIdx.x + ICP_NWG * s >= L.nct) break;
+            sum += red[s][tid];
+        }
+        __hip_atomic_store(&T[blockIdx.x * ICP_T_STRIDE + tid], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (old == (unsigned)nwg - 1);
+    }
+    __syncthreads();
+    if (!is_last) return;
+    ICP_TS(1);
+    // ---- last workgroup: final 256-wide tree over the column sums --------------------------
+    // (write-through sc1 loads: 7 x 16 B per column, aux 16 = sc1)
+    if (tid < ICP_NWG) {
+        float4 q4[7];
+        if (tid < nwg) {
+            __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(T, 0, ICP_NWG * ICP_T_STRIDE * 4, 0x00020000);
+#pragma unroll
+            for (int q = 0; q < 7; ++q) {
+                q4[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                    rs, (tid * ICP_T_STRIDE + 4 * q) * 4, 0, 16));
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 7; ++q) q4[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            tv[4 * q + 0][tid] = q4[q].x;
+            if (4 * q + 1 < 27) tv[4 * q + 1][tid] = q4[q].y;
+            if (4 * q + 2 < 27) tv[4 * q + 2][tid] = q4[q].z;
+            if (4 * q + 3 < 27) tv[4 * q + 3][tid] = q4[q].w;
+        }
+    }
+    __syncthreads();
+    ICP_TS(2);
+    if (wave != 0) return;
+    if (lane == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // halving tree over the 256 columns: steps 128 and 64 from LDS, then the transposed butterfly
+    float v[32];
+#pragma unroll
+    for (int q = 0; q < 27; ++q) {
+        float a0 = tv[q][lane] + tv[q][lane + 128];
+        float a1 = tv[q][lane + 64] + tv[q][lane + 192];
+        v[q] = a0 + a1;
+    }
+#pragma unroll
+    for (int q = 27; q < 32; ++q) v[q] = 0.f;
+    tstep<32, 32>(v, lane);
+    tstep<16, 16>(v, lane);
+    tstep<8, 8>(v, lane);
+    tstep<4, 4>(v, lane);
+    tstep<2, 2>(v, lane);
+    const float tot = v[0] + __shfl_xor(v[0], 1, 64);     // lane l holds sum (l >> 1)
+    float sm[27];
+#pragma unroll
+    for (int q = 0; q < 27; ++q) sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), 2 * q));
+    if (lane < 27) st->sums[lane] = __shfl(tot, 2 * lane, 64);
+    if (lane == 0) st->icp_iters += 1;
+    // StreamHelper::get unpacking (projective_icp.cpp:51-61)
+    float Am[6][6], bv[6];
+    {
+        int shift = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = i; j < 7; ++j) {
+                float value = sm[shift++];
+                if (j == 6) bv[i] = value;
+                else { Am[j][i] = value; Am[i][j] = value; }
+            }
+    }
+    ICP_TS(3);
+    double det = icp_det6_reg(Am);
+    ICP_TS(4);
+    if (fabs(det) < 1e-15 || isnan(det)) {                     // projective_icp.cpp:197-203
+        if (lane == 0) { st->icp_ok = 0; st->abort = 1; }
         return;
     }
-    float r[6], R[9], tinc[12], aff[12];
-    icp_solve6(A, b, r);
-    icp_rodrigues(r, R);
+    float rv[6];
+    icp_solve6_reg(Am, bv, rv);
+    ICP_TS(5);
+    float R[9], tinc[12], A[12];
+    icp_rodrigues(rv, R);
+#pragma unroll
     for (int j = 0; j < 3; ++j) {
         tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1]; tinc[j * 4 + 2] = R[j * 3 + 2];
-        tinc[j * 4 + 3] = r[3 + j];
+        tinc[j * 4 + 3] = rv[3 + j];
     }
-    for (int i = 0; i < 12; ++i) aff[i] = st->affine[i];
-    tf_rigid_mul(tinc, aff, aff);
-    for (int i = 0; i < 12; ++i) st->affine[i] = aff[i];
-    if (last_iter == 1) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) A[i] = aff[i];
+    tf_rigid_mul(tinc, A, A);
+    if (lane < 12) st->affine[lane] = A[lane];
+    ICP_TS(6);
+#ifdef TF_ICP_TIMING
+    if (threadIdx.x == 0) g_icp_ts[0] += 1;
+#endif
+    if (last_iter == 1 && lane == 0) {
         // poses_.push_back(poses_.back() * affine) (topfu.cpp:243) and the derived matrices
         float pose[12];
         for (int i = 0; i < 12; ++i) pose[i] = st->pose[i];
-        tf_rigid_mul(pose, aff, pose);
+        tf_rigid_mul(pose, A, pose);
         for (int i = 0; i < 12; ++i) st->pose[i] = pose[i];
         tf_set_pose_matrices(st, pose, 1);
     }
@@ -373,7 +504,7 @@ hipError_t tfk_frame0_matrices(tf_ctx* c)
     return hipGetLastError();
 }
 
-// estimateTransform (projective_icp.cpp:169-213): levels coarse -> fine
+// estimateTransform (projective_icp.cpp:169-213): levels coarse -> fine, one launch per iteration
 hipError_t tfk_icp(tf_ctx* c, int pose_update)
 {
     const tf_params& p = c->p;
@@ -392,10 +523,13 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update)
         L.nct = L.gx * ((L.H + 7) / 8);
         L.fx = p.fx / (float)div; L.fy = p.fy / (float)div; L.cx = p.cx / (float)div; L.cy = p.cy / (float)div;
         L.min_cosine = c->min_cosine; L.dist2 = c->dist2_thres;
+        const int nwg = L.nct < ICP_NWG ? L.nct : ICP_NWG;
+        const int slots = (L.nct + ICP_NWG - 1) / ICP_NWG;
+        if (slots > ICP_MAX_SLOTS) return hipErrorInvalidValue;
         for (int it = 0; it < p.icp_iter_num[l]; ++it) {
-            hipLaunchKernelGGL(k_icp_partial, dim3((L.nct + 3) / 4), dim3(256), 0, c->stream, L, c->st, c->icp_partial);
             int last = (pose_update && l == last_l && it == p.icp_iter_num[l] - 1) ? 1 : 0;
-            hipLaunchKernelGGL(k_icp_solve, dim3(1), dim3(256), 0, c->stream, c->icp_partial, L.nct, c->st, last);
+            hipLaunchKernelGGL(k_icp_iter, dim3(nwg), dim3(64 * ICP_WAVES), 0, c->stream, L, c->st, c->icp_partial,
+                               c->icp_ticket, nwg, slots, last);
         }
     }
     return hipGetLastError();

@@ -178,7 +178,8 @@ struct tf_ctx {
     float4* prev_pts[TF_LEVELS];
     float4* prev_nrm[TF_LEVELS];
     // ICP
-    float* icp_partial;      // [27][max CTAs]
+    float* icp_partial;      // [256][28] column sums
+    unsigned* icp_ticket;    // last-workgroup ticket (zero between launches)
     int icp_max_cta;
     float min_cosine, dist2_thres;
     // device state
