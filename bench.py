@@ -43,8 +43,10 @@ def parse():
 
 def stage_bytes(stage, p, nvis, W, H):
     """Algorithmic HBM bytes of ONE launch of a stage."""
-    if stage in ("raycast_render", "raycast_icp"):
+    if stage == "raycast_icp":
         return W * H * 16 + nvis * (2048 + 16)          # ray output float4 + every visible block once
+    if stage == "raycast_render":
+        return W * H * 4 + nvis * (2048 + 16)           # fused raycast + grey: uchar4 out + blocks once
     if stage == "integrate":
         return nvis * (4096 + 20) + W * H * 4           # voxel R+W + entry/id + depth image
     if stage == "grey":

@@ -128,6 +128,10 @@ tf_status tf_get_stats(tf_ctx* ctx, tf_stats* stats);
 tf_status tf_get_params(tf_ctx* ctx, tf_params* p);
 /* HIP stream owned by the context (hipStream_t), for interop */
 void*     tf_get_stream(tf_ctx* ctx);
+/* execution schedule chosen at tf_create (no reference counterpart): 1 when ICP runs as one
+ * persistent launch per frame (k_icp_frame), 0 for one launch per iteration; the environment
+ * variable TFUSION_ICP_PERSISTENT=0 forces the latter */
+tf_status tf_get_schedule(tf_ctx* ctx, int* icp_persistent);
 
 /* ---- stage entry points (operate on context state; parity tests) ------------- */
 /* computeDists + depthBilateralFilter + depthTruncation + depthBuildPyramid +

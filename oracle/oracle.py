@@ -87,7 +87,7 @@ def lib():
         L.tfo_render_grey.argtypes = [P, P, P]
         L.tfo_render_image.argtypes = [P, P]
         for name in ("tfo_hash", "tfo_vba", "tfo_visible_ids", "tfo_visible_type", "tfo_range_image",
-                     "tfo_raycast_result", "tfo_dists"):
+                     "tfo_raycast_result", "tfo_dists", "tfo_frame_grey"):
             getattr(L, name).argtypes = [P]; getattr(L, name).restype = P
         for name in ("tfo_prev_points", "tfo_prev_normals", "tfo_curr_points", "tfo_curr_normals", "tfo_curr_depth"):
             getattr(L, name).argtypes = [P, ctypes.c_int]; getattr(L, name).restype = P
@@ -257,6 +257,9 @@ class Oracle:
 
     def raycast_result(self):
         return self._view(lib().tfo_raycast_result(self.ctx), np.float32, self.W * self.H * 4, (self.H, self.W, 4)).copy()
+
+    def frame_grey(self):
+        return self._view(lib().tfo_frame_grey(self.ctx), np.uint8, self.W * self.H * 4, (self.H, self.W, 4)).copy()
 
     def dists(self):
         return self._view(lib().tfo_dists(self.ctx), np.float32, self.W * self.H, (self.H, self.W)).copy()

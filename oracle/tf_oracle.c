@@ -521,6 +521,7 @@ struct tfo_ctx {
     int frame_counter;
     float pose[12];
     float* dists;
+    uint8_t* frame_grey;      /* the image renderImage produced inside the last tracked frame */
     uint16_t* depth_pyr[3];
     float* curr_pts[3]; float* curr_nrm[3];
     float* prev_pts[3]; float* prev_nrm[3];
@@ -560,6 +561,7 @@ tfo_ctx* tfo_create(const tfo_params* p)
     for (size_t i = 0; i < npx; ++i) { c->range[2 * i] = p->viewFrustum_min; c->range[2 * i + 1] = p->viewFrustum_max; } /* RenderState.hpp:56-76 */
     c->raycast = (float*)calloc(4 * npx, sizeof(float));
     c->dists = (float*)calloc(npx, sizeof(float));
+    c->frame_grey = (uint8_t*)calloc(npx * 4, 1);
     int w = p->cols, h = p->rows;
     for (int l = 0; l < 3; ++l) {
         c->lvl_w[l] = w; c->lvl_h[l] = h;
@@ -580,7 +582,7 @@ void tfo_destroy(tfo_ctx* c)
 {
     if (!c) return;
     free(c->hash); free(c->excessList); free(c->vba); free(c->allocList); free(c->allocType);
-    free(c->blockCoords); free(c->visibleIds); free(c->visType); free(c->range); free(c->raycast); free(c->dists);
+    free(c->blockCoords); free(c->visibleIds); free(c->visType); free(c->range); free(c->raycast); free(c->dists); free(c->frame_grey);
     for (int l = 0; l < 3; ++l) {
         free(c->depth_pyr[l]); free(c->curr_pts[l]); free(c->curr_nrm[l]); free(c->prev_pts[l]); free(c->prev_nrm[l]);
     }
@@ -1256,9 +1258,7 @@ int tfo_process_frame(tfo_ctx* c, const uint16_t* depth)
     tfo_alloc(c, pinv, c->dists);
     tfo_integrate(c, pinv, c->dists);
     /* renderImage(image): raycast with the (stale) range image + grey shading (topfu.cpp:284-288) */
-    uint8_t* img = (uint8_t*)malloc((size_t)W * H * 4);
-    tfo_render_image(c, img);
-    free(img);
+    tfo_render_image(c, c->frame_grey);
     tfo_expected_depths(c, pinv);
     create_icp_maps(c);
     for (int l = 1; l < 3; ++l)
@@ -1292,6 +1292,7 @@ float* tfo_prev_normals(tfo_ctx* c, int l) { return c->prev_nrm[l]; }
 float* tfo_curr_points(tfo_ctx* c, int l) { return c->curr_pts[l]; }
 float* tfo_curr_normals(tfo_ctx* c, int l) { return c->curr_nrm[l]; }
 uint16_t* tfo_curr_depth(tfo_ctx* c, int l) { return c->depth_pyr[l]; }
+uint8_t* tfo_frame_grey(tfo_ctx* c) { return c->frame_grey; }
 float* tfo_dists(tfo_ctx* c) { return c->dists; }
 
 /* The point conversions used above, exposed for pinning against the reference's own

@@ -145,6 +145,7 @@ float* tfo_curr_points(tfo_ctx* c, int level);
 float* tfo_curr_normals(tfo_ctx* c, int level);
 uint16_t* tfo_curr_depth(tfo_ctx* c, int level);
 float* tfo_dists(tfo_ctx* c);
+uint8_t* tfo_frame_grey(tfo_ctx* c);    /* W*H rgba: renderImage inside the last tracked frame */
 
 #ifdef __cplusplus
 }

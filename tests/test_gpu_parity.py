@@ -105,8 +105,9 @@ def test_stage_raycast_maps_grey(oracle_mod):
     assert_bit_exact("grey", g.stage_render_grey(pose), o.render_grey(pose))
 
 
-def test_icp_stage(oracle_mod):
+def test_icp_stage(oracle_mod, icp_schedule):
     g, o = make_pair(oracle_mod)
+    _check_schedule(g, icp_schedule)
     seq = synth.orbit_sequence(2, seed=5)
     # prev = frame-0 camera maps, curr = frame-1 maps (the reference's frame-1 situation)
     g.stage_preprocess(seq[0])
@@ -140,6 +141,17 @@ def test_icp_stage(oracle_mod):
     assert_bit_exact("icp affine", aff.reshape(12), affine)
 
 
+@pytest.fixture(params=["persistent", "per_iteration"])
+def icp_schedule(request, monkeypatch):
+    """Run a test under both ICP schedules (tf_create reads TFUSION_ICP_PERSISTENT)."""
+    monkeypatch.setenv("TFUSION_ICP_PERSISTENT", "1" if request.param == "persistent" else "0")
+    return request.param
+
+
+def _check_schedule(g, sched):
+    assert g.icp_persistent() == (sched == "persistent")
+
+
 def _cosf(x):
     import ctypes
     libm = ctypes.CDLL("libm.so.6")
@@ -149,9 +161,10 @@ def _cosf(x):
 
 
 @pytest.mark.parametrize("cols,rows,nframes", [(640, 480, 6), (320, 240, 16)])
-def test_sequence(oracle_mod, cols, rows, nframes):
+def test_sequence(oracle_mod, cols, rows, nframes, icp_schedule):
     """Whole TopFu::operator() frames: state identical after every frame."""
     g, o = make_pair(oracle_mod, cols, rows)
+    _check_schedule(g, icp_schedule)
     seq = synth.orbit_sequence(nframes, cols, rows, seed=7)
     for k in range(nframes):
         okg = g(seq[k])
@@ -163,6 +176,8 @@ def test_sequence(oracle_mod, cols, rows, nframes):
         if k > 0:
             assert sg["noTotalBlocks"] == so["noTotalBlocks"], f"frame {k} noTotalBlocks"
         assert_bit_exact(f"frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
+        if k > 0 and oko:
+            assert_bit_exact(f"frame {k} renderImage grey", g.frame_grey(), o.frame_grey())
     compare_scene(g, o, "final")
     assert_bit_exact("final raycast", g.raycast_result(), o.raycast_result())
     for l in range(3):
@@ -172,9 +187,10 @@ def test_sequence(oracle_mod, cols, rows, nframes):
         assert_bit_exact(f"final prev normals L{l}", gn, on)
 
 
-def test_icp_failure_reset(oracle_mod):
+def test_icp_failure_reset(oracle_mod, icp_schedule):
     """A frame without correspondences fails the det check -> reset (topfu.cpp:263-264)."""
     g, o = make_pair(oracle_mod, 320, 240)
+    _check_schedule(g, icp_schedule)
     seq = synth.orbit_sequence(3, 320, 240, seed=9)
     empty = np.zeros_like(seq[0])
     frames = [seq[0], seq[1], empty, seq[2], seq[0]]

@@ -17,8 +17,15 @@ torch.cuda.synchronize()
 L = _lib.load()
 ts = (ctypes.c_ulonglong * 16)()
 L.tf_debug_icp_ts(ts)
-n = ts[0]
+n = max(ts[0], 1)
 names = {1: "ticket won", 2: "final tree loads+LDS", 3: "tree+unpack", 4: "det", 5: "solve", 6: "rodrigues+compose+store"}
 print("launches", n)
 for k in range(1, 7):
     print(f"{names[k]:28s} cumulative {ts[k] / n * 10 / 1000:8.3f} us (from last-WG entry)")
+
+m = ts[7]
+if m:
+    print("persistent iterations", m)
+    for k, name in ((8, "WG0 own column published"), (9, "WG0 all 256 columns gathered"), (10, "WG0 tail done"),
+                    (12, "WG255 own column published"), (13, "WG255 broadcast seen")):
+        print(f"{name:30s} {ts[k] / m * 10 / 1000:8.3f} us after iteration start")

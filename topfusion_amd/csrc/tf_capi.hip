@@ -89,9 +89,9 @@ static bool params_valid(const tf_params* p)
 static void ctx_free(tf_ctx* c)
 {
     if (!c) return;
-    void* bufs[] = { c->hash, c->excessList, c->vba, c->allocList, c->allocType, c->winnerKey, c->allocCounts,
+    void* bufs[] = { c->hash, c->excessList, c->vba, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->raycast, c->grey,
-                     c->blockBox, c->blockZ, c->blockTiles, c->blockKeep, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->st };
+                     c->blockBox, c->blockZ, c->blockTiles, c->blockKeep, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st };
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (int l = 0; l < TF_LEVELS; ++l) {
         if (c->depth_pyr[l]) (void)hipFree(c->depth_pyr[l]);
@@ -163,6 +163,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->excessList, sizeof(int) * (size_t)pin->n_excess);
     ALLOC(c->vba, sizeof(TfVoxel) * (size_t)pin->n_blocks * TF_BLK3);
     ALLOC(c->allocList, sizeof(int) * (size_t)pin->n_blocks);
+    ALLOC(c->bgrid, sizeof(int2) * (size_t)TF_GRID_DIM * TF_GRID_DIM * TF_GRID_DIM);
     ALLOC(c->allocType, ntot_pad);
     ALLOC(c->winnerKey, sizeof(int) * ntot_pad);
     ALLOC(c->allocCounts, sizeof(int) * 2 * (size_t)c->alloc_chunks);
@@ -189,6 +190,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     }
     ALLOC(c->icp_partial, sizeof(float) * 28 * 256);
     ALLOC(c->icp_ticket, 64);
+    ALLOC(c->icp_tagged, sizeof(unsigned long long) * (256 * 28 + 16));
     ALLOC(c->st, sizeof(TfDevState));
 #undef ALLOC
     e = hipHostMalloc((void**)&c->st_host, sizeof(TfDevState), hipHostMallocDefault);
@@ -200,6 +202,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     s0.icp_ok = 1;
     e = hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_ticket, 0, 64, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->bgrid, 0xff, sizeof(int2) * (size_t)TF_GRID_DIM * TF_GRID_DIM * TF_GRID_DIM, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->icp_tagged, 0, sizeof(unsigned long long) * (256 * 28 + 16), c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->allocType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->winnerKey, 0xff, sizeof(int) * ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->visType, 0, ntot_pad, c->stream);
@@ -225,6 +229,10 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     e = tfk_reset_scene(c);                              // topfu.cpp:75
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    {   // ICP schedule: one persistent launch per frame when all its workgroups fit at once
+        const char* env = getenv("TFUSION_ICP_PERSISTENT");
+        c->icp_persistent = (env && env[0] == '0') ? 0 : tfk_icp_persistent_ok(c);
+    }
     *out = c;
     return TF_OK;
 }
@@ -296,8 +304,7 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, b
     STAGE(TF_STAGE_ICP, tfk_icp(c, 1));                              // topfu.cpp:242-243
     STAGE(TF_STAGE_ALLOC, tfk_alloc(c));                             // topfu.cpp:281
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c));                     // topfu.cpp:282
-    STAGE(TF_STAGE_RAYCAST_RENDER, tfk_raycast(c, 0));               // renderImage, topfu.cpp:284-285
-    STAGE(TF_STAGE_GREY, tfk_render_grey(c));
+    STAGE(TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c));            // renderImage (raycast + grey), topfu.cpp:284-285
     STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c));         // topfu.cpp:306
     STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));                  // CreateICPMaps, topfu.cpp:307
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps(c));                       // + resizePointsNormals :308-309
@@ -310,6 +317,7 @@ static tf_status finish_frame(tf_ctx* c, bool tracked)
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
     prof_collect(c);
+    if (c->st_host->icp_ok < 0) return TF_HIP_ERROR;                  // persistent ICP lost a peer
     if (tracked && !c->st_host->icp_ok) {                            // topfu.cpp:263-264
         s = ctx_reset(c);
         if (s != TF_OK) return s;
@@ -446,6 +454,13 @@ extern "C" tf_status tf_get_params(tf_ctx* c, tf_params* p)
 
 extern "C" void* tf_get_stream(tf_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+extern "C" tf_status tf_get_schedule(tf_ctx* c, int* icp_persistent)
+{
+    if (!c) return TF_INVALID_ARG;
+    if (icp_persistent) *icp_persistent = c->icp_persistent;
+    return TF_OK;
+}
+
 // ---- stage entry points ---------------------------------------------------------------
 static tf_status set_pose_in(tf_ctx* c, const float* rt, int mode)
 {
@@ -480,6 +495,7 @@ extern "C" tf_status tf_stage_icp(tf_ctx* c, float affine_rt[12], int* ok, int* 
     TF_CHECK(tfk_icp(c, 0));
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
+    if (c->st_host->icp_ok < 0) return TF_HIP_ERROR;
     if (affine_rt) memcpy(affine_rt, c->st_host->affine, sizeof(float) * 12);
     if (ok) *ok = c->st_host->icp_ok;
     if (iterations) *iterations = c->st_host->icp_iters;
@@ -611,6 +627,7 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
     void* p = buffer_ptr(c, which, level, &n);
     if (!p || n != bytes) return TF_INVALID_ARG;
     TF_CHECK(hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
+    if (which == TF_BUF_HASH) TF_CHECK(tfk_grid_rebuild(c));       // keep the block grid exact
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }

@@ -16,6 +16,7 @@
 //     holding the 6x7 system one element per lane.
 // A failed det check sets state->abort; every later ICP / scene kernel of the frame no-ops.
 #include "tf_internal.h"
+#include <string.h>
 
 #define ICP_T_STRIDE 28        // 27 column sums per workgroup, padded
 #define ICP_NWG 256            // = FINAL_REDUCE_CTA_SIZE (proj_icp.cu:25-26)
@@ -31,9 +32,13 @@ extern "C" int tf_debug_icp_ts(unsigned long long* out)
 {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_ts), sizeof(g_icp_ts), 0, hipMemcpyDeviceToHost);
 }
+#define IPT_NOW() __builtin_amdgcn_s_memrealtime()
+#define IPT_ADD(k, v) do { if (threadIdx.x == 0) g_icp_ts[k] += (v); } while (0)
 #else
 #define ICP_TS0()
 #define ICP_TS(k)
+#define IPT_NOW() 0ull
+#define IPT_ADD(k, v) do { } while (0)
 #endif
 
 struct IcpLevel {
@@ -466,6 +471,349 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
     }
 }
 
+// =========================================================================================
+// Persistent ICP: ONE launch per frame for all levels and iterations.
+//
+// 256 workgroups x 8 waves stay resident.  Workgroup w owns reference CTAs w, w+256, ... of
+// every level (the column of icp_final_reduce_kernel it reproduces); its current-frame maps
+// stay in registers for the whole level, so an iteration costs one dependent gather (previous
+// maps) instead of a launch plus four dependent loads.  Cross-workgroup exchange uses 64-bit
+// TAGGED slots: each value is stored as (generation << 32 | float bits) with one agent-scope
+// (sc1) 8-byte atomic store, so a reader that sees the current generation also sees the data
+// -- no ticket counter, no fence.  Workgroup 0 polls the 256 column sums, runs the final tree,
+// det (wave 1) and solve/Rodrigues/compose (wave 0) concurrently, and broadcasts the new affine
+// as 13 tagged slots that the other workgroups poll.  Every spin is bounded (status 2 -> the
+// host reports a HIP error) so no wave can outlive a missing peer.
+// =========================================================================================
+#define IP_WAVES 8
+#define IP_SREG 1                       // CTA slots kept in registers per wave (8 per WG; larger images use k_icp_iter)
+#define IP_SPIN_LIMIT (1u << 21)
+#define IP_BCAST (ICP_NWG * ICP_T_STRIDE)
+
+struct IcpFrameArgs {
+    IcpLevel lv[TF_LEVELS];             // in processing order (coarse -> fine)
+    int iters[TF_LEVELS];
+    int slots[TF_LEVELS];
+    int nlev;
+    int total_iters;
+    int pose_update;
+    TfDevState* st;
+    unsigned long long* tag;            // [256][28] column sums, then [16] broadcast
+};
+
+__device__ __forceinline__ unsigned long long ip_pack(unsigned gen, float v)
+{
+    return ((unsigned long long)gen << 32) | (unsigned long long)__float_as_uint(v);
+}
+__device__ __forceinline__ void ip_store(unsigned long long* p, unsigned long long v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ip_load(const unsigned long long* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// rows of one pixel (same arithmetic as icp_row), with the current-frame point/normal in
+// registers and both previous-map loads issued before any of the dependent tests
+struct IpPix { float vx, vy, vz, nx, ny, nz; };
+
+__device__ __forceinline__ void ip_rows4(const IcpLevel& L, const float* aff, const IpPix (&px)[4],
+                                         const int (&xy)[4], float (&r)[4][7])
+{
+    tf3 R0 = mk3(aff[0], aff[1], aff[2]), R1 = mk3(aff[4], aff[5], aff[6]), R2 = mk3(aff[8], aff[9], aff[10]);
+    tf3 s[4];
+    bool ok[4];
+    int idx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        tf3 v = mk3(px[j].vx, px[j].vy, px[j].vz);
+        ok[j] = xy[j] >= 0 && !isnan(v.x);
+        s[j] = mk3(kdot(R0, v) + aff[3], kdot(R1, v) + aff[7], kdot(R2, v) + aff[11]);
+        float coox = fmaf(L.fx, s[j].x / s[j].z, L.cx);
+        float cooy = fmaf(L.fy, s[j].y / s[j].z, L.cy);
+        ok[j] = ok[j] && !(s[j].z <= 0 || coox < 0 || cooy < 0 || coox >= (float)L.W || cooy >= (float)L.H);
+        idx[j] = ok[j] ? (int)floorf(cooy) * L.W + (int)floorf(coox) : 0;
+    }
+    float4 dp[4], ndp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { dp[j] = L.vprev[idx[j]]; ndp[j] = L.nprev[idx[j]]; }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        tf3 d = mk3(dp[j].x, dp[j].y, dp[j].z);
+        bool good = ok[j] && !isnan(d.x);
+        tf3 sd = sub3(s[j], d);
+        good = good && !(kdot(sd, sd) > L.dist2);
+        tf3 nc = mk3(px[j].nx, px[j].ny, px[j].nz);
+        tf3 ns = mk3(kdot(R0, nc), kdot(R1, nc), kdot(R2, nc));
+        tf3 nd = mk3(ndp[j].x, ndp[j].y, ndp[j].z);
+        good = good && !(fabsf(kdot(ns, nd)) < L.min_cosine);
+        tf3 cr = kcross(s[j], nd);
+        float b = kdot(nd, sub3(d, s[j]));
+        r[j][0] = good ? cr.x : 0.f; r[j][1] = good ? cr.y : 0.f; r[j][2] = good ? cr.z : 0.f;
+        r[j][3] = good ? nd.x : 0.f; r[j][4] = good ? nd.y : 0.f; r[j][5] = good ? nd.z : 0.f;
+        r[j][6] = good ? b : 0.f;
+    }
+}
+
+// 256-pixel CTA reduction (partial_reduce order): lane l ends holding sum (l >> 1)
+__device__ __forceinline__ float ip_cta_reduce(const float (&r)[4][7], int lane)
+{
+    float v[32];
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = a; b < 7; ++b, ++k) {
+            float a0 = r[0][a] * r[0][b] + r[2][a] * r[2][b];
+            float a1 = r[1][a] * r[1][b] + r[3][a] * r[3][b];
+            v[k] = a0 + a1;
+        }
+#pragma unroll
+    for (int j = 27; j < 32; ++j) v[j] = 0.f;
+    tstep<32, 32>(v, lane);
+    tstep<16, 16>(v, lane);
+    tstep<8, 8>(v, lane);
+    tstep<4, 4>(v, lane);
+    tstep<2, 2>(v, lane);
+    return v[0] + __shfl_xor(v[0], 1, 64);
+}
+
+// final 256-wide tree of the column sums in LDS -> the 27 sums in every lane (uniform)
+__device__ __forceinline__ void ip_final_tree(const float (*tv)[ICP_NWG], int lane, float (&sm)[27])
+{
+    float v[32];
+#pragma unroll
+    for (int q = 0; q < 27; ++q) {
+        float a0 = tv[q][lane] + tv[q][lane + 128];
+        float a1 = tv[q][lane + 64] + tv[q][lane + 192];
+        v[q] = a0 + a1;
+    }
+#pragma unroll
+    for (int q = 27; q < 32; ++q) v[q] = 0.f;
+    tstep<32, 32>(v, lane);
+    tstep<16, 16>(v, lane);
+    tstep<8, 8>(v, lane);
+    tstep<4, 4>(v, lane);
+    tstep<2, 2>(v, lane);
+    const float tot = v[0] + __shfl_xor(v[0], 1, 64);
+#pragma unroll
+    for (int q = 0; q < 27; ++q)
+        sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), 2 * q));
+}
+
+__device__ __forceinline__ void ip_unpack(const float (&sm)[27], float (&Am)[6][6], float (&bv)[6])
+{   // StreamHelper::get (projective_icp.cpp:51-61)
+    int shift = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = i; j < 7; ++j) {
+            float value = sm[shift++];
+            if (j == 6) bv[i] = value;
+            else { Am[j][i] = value; Am[i][j] = value; }
+        }
+}
+
+__global__ void __launch_bounds__(64 * IP_WAVES)
+k_icp_frame(IcpFrameArgs a)
+{
+    __shared__ float red[IP_WAVES * IP_SREG][ICP_T_STRIDE];
+    __shared__ float tv[27][ICP_NWG];
+    __shared__ float aff_s[12];
+    __shared__ int status_s, det_ok_s;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, wg = blockIdx.x;
+    TfDevState* st = a.st;
+    unsigned long long* tag = a.tag;
+    const unsigned base = st->icp_gen;
+    unsigned gen = base;
+    float aff[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) aff[i] = (i % 5 == 0) ? 1.0f : 0.0f;     // affine = Identity
+    int status = 1, done = 0;
+    float last_sums = 0.f;
+
+#pragma unroll 1
+    for (int li = 0; li < a.nlev && status == 1; ++li) {
+        // uniform selects instead of a dynamic index into the kernel arguments (no scratch copy)
+        const IcpLevel L = li == 0 ? a.lv[0] : (li == 1 ? a.lv[1] : a.lv[2]);
+        const int slots = li == 0 ? a.slots[0] : (li == 1 ? a.slots[1] : a.slots[2]);
+        // current-frame maps of my CTA slots -> registers (constant over the level)
+        IpPix px[IP_SREG][4];
+        int xy[IP_SREG][4];
+#pragma unroll
+        for (int rr = 0; rr < IP_SREG; ++rr) {
+            const int sl = wave + IP_WAVES * rr;
+            const int cta = wg + ICP_NWG * sl;
+            const bool live = sl < slots && cta < L.nct;
+            const int bx = live ? cta % L.gx : 0, by = live ? cta / L.gx : 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int t = lane + 64 * j;
+                const int x = bx * 32 + (t & 31), y = by * 8 + (t >> 5);
+                const bool in = live && x < L.W && y < L.H;
+                xy[rr][j] = in ? 1 : -1;
+                float4 v = in ? L.vcurr[y * L.W + x] : make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 n = in ? L.ncurr[y * L.W + x] : make_float4(0.f, 0.f, 0.f, 0.f);
+                px[rr][j].vx = v.x; px[rr][j].vy = v.y; px[rr][j].vz = v.z;
+                px[rr][j].nx = n.x; px[rr][j].ny = n.y; px[rr][j].nz = n.z;
+            }
+        }
+        const int iters = li == 0 ? a.iters[0] : (li == 1 ? a.iters[1] : a.iters[2]);
+#pragma unroll 1
+        for (int it = 0; it < iters; ++it) {
+            ++gen;
+            const unsigned long long t_it = IPT_NOW(); (void)t_it;
+            // ---- per-CTA reductions -> column sum of this workgroup -> tagged slot
+#pragma unroll
+            for (int rr = 0; rr < IP_SREG; ++rr) {
+                const int sl = wave + IP_WAVES * rr;
+                if (sl < slots && wg + ICP_NWG * sl < L.nct) {
+                    float r[4][7];
+                    ip_rows4(L, aff, px[rr], xy[rr], r);
+                    const float tot = ip_cta_reduce(r, lane);
+                    if (!(lane & 1) && (lane >> 1) < 27) red[sl][lane >> 1] = tot;
+                }
+            }
+            __syncthreads();
+            if (tid < 27) {
+                float sum = 0.f;                                   // 0 + P[w] + P[w+256] + ...
+                for (int sl = 0; sl < slots; ++sl) {
+                    if (wg + ICP_NWG * sl >= L.nct) break;
+                    sum += red[sl][tid];
+                }
+                ip_store(&tag[wg * ICP_T_STRIDE + tid], ip_pack(gen, sum));
+            }
+            if (wg == 0 || wg == ICP_NWG - 1) IPT_ADD(wg == 0 ? 8 : 12, IPT_NOW() - t_it);
+            if (wg == 0) {
+                // ---- gather the 256 column sums (tagged polling; all loads in flight at once)
+                constexpr int PER = (ICP_NWG * 27 + 64 * IP_WAVES - 1) / (64 * IP_WAVES);
+                unsigned long long v[PER];
+#pragma unroll
+                for (int k = 0; k < PER; ++k) {
+                    const int e = tid + 64 * IP_WAVES * k;
+                    const int col = e / 27, q = e - col * 27;
+                    v[k] = e < ICP_NWG * 27 ? ip_load(&tag[col * ICP_T_STRIDE + q]) : ((unsigned long long)gen << 32);
+                }
+                bool timeout = false;
+                for (unsigned spins = 0;; ++spins) {
+                    bool ready = true;
+#pragma unroll
+                    for (int k = 0; k < PER; ++k) {
+                        if ((unsigned)(v[k] >> 32) != gen) {
+                            ready = false;
+                            const int e = tid + 64 * IP_WAVES * k;
+                            const int col = e / 27, q = e - col * 27;
+                            v[k] = ip_load(&tag[col * ICP_T_STRIDE + q]);
+                        }
+                    }
+                    if (ready) break;
+                    if (spins > IP_SPIN_LIMIT) { timeout = true; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+#pragma unroll
+                for (int k = 0; k < PER; ++k) {
+                    const int e = tid + 64 * IP_WAVES * k;
+                    const int col = e / 27, q = e - col * 27;
+                    if (e < ICP_NWG * 27) tv[q][col] = __uint_as_float((unsigned)v[k]);
+                }
+                if (tid == 0) det_ok_s = 1;
+                const int any_timeout = __syncthreads_or(timeout);
+                IPT_ADD(9, IPT_NOW() - t_it);
+                if (!any_timeout) {
+                    if (wave == 1) {                                   // det on its own wave
+                        float sm[27], Am[6][6], bv[6];
+                        ip_final_tree(tv, lane, sm);
+                        ip_unpack(sm, Am, bv);
+                        const double det = icp_det6_reg(Am);           // projective_icp.cpp:197-203
+                        if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
+                    } else if (wave == 0) {                            // solve -> Rodrigues -> compose
+                        float sm[27], Am[6][6], bv[6], rv[6], R[9], tinc[12];
+                        ip_final_tree(tv, lane, sm);
+                        ip_unpack(sm, Am, bv);
+                        icp_solve6_reg(Am, bv, rv);                     // projective_icp.cpp:206-209
+                        icp_rodrigues(rv, R);
+#pragma unroll
+                        for (int j = 0; j < 3; ++j) {
+                            tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1];
+                            tinc[j * 4 + 2] = R[j * 3 + 2]; tinc[j * 4 + 3] = rv[3 + j];
+                        }
+                        float A[12];
+#pragma unroll
+                        for (int i = 0; i < 12; ++i) A[i] = aff[i];
+                        tf_rigid_mul(tinc, A, A);
+                        if (lane < 12) aff_s[lane] = A[lane];
+                        float mine = 0.f;
+#pragma unroll
+                        for (int q = 0; q < 27; ++q) if (lane == q) mine = sm[q];
+                        last_sums = mine;
+                    }
+                    __syncthreads();
+                }
+                IPT_ADD(10, IPT_NOW() - t_it);
+                IPT_ADD(7, 1);
+                status = any_timeout ? 2 : (det_ok_s ? 1 : 0);
+                if (wave == 0 && lane <= 12) {                          // broadcast affine + status
+                    const float v = lane < 12 ? aff_s[lane] : (float)status;
+                    ip_store(&tag[IP_BCAST + lane], ip_pack(gen, v));
+                }
+                if (status == 1) {
+#pragma unroll
+                    for (int i = 0; i < 12; ++i) aff[i] = aff_s[i];
+                }
+            } else {
+                // ---- wait for workgroup 0's broadcast
+                if (wave == 0) {
+                    unsigned long long v = 0;
+                    bool mine_ok = true;
+                    if (lane <= 12) {
+                        unsigned spins = 0;
+                        v = ip_load(&tag[IP_BCAST + lane]);
+                        while ((unsigned)(v >> 32) != gen) {
+                            if (++spins > IP_SPIN_LIMIT) { mine_ok = false; break; }
+                            __builtin_amdgcn_s_sleep(1);
+                            v = ip_load(&tag[IP_BCAST + lane]);
+                        }
+                        if (lane < 12) aff_s[lane] = __uint_as_float((unsigned)v);
+                        if (lane == 12) status_s = mine_ok ? (int)__uint_as_float((unsigned)v) : 2;
+                    }
+                    const bool all_ok = __all(mine_ok);
+                    if (lane == 0 && !all_ok) status_s = 2;
+                }
+                __syncthreads();
+                if (wg == ICP_NWG - 1) IPT_ADD(13, IPT_NOW() - t_it);
+                status = status_s;
+                if (status == 1) {
+#pragma unroll
+                    for (int i = 0; i < 12; ++i) aff[i] = aff_s[i];
+                }
+            }
+            ++done;
+            if (status != 1) break;
+            __syncthreads();                       // red[] / aff_s reuse in the next iteration
+        }
+    }
+    // ---- workgroup 0 records the frame's ICP result
+    if (wg == 0 && wave == 0) {
+        if (lane < 27 && done > 0 && status != 2) st->sums[lane] = last_sums;
+        if (lane == 0) {
+            st->icp_gen = base + (unsigned)a.total_iters;   // every generation this launch could use
+            st->icp_iters = done;
+            st->icp_ok = status == 1 ? 1 : (status == 0 ? 0 : -1);
+            st->abort = status == 1 ? 0 : 1;
+            for (int i = 0; i < 12; ++i) st->affine[i] = aff[i];
+            if (status == 1 && a.pose_update) {
+                // poses_.push_back(poses_.back() * affine) (topfu.cpp:243) and the derived matrices
+                float pose[12];
+                for (int i = 0; i < 12; ++i) pose[i] = st->pose[i];
+                tf_rigid_mul(pose, aff, pose);
+                for (int i = 0; i < 12; ++i) st->pose[i] = pose[i];
+                tf_set_pose_matrices(st, pose, 1);
+            }
+        }
+    }
+}
+
 __global__ void k_icp_begin(TfDevState* st)
 {
     for (int i = 0; i < 12; ++i) st->affine[i] = (i % 5 == 0) ? 1.0f : 0.0f;   // affine = Identity
@@ -504,25 +852,70 @@ hipError_t tfk_frame0_matrices(tf_ctx* c)
     return hipGetLastError();
 }
 
-// estimateTransform (projective_icp.cpp:169-213): levels coarse -> fine, one launch per iteration
+// estimateTransform (projective_icp.cpp:169-213): levels coarse -> fine.
+// Persistent path: one k_icp_frame launch; fallback: one k_icp_iter launch per iteration.
+static void icp_level(tf_ctx* c, int l, IcpLevel& L)
+{
+    const tf_params& p = c->p;
+    const int div = 1 << l;                                               // setLevelIntr
+    L.vcurr = c->curr_pts[l]; L.ncurr = c->curr_nrm[l]; L.vprev = c->prev_pts[l]; L.nprev = c->prev_nrm[l];
+    L.W = c->lw[l]; L.H = c->lh[l];
+    L.gx = (L.W + 31) / 32;
+    L.nct = L.gx * ((L.H + 7) / 8);
+    L.fx = p.fx / (float)div; L.fy = p.fy / (float)div; L.cx = p.cx / (float)div; L.cy = p.cy / (float)div;
+    L.min_cosine = c->min_cosine; L.dist2 = c->dist2_thres;
+}
+
+static int icp_used_levels(const tf_params& p)
+{
+    int levels = 4;
+    while (levels > 0 && p.icp_iter_num[levels - 1] == 0) --levels;      // getUsedLevelsNum
+    return levels > TF_LEVELS ? TF_LEVELS : levels;
+}
+
+// can every workgroup of k_icp_frame be resident at once, and do the levels fit its slots?
+int tfk_icp_persistent_ok(tf_ctx* c)
+{
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame, 64 * IP_WAVES, 0) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) return 0;
+    if (per_cu * cus < ICP_NWG) return 0;
+    for (int l = 0; l < TF_LEVELS; ++l) {
+        IcpLevel L;
+        icp_level(c, l, L);
+        if ((L.nct + ICP_NWG - 1) / ICP_NWG > IP_WAVES * IP_SREG) return 0;
+    }
+    return 1;
+}
+
 hipError_t tfk_icp(tf_ctx* c, int pose_update)
 {
     const tf_params& p = c->p;
+    const int levels = icp_used_levels(p);
+    if (c->icp_persistent) {
+        IcpFrameArgs a;
+        memset(&a, 0, sizeof(a));
+        for (int l = levels - 1; l >= 0; --l) {
+            if (p.icp_iter_num[l] <= 0) continue;
+            IcpLevel& L = a.lv[a.nlev];
+            icp_level(c, l, L);
+            a.iters[a.nlev] = p.icp_iter_num[l];
+            a.slots[a.nlev] = (L.nct + ICP_NWG - 1) / ICP_NWG;
+            a.total_iters += p.icp_iter_num[l];
+            a.nlev++;
+        }
+        a.pose_update = pose_update;
+        a.st = c->st;
+        a.tag = c->icp_tagged;
+        hipLaunchKernelGGL(k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), 0, c->stream, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, c->stream, c->st);
-    int levels = 4;
-    while (levels > 0 && p.icp_iter_num[levels - 1] == 0) --levels;      // getUsedLevelsNum
-    if (levels > TF_LEVELS) levels = TF_LEVELS;
     int last_l = -1;
     for (int l = 0; l < levels; ++l) if (p.icp_iter_num[l] > 0) { last_l = l; break; }
     for (int l = levels - 1; l >= 0; --l) {
         IcpLevel L;
-        int div = 1 << l;                                                 // setLevelIntr
-        L.vcurr = c->curr_pts[l]; L.ncurr = c->curr_nrm[l]; L.vprev = c->prev_pts[l]; L.nprev = c->prev_nrm[l];
-        L.W = c->lw[l]; L.H = c->lh[l];
-        L.gx = (L.W + 31) / 32;
-        L.nct = L.gx * ((L.H + 7) / 8);
-        L.fx = p.fx / (float)div; L.fy = p.fy / (float)div; L.cx = p.cx / (float)div; L.cy = p.cy / (float)div;
-        L.min_cosine = c->min_cosine; L.dist2 = c->dist2_thres;
+        icp_level(c, l, L);
         const int nwg = L.nct < ICP_NWG ? L.nct : ICP_NWG;
         const int slots = (L.nct + ICP_NWG - 1) / ICP_NWG;
         if (slots > ICP_MAX_SLOTS) return hipErrorInvalidValue;

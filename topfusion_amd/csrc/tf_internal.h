@@ -52,7 +52,8 @@ struct TfDevState {
     int noTotalBlocks;
     int alloc_exhausted;     // capacity exhausted this frame -> serial allocation
     unsigned tiles_total;    // rendering tiles requested (before the MAX cap)
-    int pad_[3];
+    int pad_[2];             // alloc totals (tf_scene.hip)
+    unsigned icp_gen;        // last generation tag used by the persistent ICP kernel
 };
 
 // ---------------------------------------------------------------------------------------
@@ -124,6 +125,25 @@ __device__ __forceinline__ int tf_hash_index(int x, int y, int z, unsigned mask)
 
 __device__ __forceinline__ float tf_qnan() { return __int_as_float(0x7fffffff); }
 
+// Block grid: a dense TF_GRID_DIM^3 array over block coordinates [-HALF, HALF) holding, for
+// every block findVoxel would find, (hash entry index, VBA voxel offset = ptr*512), else
+// (-1,-1).  It mirrors the hash exactly (written wherever a block is allocated, cleared on
+// reset, rebuilt after a hash upload) and replaces the bucket/excess walk on the raycasting
+// side by one 8-byte load.  256^3 x 8 B = 128 MiB of HBM.
+#define TF_GRID_LOG 8
+#define TF_GRID_DIM (1 << TF_GRID_LOG)
+#define TF_GRID_HALF (TF_GRID_DIM / 2)
+__host__ __device__ __forceinline__ bool tf_grid_in(int bx, int by, int bz)
+{
+    return ((unsigned)(bx + TF_GRID_HALF) | (unsigned)(by + TF_GRID_HALF) | (unsigned)(bz + TF_GRID_HALF)) <
+           (unsigned)TF_GRID_DIM;
+}
+__host__ __device__ __forceinline__ size_t tf_grid_cell(int bx, int by, int bz)
+{
+    return ((size_t)(bz + TF_GRID_HALF) << (2 * TF_GRID_LOG)) | ((size_t)(by + TF_GRID_HALF) << TF_GRID_LOG) |
+           (size_t)(bx + TF_GRID_HALF);
+}
+
 // wave64 butterfly sum that reproduces the reference's halving tree bit for bit
 // (temp_utils.hpp:503-523 for lanes 0..63 after the cross-wave steps)
 __device__ __forceinline__ float tf_wave_tree64(float b)
@@ -152,6 +172,7 @@ struct tf_ctx {
     int* excessList;
     TfVoxel* vba;
     int* allocList;
+    int2* bgrid;             // block grid (TF_GRID_*), mirrors the hash
     // SceneReconstructionEngine temporaries
     unsigned char* allocType;
     int* winnerKey;          // per-entry last-writer key (pixel*64+step), replaces blockCoords races
@@ -180,6 +201,8 @@ struct tf_ctx {
     // ICP
     float* icp_partial;      // [256][28] column sums
     unsigned* icp_ticket;    // last-workgroup ticket (zero between launches)
+    unsigned long long* icp_tagged;   // persistent ICP: [256][28] tagged column sums + [16] broadcast
+    int icp_persistent;      // 1: one launch per frame (k_icp_frame), 0: one launch per iteration
     int icp_max_cta;
     float min_cosine, dist2_thres;
     // device state
@@ -202,12 +225,15 @@ struct tf_ctx {
 // ---------------------------------------------------------------------------------------
 hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch);
 hipError_t tfk_icp(tf_ctx* c, int pose_update);
+int tfk_icp_persistent_ok(tf_ctx* c);      // k_icp_frame fits (co-residency, slot count)
 hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / raycast matrices
 hipError_t tfk_reset_scene(tf_ctx* c);
+hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a hash upload)
 hipError_t tfk_alloc(tf_ctx* c);
 hipError_t tfk_integrate(tf_ctx* c);
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_grey(tf_ctx* c);
+hipError_t tfk_raycast_grey(tf_ctx* c);    // renderImage raycast + grey, fused (frame path)
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_expected_depths(tf_ctx* c);
 hipError_t tfk_frame0_matrices(tf_ctx* c);

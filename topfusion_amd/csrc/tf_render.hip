@@ -14,121 +14,161 @@
 struct SceneView {
     const TfHashEntry* hash;
     const TfVoxel* vba;
+    const int2* grid;        // block grid (tf_internal.h, TF_GRID_*)
     unsigned mask;
     int n_buckets;
 };
 
-struct RCache { int bx, by, bz, blockPtr; };   // VoxelBlockHash::IndexCache (VoxelBlockHash.hpp:58-62)
+struct RCache { int bx, by, bz, voff; };   // VoxelBlockHash::IndexCache (VoxelBlockHash.hpp:58-62)
 
-// readVoxel with cache (RepresentationAccess.hpp:73-104); pointToVoxelBlockPos :9-17
-__device__ __forceinline__ TfVoxel rv_read(const SceneView& s, int px, int py, int pz, int* vm, RCache* k)
+// ---------------------------------------------------------------------------------------
+// Voxel access through the block grid.  readVoxel (RepresentationAccess.hpp:73-104) walks a
+// hash bucket and its excess chain for every block it enters; here a dense grid of
+// (hash entry, VBA offset) pairs, kept exact by the allocation kernels (tf_scene.hip), answers
+// the same question with one 8-byte load and no chain (blocks outside the grid fall back to
+// the hash walk).  Every sample on the raycasting side touches a 2x2x2 (interpolation) or
+// 4x4x4 (SDF gradient) voxel neighbourhood, so its <= 2x2x2 blocks are looked up together
+// and the voxels then loaded together: two dependent round trips per sample, whatever the
+// reference's serial corner order.  Values, the IndexCache state and vmIndex are exactly
+// those of the reference's serial reads (RepresentationAccess.hpp:73-199).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int vblk(int p) { return ((p < 0) ? p - TF_BLK + 1 : p) / TF_BLK; }   // :9-17
+__device__ __forceinline__ int vlin(int x, int y, int z) { return (x & 7) + ((y & 7) << 3) + ((z & 7) << 6); }
+
+// (hash entry index, VBA voxel offset) of block (bx,by,bz), or (-1,-1) when findVoxel fails
+__device__ __forceinline__ int2 blk_find(const SceneView& s, int bx, int by, int bz)
 {
-    int bx = ((px < 0) ? px - TF_BLK + 1 : px) / TF_BLK;
-    int by = ((py < 0) ? py - TF_BLK + 1 : py) / TF_BLK;
-    int bz = ((pz < 0) ? pz - TF_BLK + 1 : pz) / TF_BLK;
-    int lin = px + (py - bx) * TF_BLK + (pz - by) * TF_BLK * TF_BLK - bz * TF_BLK3;
-    if (bx == k->bx && by == k->by && bz == k->bz) {
-        *vm = 1;
-        return s.vba[k->blockPtr + lin];
-    }
-    int hashIdx = tf_hash_index(bx, by, bz, s.mask);
+    const unsigned gx = (unsigned)(bx + TF_GRID_HALF), gy = (unsigned)(by + TF_GRID_HALF), gz = (unsigned)(bz + TF_GRID_HALF);
+    if ((gx | gy | gz) < (unsigned)TF_GRID_DIM) return s.grid[tf_grid_cell(bx, by, bz)];
+    int hi = tf_hash_index(bx, by, bz, s.mask);
     while (true) {
-        TfHashEntry e = s.hash[hashIdx];
-        if (e.x == (short)bx && e.y == (short)by && e.z == (short)bz && e.ptr >= 0) {
-            k->bx = bx; k->by = by; k->bz = bz; k->blockPtr = e.ptr * TF_BLK3;
-            *vm = hashIdx + 1;
-            return s.vba[k->blockPtr + lin];
-        }
-        if (e.offset < 1) break;
-        hashIdx = s.n_buckets + e.offset - 1;
+        const TfHashEntry e = s.hash[hi];
+        if (e.x == (short)bx && e.y == (short)by && e.z == (short)bz && e.ptr >= 0) return make_int2(hi, e.ptr * TF_BLK3);
+        if (e.offset < 1) return make_int2(-1, -1);
+        hi = s.n_buckets + e.offset - 1;
     }
-    *vm = 0;
-    TfVoxel d; d.sdf = 32767; d.w = 0; d.pad = 0;
-    return d;
 }
 
-__device__ __forceinline__ float rv_sdf_nc(const SceneView& s, int px, int py, int pz)
+// raw Voxel_s word (sdf = low 16 bits, w = bits 16-23); unallocated -> Voxel_s() = (32767, 0)
+__device__ __forceinline__ unsigned vox_raw(const SceneView& s, int voff, int x, int y, int z)
 {
-    RCache k; k.bx = k.by = k.bz = 0x7fffffff; k.blockPtr = -1;
-    int vm;
-    return (float)rv_read(s, px, py, pz, &vm, &k).sdf;
+    return voff >= 0 ? reinterpret_cast<const unsigned*>(s.vba)[voff + vlin(x, y, z)] : 0x7fffu;
+}
+__device__ __forceinline__ float raw_sdf(unsigned r) { return (float)(short)(r & 0xffffu); }
+__device__ __forceinline__ float raw_w(unsigned r) { return (float)((r >> 16) & 0xffu); }
+
+// v[i] for a runtime i as a chain of v_cndmask (the empty asm keeps each element in a VGPR;
+// without it the optimiser turns the chain into a dynamically indexed private array)
+__device__ __forceinline__ int sel8(const int (&v)[8], int i)
+{
+    int r = v[0];
+    asm volatile("" : "+v"(r));
+#pragma unroll
+    for (int o = 1; o < 8; ++o) {
+        int t = v[o];
+        asm volatile("" : "+v"(t));
+        r = (i == o) ? t : r;
+    }
+    return r;
 }
 
-__device__ __forceinline__ int tf_round(float x) { return (int)((x < 0) ? (x - 0.5f) : (x + 0.5f)); }
+// the 8 interpolation corners of pt (floor .. floor+1) in the read order of
+// readFromSDF_float_interpolated (RepresentationAccess.hpp:137-162): corner c = (c&1, c>>1&1, c>>2)
+struct Corners {
+    int fx, fy, fz;          // floor(pt)
+    float cx, cy, cz;        // fractions
+    int bx, by, bz;          // block of floor(pt)
+    int sx, sy, sz;          // 1 when floor+1 is in the next block along that axis
+    int hidx[8], voff[8];    // per corner: hash entry / VBA offset of its block
+    unsigned raw[8];         // per corner: voxel word
+};
 
-// readFromSDF_float_interpolated (RepresentationAccess.hpp:137-162)
-__device__ __forceinline__ float rv_interp(const SceneView& s, const float* pt, int* vm, RCache* k)
+__device__ __forceinline__ void corners_fetch(const SceneView& s, const float* pt, Corners& q)
 {
+    const float ffx = floorf(pt[0]), ffy = floorf(pt[1]), ffz = floorf(pt[2]);
+    q.fx = (int)ffx; q.fy = (int)ffy; q.fz = (int)ffz;
+    q.cx = pt[0] - ffx; q.cy = pt[1] - ffy; q.cz = pt[2] - ffz;
+    q.bx = vblk(q.fx); q.by = vblk(q.fy); q.bz = vblk(q.fz);
+    q.sx = vblk(q.fx + 1) - q.bx; q.sy = vblk(q.fy + 1) - q.by; q.sz = vblk(q.fz + 1) - q.bz;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int2 g = blk_find(s, q.bx + ((c & 1) & q.sx), q.by + (((c >> 1) & 1) & q.sy), q.bz + ((c >> 2) & q.sz));
+        q.hidx[c] = g.x; q.voff[c] = g.y;
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        q.raw[c] = vox_raw(s, q.voff[c], q.fx + (c & 1), q.fy + ((c >> 1) & 1), q.fz + (c >> 2));
+}
+
+// the IndexCache after the 8 serial corner reads: the block of the last corner whose block exists
+__device__ __forceinline__ void corners_cache(const Corners& q, RCache* k)
+{
+    int last = -1;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) last = q.voff[c] >= 0 ? c : last;
+    if (last >= 0) {
+        k->bx = q.bx + ((last & 1) & q.sx); k->by = q.by + (((last >> 1) & 1) & q.sy); k->bz = q.bz + ((last >> 2) & q.sz);
+        k->voff = sel8(q.voff, last);
+    }
+}
+
+__device__ __forceinline__ float interp_sdf(const Corners& q)
+{   // readFromSDF_float_interpolated arithmetic
+    const float cx = q.cx, cy = q.cy, cz = q.cz;
     float res1, res2, v1, v2;
-    float fx = floorf(pt[0]), fy = floorf(pt[1]), fz = floorf(pt[2]);
-    int px = (int)fx, py = (int)fy, pz = (int)fz;
-    float cx = pt[0] - fx, cy = pt[1] - fy, cz = pt[2] - fz;
-    v1 = rv_read(s, px, py, pz, vm, k).sdf;
-    v2 = rv_read(s, px + 1, py, pz, vm, k).sdf;
+    v1 = raw_sdf(q.raw[0]); v2 = raw_sdf(q.raw[1]);
     res1 = (1.0f - cx) * v1 + cx * v2;
-    v1 = rv_read(s, px, py + 1, pz, vm, k).sdf;
-    v2 = rv_read(s, px + 1, py + 1, pz, vm, k).sdf;
+    v1 = raw_sdf(q.raw[2]); v2 = raw_sdf(q.raw[3]);
     res1 = (1.0f - cy) * res1 + cy * ((1.0f - cx) * v1 + cx * v2);
-    v1 = rv_read(s, px, py, pz + 1, vm, k).sdf;
-    v2 = rv_read(s, px + 1, py, pz + 1, vm, k).sdf;
+    v1 = raw_sdf(q.raw[4]); v2 = raw_sdf(q.raw[5]);
     res2 = (1.0f - cx) * v1 + cx * v2;
-    v1 = rv_read(s, px, py + 1, pz + 1, vm, k).sdf;
-    v2 = rv_read(s, px + 1, py + 1, pz + 1, vm, k).sdf;
+    v1 = raw_sdf(q.raw[6]); v2 = raw_sdf(q.raw[7]);
     res2 = (1.0f - cy) * res2 + cy * ((1.0f - cx) * v1 + cx * v2);
-    *vm = 1;
     return ((1.0f - cz) * res1 + cz * res2) / 32767.0f;
 }
 
-// readWithConfidenceFromSDF_float_interpolated (RepresentationAccess.hpp:164-199)
-__device__ __forceinline__ float rv_interp_conf(const SceneView& s, float* conf, const float* pt, int* vm, RCache* k)
-{
+__device__ __forceinline__ float interp_sdf_conf(const Corners& q, float* conf)
+{   // readWithConfidenceFromSDF_float_interpolated arithmetic (RepresentationAccess.hpp:164-199)
+    const float cx = q.cx, cy = q.cy, cz = q.cz;
     float res1, res2, v1, v2, res1_c, res2_c, v1_c, v2_c;
-    TfVoxel vx;
-    float fx = floorf(pt[0]), fy = floorf(pt[1]), fz = floorf(pt[2]);
-    int px = (int)fx, py = (int)fy, pz = (int)fz;
-    float cx = pt[0] - fx, cy = pt[1] - fy, cz = pt[2] - fz;
-    vx = rv_read(s, px, py, pz, vm, k); v1 = vx.sdf; v1_c = vx.w;
-    vx = rv_read(s, px + 1, py, pz, vm, k); v2 = vx.sdf; v2_c = vx.w;
+    v1 = raw_sdf(q.raw[0]); v1_c = raw_w(q.raw[0]); v2 = raw_sdf(q.raw[1]); v2_c = raw_w(q.raw[1]);
     res1 = (1.0f - cx) * v1 + cx * v2;
     res1_c = (1.0f - cx) * v1_c + cx * v2_c;
-    vx = rv_read(s, px, py + 1, pz, vm, k); v1 = vx.sdf; v1_c = vx.w;
-    vx = rv_read(s, px + 1, py + 1, pz, vm, k); v2 = vx.sdf; v2_c = vx.w;
+    v1 = raw_sdf(q.raw[2]); v1_c = raw_w(q.raw[2]); v2 = raw_sdf(q.raw[3]); v2_c = raw_w(q.raw[3]);
     res1 = (1.0f - cy) * res1 + cy * ((1.0f - cx) * v1 + cx * v2);
     res1_c = (1.0f - cy) * res1_c + cy * ((1.0f - cx) * v1_c + cx * v2_c);
-    vx = rv_read(s, px, py, pz + 1, vm, k); v1 = vx.sdf; v1_c = vx.w;
-    vx = rv_read(s, px + 1, py, pz + 1, vm, k); v2 = vx.sdf; v2_c = vx.w;
+    v1 = raw_sdf(q.raw[4]); v1_c = raw_w(q.raw[4]); v2 = raw_sdf(q.raw[5]); v2_c = raw_w(q.raw[5]);
     res2 = (1.0f - cx) * v1 + cx * v2;
     res2_c = (1.0f - cx) * v1_c + cx * v2_c;
-    vx = rv_read(s, px, py + 1, pz + 1, vm, k); v1 = vx.sdf; v1_c = vx.w;
-    vx = rv_read(s, px + 1, py + 1, pz + 1, vm, k); v2 = vx.sdf; v2_c = vx.w;
+    v1 = raw_sdf(q.raw[6]); v1_c = raw_w(q.raw[6]); v2 = raw_sdf(q.raw[7]); v2_c = raw_w(q.raw[7]);
     res2 = (1.0f - cy) * res2 + cy * ((1.0f - cx) * v1 + cx * v2);
     res2_c = (1.0f - cy) * res2_c + cy * ((1.0f - cx) * v1_c + cx * v2_c);
-    *vm = 1;
     *conf = (1.0f - cz) * res1_c + cz * res2_c;
     return ((1.0f - cz) * res1 + cz * res2) / 32767.0f;
 }
+
+__device__ __forceinline__ int tf_round(float x) { return (int)((x < 0) ? (x - 0.5f) : (x + 0.5f)); }
 
 struct RayArgs {
     SceneView s;
     const float2* range;
     float4* out;
     unsigned char* visType;      // non-null: castRay<true>
+    uchar4* grey;                // non-null: fused renderGrey (frame path)
     int W, H;
     float invfx, invfy, ncx, ncy; // InvertProjectionParams (VisualisationEngine_Shared.hpp:28-31)
     float oneOverVoxelSize, mu;
 };
 
-__global__ void __launch_bounds__(256)
-k_raycast(RayArgs a, const TfDevState* __restrict__ st)
+// castRay (VisualisationEngine_Shared.hpp:99-172).  One step = the uninterpolated read at
+// ROUND(pt) and, in the band, the interpolated read at pt.  ROUND(pt) is one of the eight
+// interpolation corners, so a step fetches the corners once (speculatively): one grid round
+// trip + one voxel round trip per step.
+__device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, int x, int y, float* pt)
 {
-    if (st->abort) return;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.H) return;
-    const float* invM = st->M_ray;
     int locId2 = (int)floorf((float)x / TF_SUBSAMPLE) + (int)floorf((float)y / TF_SUBSAMPLE) * a.W;
     float2 vf = a.range[locId2];
-    float r[3], ps[3], pe[3], dir[3], pt[3];
-    int vmIndex = 0;
+    float r[3], ps[3], pe[3], dir[3];
     float sdfValue = 1.0f, confidence = 0.0f, stepLength;
     const float stepScale = a.mu * a.oneOverVoxelSize;
     float pz = vf.x;
@@ -147,17 +187,33 @@ k_raycast(RayArgs a, const TfDevState* __restrict__ st)
     float dn = 1.0f / sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
     dir[0] *= dn; dir[1] *= dn; dir[2] *= dn;
     pt[0] = ps[0]; pt[1] = ps[1]; pt[2] = ps[2];
-    RCache k; k.bx = k.by = k.bz = 0x7fffffff; k.blockPtr = -1;
+    RCache k; k.bx = k.by = k.bz = 0x7fffffff; k.voff = -1;
     while (totalLength < totalLengthMax) {
-        sdfValue = (float)rv_read(a.s, tf_round(pt[0]), tf_round(pt[1]), tf_round(pt[2]), &vmIndex, &k).sdf / 32767.0f;
+        Corners q;
+        corners_fetch(a.s, pt, q);
+        // uninterpolated read at ROUND(pt) (readFromSDF_float_uninterpolated, :129-135)
+        const int ux = tf_round(pt[0]) - q.fx, uy = tf_round(pt[1]) - q.fy, uz = tf_round(pt[2]) - q.fz;
+        const int cu = ux + 2 * uy + 4 * uz;
+        const int vu = sel8(q.voff, cu);
+        int vmIndex = 0;
+        if (vu >= 0) {
+            const int Ubx = q.bx + (ux & q.sx), Uby = q.by + (uy & q.sy), Ubz = q.bz + (uz & q.sz);
+            const bool hit = Ubx == k.bx && Uby == k.by && Ubz == k.bz;
+            vmIndex = hit ? 1 : sel8(q.hidx, cu) + 1;
+            k.bx = Ubx; k.by = Uby; k.bz = Ubz; k.voff = vu;
+        }
+        sdfValue = raw_sdf((unsigned)sel8(reinterpret_cast<const int(&)[8]>(q.raw), cu)) / 32767.0f;
         if (a.visType && vmIndex) a.visType[vmIndex - 1] = 1;
         if (!vmIndex) {
             stepLength = (float)TF_BLK;
         } else {
-            if ((sdfValue <= 0.1f) && (sdfValue >= -0.5f)) sdfValue = rv_interp(a.s, pt, &vmIndex, &k);
+            if ((sdfValue <= 0.1f) && (sdfValue >= -0.5f)) {
+                sdfValue = interp_sdf(q);
+                corners_cache(q, &k);
+            }
             if (sdfValue <= 0.0f) break;
-            float q = sdfValue * stepScale;
-            stepLength = (q < 1.0f) ? 1.0f : q;
+            float qq = sdfValue * stepScale;
+            stepLength = (qq < 1.0f) ? 1.0f : qq;
         }
         pt[0] += stepLength * dir[0]; pt[1] += stepLength * dir[1]; pt[2] += stepLength * dir[2];
         totalLength += stepLength;
@@ -166,30 +222,20 @@ k_raycast(RayArgs a, const TfDevState* __restrict__ st)
     if (sdfValue <= 0.0f) {
         stepLength = sdfValue * stepScale;
         pt[0] += stepLength * dir[0]; pt[1] += stepLength * dir[1]; pt[2] += stepLength * dir[2];
-        sdfValue = rv_interp_conf(a.s, &confidence, pt, &vmIndex, &k);
+        Corners q;
+        corners_fetch(a.s, pt, q);
+        sdfValue = interp_sdf_conf(q, &confidence);
         stepLength = sdfValue * stepScale;
         pt[0] += stepLength * dir[0]; pt[1] += stepLength * dir[1]; pt[2] += stepLength * dir[2];
         w = confidence + 1.0f;
     }
-    a.out[x + y * a.W] = make_float4(pt[0], pt[1], pt[2], w);
-}
-
-hipError_t tfk_raycast(tf_ctx* c, int update_visible)
-{
-    RayArgs a;
-    a.s.hash = c->hash; a.s.vba = c->vba; a.s.mask = (unsigned)(c->p.n_buckets - 1); a.s.n_buckets = c->p.n_buckets;
-    a.range = (const float2*)c->range; a.out = (float4*)c->raycast;
-    a.visType = update_visible ? c->visType : nullptr;
-    a.W = c->W; a.H = c->H;
-    a.invfx = 1.0f / c->p.fx; a.invfy = 1.0f / c->p.fy; a.ncx = -c->p.cx; a.ncy = -c->p.cy;
-    a.oneOverVoxelSize = 1.0f / c->p.voxelSize; a.mu = c->p.mu;
-    hipLaunchKernelGGL(k_raycast, dim3((c->W + 15) / 16, (c->H + 15) / 16), dim3(256), 0, c->stream, a, c->st);
-    return hipGetLastError();
+    return w;
 }
 
 // ---------------------------------------------------------------------------------------
 // renderGrey_device: computeSingleNormalFromSDF (RepresentationAccess.hpp:340-453),
-// computeNormalAndAngle (VisualisationEngine_Shared.hpp:187-203), drawPixelGrey (:272-276)
+// computeNormalAndAngle (VisualisationEngine_Shared.hpp:187-203), drawPixelGrey (:272-276).
+// The 32 uncached reads cover pt's 4x4x4 neighbourhood (floor-1 .. floor+2): <= 2x2x2 blocks.
 // ---------------------------------------------------------------------------------------
 __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
 {
@@ -197,7 +243,19 @@ __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
     int px = (int)ffx, py = (int)ffy, pz = (int)ffz;
     float cx = pt[0] - ffx, cy = pt[1] - ffy, cz = pt[2] - ffz;
     float nx = 1.0f - cx, ny = 1.0f - cy, nz = 1.0f - cz;
-#define RV(dx, dy, dz) rv_sdf_nc(s, px + (dx), py + (dy), pz + (dz))
+    const int bx = vblk(px - 1), by = vblk(py - 1), bz = vblk(pz - 1);
+    const int sx = vblk(px + 2) - bx, sy = vblk(py + 2) - by, sz = vblk(pz + 2) - bz;
+    int voff[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o)
+        voff[o] = blk_find(s, bx + ((o & 1) & sx), by + (((o >> 1) & 1) & sy), bz + ((o >> 2) & sz)).y;
+    int ox[4], oy[4], oz[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        ox[d] = vblk(px - 1 + d) - bx; oy[d] = vblk(py - 1 + d) - by; oz[d] = vblk(pz - 1 + d) - bz;
+    }
+#define RV(dx, dy, dz) raw_sdf(vox_raw(s, sel8(voff, ox[(dx) + 1] + 2 * oy[(dy) + 1] + 4 * oz[(dz) + 1]), \
+                                       px + (dx), py + (dy), pz + (dz)))
     float f0 = RV(0, 0, 0), f1 = RV(1, 0, 0), f2 = RV(0, 1, 0), f3 = RV(1, 1, 0);
     float b0 = RV(0, 0, 1), b1 = RV(1, 0, 1), b2 = RV(0, 1, 1), b3 = RV(1, 1, 1);
     float t0, t1, t2, t3, p1, p2, v1;
@@ -228,6 +286,81 @@ __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
 #undef RV
 }
 
+__device__ __forceinline__ unsigned char grey_pixel(const SceneView& s, const float* pt, float lx, float ly, float lz)
+{
+    float nn[3];
+    sdf_normal(s, pt, nn);
+    float ns = 1.0f / sqrtf(nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]);
+    nn[0] *= ns; nn[1] *= ns; nn[2] *= ns;
+    float angle = nn[0] * lx + nn[1] * ly + nn[2] * lz;
+    return angle > 0.0f ? (unsigned char)((0.8f * angle + 0.2f) * 255.0f) : (unsigned char)0;
+}
+
+// XCD-aware tile order: consecutive image tiles land on the same XCD (and its L2)
+__device__ __forceinline__ int xcd_tile(int bid, int n)
+{
+    const int per = (n + 7) / 8;
+    const int t = (bid % 8) * per + bid / 8;
+    return t < n ? t : -1;
+}
+
+__global__ void __launch_bounds__(256)
+k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles)
+{
+    if (st->abort) return;
+    const int tile = xcd_tile(blockIdx.x, n_tiles);     // grid padded to a multiple of 8
+    if (tile < 0) return;
+    const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15), y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
+    if (x >= a.W || y >= a.H) return;
+    float pt[3];
+    const float w = ray_march(a, st->M_ray, x, y, pt);
+    if (a.grey) {
+        // renderImage: lightSource = -Vector3f(pose.getColumn(2)) (VisualisationEngine_CUDA.cu:243)
+        unsigned char v = 0;
+        if (w > 0) v = grey_pixel(a.s, pt, -st->M_ray[8], -st->M_ray[9], -st->M_ray[10]);
+        a.grey[x + y * a.W] = make_uchar4(v, v, v, v);
+    } else {
+        a.out[x + y * a.W] = make_float4(pt[0], pt[1], pt[2], w);
+    }
+}
+
+static void ray_args(tf_ctx* c, RayArgs& a)
+{
+    a.s.hash = c->hash; a.s.vba = c->vba; a.s.grid = c->bgrid; a.s.mask = (unsigned)(c->p.n_buckets - 1); a.s.n_buckets = c->p.n_buckets;
+    a.range = (const float2*)c->range; a.out = (float4*)c->raycast;
+    a.visType = nullptr;
+    a.grey = nullptr;
+    a.W = c->W; a.H = c->H;
+    a.invfx = 1.0f / c->p.fx; a.invfy = 1.0f / c->p.fy; a.ncx = -c->p.cx; a.ncy = -c->p.cy;
+    a.oneOverVoxelSize = 1.0f / c->p.voxelSize; a.mu = c->p.mu;
+}
+
+static hipError_t launch_ray(tf_ctx* c, const RayArgs& a)
+{
+    const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty;
+    hipLaunchKernelGGL(k_raycast, dim3((n + 7) / 8 * 8), dim3(256), 0, c->stream, a, c->st, tx, n);
+    return hipGetLastError();
+}
+
+hipError_t tfk_raycast(tf_ctx* c, int update_visible)
+{
+    RayArgs a;
+    ray_args(c, a);
+    a.visType = update_visible ? c->visType : nullptr;
+    return launch_ray(c, a);
+}
+
+// renderImage in the frame path: castRay<false> + renderGrey fused (the intermediate point
+// image is overwritten by CreateICPMaps before anything can observe it)
+hipError_t tfk_raycast_grey(tf_ctx* c)
+{
+    RayArgs a;
+    ray_args(c, a);
+    a.grey = c->grey;
+    return launch_ray(c, a);
+}
+
+
 __global__ void __launch_bounds__(256)
 k_grey(SceneView s, const float4* __restrict__ ray, int n, const TfDevState* __restrict__ st, uchar4* __restrict__ out)
 {
@@ -239,19 +372,15 @@ k_grey(SceneView s, const float4* __restrict__ ray, int n, const TfDevState* __r
     float4 p = ray[i];
     unsigned char v = 0;
     if (p.w > 0) {
-        float pt[3] = { p.x, p.y, p.z }, nn[3];
-        sdf_normal(s, pt, nn);
-        float ns = 1.0f / sqrtf(nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]);
-        nn[0] *= ns; nn[1] *= ns; nn[2] *= ns;
-        float angle = nn[0] * lx + nn[1] * ly + nn[2] * lz;
-        if (angle > 0.0f) v = (unsigned char)((0.8f * angle + 0.2f) * 255.0f);
+        float pt[3] = { p.x, p.y, p.z };
+        v = grey_pixel(s, pt, lx, ly, lz);
     }
     out[i] = make_uchar4(v, v, v, v);
 }
 
 hipError_t tfk_render_grey(tf_ctx* c)
 {
-    SceneView s; s.hash = c->hash; s.vba = c->vba; s.mask = (unsigned)(c->p.n_buckets - 1); s.n_buckets = c->p.n_buckets;
+    SceneView s; s.hash = c->hash; s.vba = c->vba; s.grid = c->bgrid; s.mask = (unsigned)(c->p.n_buckets - 1); s.n_buckets = c->p.n_buckets;
     int n = c->W * c->H;
     hipLaunchKernelGGL(k_grey, dim3((n + 255) / 256), dim3(256), 0, c->stream, s, (const float4*)c->raycast, n, c->st, c->grey);
     return hipGetLastError();

@@ -29,7 +29,7 @@ __device__ __forceinline__ void load16(const unsigned char* p, unsigned long lon
 // ResetScene (SceneReconstructionEngine_host.cu:51-73)
 // ---------------------------------------------------------------------------------------
 __global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_blocks, TfHashEntry* hash,
-                              int n_total, int* excessList, int n_excess, TfDevState* st)
+                              int n_total, int* excessList, int n_excess, TfDevState* st, int2* grid)
 {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -38,7 +38,11 @@ __global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_
     for (size_t i = tid; i < n_vox / 4; i += stride) v4[i] = vfill;
     for (size_t i = tid; i < (size_t)n_blocks; i += stride) allocList[i] = (int)i;
     TfHashEntry e; e.x = e.y = e.z = e.pad = 0; e.offset = 0; e.ptr = -2;
-    for (size_t i = tid; i < (size_t)n_total; i += stride) hash[i] = e;
+    for (size_t i = tid; i < (size_t)n_total; i += stride) {
+        const TfHashEntry o = hash[i];                       // clear the grid cells of live blocks
+        if (o.ptr >= 0 && tf_grid_in(o.x, o.y, o.z)) grid[tf_grid_cell(o.x, o.y, o.z)] = make_int2(-1, -1);
+        hash[i] = e;
+    }
     for (size_t i = tid; i < (size_t)n_excess; i += stride) excessList[i] = (int)i;
     if (tid == 0) {
         st->lastFreeBlockId = n_blocks - 1;
@@ -49,7 +53,26 @@ __global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_
 hipError_t tfk_reset_scene(tf_ctx* c)
 {
     hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, c->vba, (size_t)c->p.n_blocks * TF_BLK3,
-                       c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st);
+                       c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st, c->bgrid);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ void grid_set(int2* grid, const TfHashEntry& e, int idx)
+{
+    if (e.ptr >= 0 && tf_grid_in(e.x, e.y, e.z)) grid[tf_grid_cell(e.x, e.y, e.z)] = make_int2(idx, e.ptr * TF_BLK3);
+}
+
+__global__ void k_grid_build(const TfHashEntry* __restrict__ hash, int n_total, int2* __restrict__ grid)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_total; i += gridDim.x * blockDim.x)
+        grid_set(grid, hash[i], i);
+}
+
+hipError_t tfk_grid_rebuild(tf_ctx* c)
+{
+    hipError_t e = hipMemsetAsync(c->bgrid, 0xff, sizeof(int2) * (size_t)TF_GRID_DIM * TF_GRID_DIM * TF_GRID_DIM, c->stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_grid_build, dim3(1024), dim3(256), 0, c->stream, c->hash, c->n_total, c->bgrid);
     return hipGetLastError();
 }
 
@@ -64,6 +87,7 @@ struct AllocArgs {
     float vf_min, vf_max;
     unsigned mask;
     int n_buckets;
+    int2* grid;                        // block grid, kept in step with the hash
 };
 
 // ray segment [d-mu, d+mu] of pixel (x,y) in block units; false if the pixel is skipped
@@ -258,10 +282,12 @@ k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int*
             e.ptr = allocList[v0 - r12];
             if (t == 1) {
                 hash[idx] = e;
+                grid_set(a.grid, e, idx);
             } else {
                 int exlOffset = excessList[e0 - r2];
                 hash[idx].offset = exlOffset + 1;
                 hash[a.n_buckets + exlOffset] = e;
+                grid_set(a.grid, e, a.n_buckets + exlOffset);
                 visType[a.n_buckets + exlOffset] = 1;
             }
             allocType[idx] = 0;
@@ -297,6 +323,7 @@ __global__ void k_alloc_finish(AllocArgs a, TfDevState* __restrict__ st, unsigne
                 TfHashEntry he; he.x = pos[0]; he.y = pos[1]; he.z = pos[2]; he.pad = 0; he.offset = 0;
                 he.ptr = allocList[vbaIdx];
                 hash[idx] = he;
+                grid_set(a.grid, he, idx);
             } else {
                 visType[idx] = 0;
                 v++;
@@ -311,6 +338,7 @@ __global__ void k_alloc_finish(AllocArgs a, TfDevState* __restrict__ st, unsigne
                 int exlOffset = excessList[exlIdx];
                 hash[idx].offset = exlOffset + 1;
                 hash[a.n_buckets + exlOffset] = he;
+                grid_set(a.grid, he, a.n_buckets + exlOffset);
                 visType[a.n_buckets + exlOffset] = 1;
             } else {
                 v++; e++;
@@ -428,6 +456,7 @@ static AllocArgs make_alloc_args(tf_ctx* c)
     a.vf_min = c->p.viewFrustum_min; a.vf_max = c->p.viewFrustum_max;
     a.mask = (unsigned)(c->p.n_buckets - 1);
     a.n_buckets = c->p.n_buckets;
+    a.grid = c->bgrid;
     return a;
 }
 

@@ -96,6 +96,10 @@ class TopFu:
         L.check(L.load().tf_render_image(self._h, None, 0), "tf_render_image")
         return self.download(L.TF_BUF_GREY).view(np.uint8).reshape(self.H, self.W, 4)
 
+    def frame_grey(self):
+        """The grey image renderImage produced inside the last tracked frame (no re-render)."""
+        return self.download(L.TF_BUF_GREY).view(np.uint8).reshape(self.H, self.W, 4)
+
     def getCameraPose(self):
         rt = np.zeros(12, np.float32)
         L.check(L.load().tf_get_pose(self._h, _ptr(rt)), "tf_get_pose")
@@ -113,6 +117,12 @@ class TopFu:
 
     def stream(self):
         return L.load().tf_get_stream(self._h)
+
+    def icp_persistent(self):
+        """True when ICP runs as one persistent launch per frame."""
+        v = ctypes.c_int()
+        L.check(L.load().tf_get_schedule(self._h, ctypes.byref(v)), "tf_get_schedule")
+        return bool(v.value)
 
     # -- per-stage HIP-event timing ----------------------------------------------------
     def profile(self, enable=True):
