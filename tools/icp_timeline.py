@@ -1,0 +1,38 @@
+"""Timeline of the persistent ICP kernel's last launch (debug build, `make -C topfusion_amd/csrc
+timing`).  On the GPU box:
+  TFUSION_HIP_LIB=tools/_build/libtfusion_hip_timing.so python tools/icp_timeline.py"""
+import ctypes, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch
+from topfusion_amd import TopFu, default_params, synth
+from topfusion_amd import _lib
+W, H = 640, 480
+fx, fy, cx, cy = synth.intrinsics(W, H)
+frames = synth.orbit_sequence(8, W, H, seed=7)
+dev = torch.from_numpy(frames.view(np.int16)).cuda()
+tf = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy), device=0)
+tf.process_frames(dev.data_ptr(), 3)
+torch.cuda.synchronize()
+NW = 256
+S = 2 * NW + 8
+buf = (ctypes.c_ulonglong * (64 * S))()
+_lib.load().tf_debug_icp_timeline(buf)
+tl = np.frombuffer(buf, dtype=np.uint64).reshape(64, S).astype(np.int64)
+its = tf.stats()["icp_iterations"]
+print("iterations", its, "(times in us, 100 MHz clock, relative to WG0's iteration start)")
+for i in range(its):
+    t0 = tl[i, 0]
+    st = (tl[i, :NW] - t0) / 100.0
+    pub = (tl[i, NW:2 * NW] - t0) / 100.0
+    g = (tl[i, 2 * NW] - t0) / 100.0
+    tail = (tl[i, 2 * NW + 1] - t0) / 100.0
+    ph = [(tl[i, 2 * NW + k] - t0) / 100.0 for k in (2, 3, 4, 5)]
+    nxt = (tl[i + 1, :NW] - t0) / 100.0 if i + 1 < its else None
+    line = (f"it {i:2d}: start[min/med/max] {st.min():5.2f}/{np.median(st):5.2f}/{st.max():5.2f} "
+            f"pub {pub.min():5.2f}/{np.median(pub):5.2f}/{pub.max():5.2f} (max wg {int(pub.argmax())}) "
+            f"wg0 pub {pub[0]:5.2f} gathered {g:5.2f} [tree {ph[0]:5.2f} solve {ph[1]:5.2f} rod+comp {ph[2]:5.2f} det {ph[3]:5.2f}] tail {tail:5.2f}")
+    if nxt is not None:
+        line += f" next-start {nxt.min():5.2f}/{np.median(nxt):5.2f}/{nxt.max():5.2f}"
+    print(line)

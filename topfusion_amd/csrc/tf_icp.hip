@@ -33,12 +33,23 @@ extern "C" int tf_debug_icp_ts(unsigned long long* out)
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_ts), sizeof(g_icp_ts), 0, hipMemcpyDeviceToHost);
 }
 #define IPT_NOW() __builtin_amdgcn_s_memrealtime()
-#define IPT_ADD(k, v) do { if (threadIdx.x == 0) g_icp_ts[k] += (v); } while (0)
+#define IPT_ADD(k, v) do { } while (0)
+// timeline of the last persistent launch: per iteration [256 starts][256 publishes][8 WG0 events]
+#define IPT_STRIDE (2 * ICP_NWG + 8)
+__device__ unsigned long long g_icp_tl[64 * IPT_STRIDE];
+#define IPT_REC(it, slot) IPT_REC_T(it, slot, 0)
+#define IPT_REC_T(it, slot, t) do { if (threadIdx.x == (t) && (it) < 64) g_icp_tl[(it) * IPT_STRIDE + (slot)] = IPT_NOW(); } while (0)
+extern "C" int tf_debug_icp_timeline(unsigned long long* out)
+{
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_tl), sizeof(g_icp_tl), 0, hipMemcpyDeviceToHost);
+}
 #else
 #define ICP_TS0()
 #define ICP_TS(k)
 #define IPT_NOW() 0ull
 #define IPT_ADD(k, v) do { } while (0)
+#define IPT_REC(it, slot) do { } while (0)
+#define IPT_REC_T(it, slot, t) do { } while (0)
 #endif
 
 struct IcpLevel {
@@ -82,16 +93,37 @@ __device__ __forceinline__ bool icp_row(const IcpLevel& L, const float* aff, int
 
 // One exchange step of the transposed butterfly: lanes with (lane & OFF) keep the upper half
 // of the N live sums, the others the lower half; each kept sum is completed with the
-// partner lane's copy, so every sum sees the same pairings as a full xor butterfly.
+// partner lane's copy, so every sum sees the same pairings as a full xor butterfly.  The
+// exchanges are cross-lane register moves, no LDS: v_permlane32_swap / v_permlane16_swap for
+// the 32- and 16-lane steps (one instruction swaps the halves of two sums), DPP for the rest
+// (xor 8 = row_ror:8, xor 4 = row_half_mirror then quad_perm xor 3, xor 2/1 = quad_perm).
+// a + b == b + a bit for bit, so which operand is the kept one does not matter.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float xor1(float v) { return dppf<0xB1>(v); }                  // quad_perm [1,0,3,2]
+__device__ __forceinline__ float xor2(float v) { return dppf<0x4E>(v); }                  // quad_perm [2,3,0,1]
+__device__ __forceinline__ float xor4(float v) { return dppf<0x1B>(dppf<0x141>(v)); }     // half_mirror, [3,2,1,0]
+__device__ __forceinline__ float xor8(float v) { return dppf<0x128>(v); }                 // row_ror:8
+
 template <int N, int OFF>
 __device__ __forceinline__ void tstep(float* v, int lane)
 {
-    const bool hi = (lane & OFF) != 0;
 #pragma unroll
     for (int j = 0; j < N / 2; ++j) {
-        float send = hi ? v[j] : v[j + N / 2];
-        float keep = hi ? v[j + N / 2] : v[j];
-        v[j] = keep + __shfl_xor(send, OFF, 64);
+        if constexpr (OFF == 32 || OFF == 16) {
+            auto r = OFF == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + N / 2]), false, false)
+                               : __builtin_amdgcn_permlane16_swap(__float_as_uint(v[j]), __float_as_uint(v[j + N / 2]), false, false);
+            v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+        } else {
+            const bool hi = (lane & OFF) != 0;
+            const float send = hi ? v[j] : v[j + N / 2];
+            const float keep = hi ? v[j + N / 2] : v[j];
+            const float recv = OFF == 8 ? xor8(send) : (OFF == 4 ? xor4(send) : xor2(send));
+            v[j] = keep + recv;
+        }
     }
 }
 
@@ -237,6 +269,7 @@ __device__ __forceinline__ double icp_det6_reg(const float (&A0)[6][6])
         int k = i;
 #pragma unroll
         for (int j = i + 1; j < 6; j++) { float v = fabsf(A[j][i]); if (v > best) { best = v; k = j; } }
+        k = __builtin_amdgcn_readfirstlane(k);          // uniform: swaps become scalar branches
         if (best < eps) return 0.0;
         if (k != i) {
 #pragma unroll
@@ -278,6 +311,7 @@ __device__ __forceinline__ void icp_solve6_reg(const float (&Af)[6][6], const fl
         int k = i;
 #pragma unroll
         for (int j = i + 1; j < 6; ++j) { double v = fabs(A[j][i]); if (v > best) { best = v; k = j; } }
+        k = __builtin_amdgcn_readfirstlane(k);          // uniform: swaps become scalar branches
         if (k != i) {
 #pragma unroll
             for (int r = i + 1; r < 6; ++r)
@@ -352,7 +386,7 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
         tstep<8, 8>(v, lane);
         tstep<4, 4>(v, lane);
         tstep<2, 2>(v, lane);
-        float tot = v[0] + __shfl_xor(v[0], 1, 64);
+        float tot = v[0] + xor1(v[0]);
         const int sidx = lane >> 1;
         if (!(lane & 1) && sidx < 27) red[s][sidx] = tot;
     }
@@ -417,7 +451,7 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
     tstep<8, 8>(v, lane);
     tstep<4, 4>(v, lane);
     tstep<2, 2>(v, lane);
-    const float tot = v[0] + __shfl_xor(v[0], 1, 64);     // lane l holds sum (l >> 1)
+    const float tot = v[0] + xor1(v[0]);     // lane l holds sum (l >> 1)
     float sm[27];
 #pragma unroll
     for (int q = 0; q < 27; ++q) sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), 2 * q));
@@ -489,6 +523,7 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 #define IP_SREG 1                       // CTA slots kept in registers per wave (8 per WG; larger images use k_icp_iter)
 #define IP_SPIN_LIMIT (1u << 21)
 #define IP_BCAST (ICP_NWG * ICP_T_STRIDE)
+#define IP_LDS_PAD (56 * 1024)
 
 struct IcpFrameArgs {
     IcpLevel lv[TF_LEVELS];             // in processing order (coarse -> fine)
@@ -576,7 +611,7 @@ __device__ __forceinline__ float ip_cta_reduce(const float (&r)[4][7], int lane)
     tstep<8, 8>(v, lane);
     tstep<4, 4>(v, lane);
     tstep<2, 2>(v, lane);
-    return v[0] + __shfl_xor(v[0], 1, 64);
+    return v[0] + xor1(v[0]);
 }
 
 // final 256-wide tree of the column sums in LDS -> the 27 sums in every lane (uniform)
@@ -596,7 +631,7 @@ __device__ __forceinline__ void ip_final_tree(const float (*tv)[ICP_NWG], int la
     tstep<8, 8>(v, lane);
     tstep<4, 4>(v, lane);
     tstep<2, 2>(v, lane);
-    const float tot = v[0] + __shfl_xor(v[0], 1, 64);
+    const float tot = v[0] + xor1(v[0]);
 #pragma unroll
     for (int q = 0; q < 27; ++q)
         sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), 2 * q));
@@ -663,7 +698,7 @@ k_icp_frame(IcpFrameArgs a)
 #pragma unroll 1
         for (int it = 0; it < iters; ++it) {
             ++gen;
-            const unsigned long long t_it = IPT_NOW(); (void)t_it;
+            IPT_REC(done, wg);
             // ---- per-CTA reductions -> column sum of this workgroup -> tagged slot
 #pragma unroll
             for (int rr = 0; rr < IP_SREG; ++rr) {
@@ -684,7 +719,7 @@ k_icp_frame(IcpFrameArgs a)
                 }
                 ip_store(&tag[wg * ICP_T_STRIDE + tid], ip_pack(gen, sum));
             }
-            if (wg == 0 || wg == ICP_NWG - 1) IPT_ADD(wg == 0 ? 8 : 12, IPT_NOW() - t_it);
+            IPT_REC(done, ICP_NWG + wg);
             if (wg == 0) {
                 // ---- gather the 256 column sums (tagged polling; all loads in flight at once)
                 constexpr int PER = (ICP_NWG * 27 + 64 * IP_WAVES - 1) / (64 * IP_WAVES);
@@ -719,7 +754,7 @@ k_icp_frame(IcpFrameArgs a)
                 }
                 if (tid == 0) det_ok_s = 1;
                 const int any_timeout = __syncthreads_or(timeout);
-                IPT_ADD(9, IPT_NOW() - t_it);
+                IPT_REC(done, 2 * ICP_NWG + 0);
                 if (!any_timeout) {
                     if (wave == 1) {                                   // det on its own wave
                         float sm[27], Am[6][6], bv[6];
@@ -727,11 +762,14 @@ k_icp_frame(IcpFrameArgs a)
                         ip_unpack(sm, Am, bv);
                         const double det = icp_det6_reg(Am);           // projective_icp.cpp:197-203
                         if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
+                        IPT_REC_T(done, 2 * ICP_NWG + 5, 64);
                     } else if (wave == 0) {                            // solve -> Rodrigues -> compose
                         float sm[27], Am[6][6], bv[6], rv[6], R[9], tinc[12];
                         ip_final_tree(tv, lane, sm);
                         ip_unpack(sm, Am, bv);
+                        IPT_REC(done, 2 * ICP_NWG + 2);
                         icp_solve6_reg(Am, bv, rv);                     // projective_icp.cpp:206-209
+                        IPT_REC(done, 2 * ICP_NWG + 3);
                         icp_rodrigues(rv, R);
 #pragma unroll
                         for (int j = 0; j < 3; ++j) {
@@ -743,6 +781,7 @@ k_icp_frame(IcpFrameArgs a)
                         for (int i = 0; i < 12; ++i) A[i] = aff[i];
                         tf_rigid_mul(tinc, A, A);
                         if (lane < 12) aff_s[lane] = A[lane];
+                        IPT_REC(done, 2 * ICP_NWG + 4);
                         float mine = 0.f;
 #pragma unroll
                         for (int q = 0; q < 27; ++q) if (lane == q) mine = sm[q];
@@ -750,8 +789,7 @@ k_icp_frame(IcpFrameArgs a)
                     }
                     __syncthreads();
                 }
-                IPT_ADD(10, IPT_NOW() - t_it);
-                IPT_ADD(7, 1);
+                IPT_REC(done, 2 * ICP_NWG + 1);
                 status = any_timeout ? 2 : (det_ok_s ? 1 : 0);
                 if (wave == 0 && lane <= 12) {                          // broadcast affine + status
                     const float v = lane < 12 ? aff_s[lane] : (float)status;
@@ -781,7 +819,7 @@ k_icp_frame(IcpFrameArgs a)
                     if (lane == 0 && !all_ok) status_s = 2;
                 }
                 __syncthreads();
-                if (wg == ICP_NWG - 1) IPT_ADD(13, IPT_NOW() - t_it);
+
                 status = status_s;
                 if (status == 1) {
 #pragma unroll
@@ -877,7 +915,7 @@ static int icp_used_levels(const tf_params& p)
 int tfk_icp_persistent_ok(tf_ctx* c)
 {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame, 64 * IP_WAVES, 0) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame, 64 * IP_WAVES, IP_LDS_PAD) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) return 0;
     if (per_cu * cus < ICP_NWG) return 0;
     for (int l = 0; l < TF_LEVELS; ++l) {
@@ -907,7 +945,9 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update)
         a.pose_update = pose_update;
         a.st = c->st;
         a.tag = c->icp_tagged;
-        hipLaunchKernelGGL(k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), 0, c->stream, a);
+        // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
+        // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up
+        hipLaunchKernelGGL(k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, c->stream, c->st);
