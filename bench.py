@@ -26,6 +26,11 @@ sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
+# stages that are one kernel launch per frame (persistent ICP), and that kernel's name
+KERNEL_OF_STAGE = {"icp": "k_icp_frame", "raycast_render": "k_raycast<2> (raycast + grey)",
+                   "raycast_icp": "k_raycast<1>", "integrate": "k_integrate"}
+SINGLE_KERNEL_STAGES = tuple(KERNEL_OF_STAGE)
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -137,25 +142,30 @@ def main():
         icp_integ = None
         if prof and prof["icp"][1]:
             icp_integ = per_stage["icp"] + per_stage["alloc"] + per_stage["integrate"]
-        # dominant single-kernel stage by measured time
-        roof = None
+        # roofline of the dominant single-kernel stage (by measured time); every single-kernel
+        # stage is also reported under roofline_stages
+        roof, roof_all = None, {}
         if prof:
-            cands = {k: per_stage[k] for k in ("raycast_render", "raycast_icp", "integrate", "grey") if per_stage[k]}
-            if cands:
-                dom = max(cands, key=cands.get)
-                nvis = st["noVisibleEntries"]
-                b = stage_bytes(dom, tf.params(), nvis, W, H)
-                ach = b / (cands[dom] * 1e-3) / 1e9
-                traffic = None
-                pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-                if os.path.exists(pmc_path):
-                    try:
-                        traffic = json.load(open(pmc_path)).get(dom, {}).get("bytes_per_launch")
-                    except Exception:
-                        traffic = None
-                roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": traffic, "kernel": dom,
-                        "algorithmic_bytes_per_launch": b, "avg_launch_ms": round(cands[dom], 5)}
+            pmc = {}
+            pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc_path):
+                try:
+                    pmc = json.load(open(pmc_path))
+                except Exception:
+                    pmc = {}
+            nvis = st["noVisibleEntries"]
+            for k in SINGLE_KERNEL_STAGES:
+                if not per_stage.get(k) or (k == "icp" and not tf.icp_persistent()):
+                    continue
+                b = stage_bytes(k, tf.params(), nvis, W, H)
+                ach = b / (per_stage[k] * 1e-3) / 1e9
+                roof_all[k] = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                               "frac": round(ach / PEAK_HBM_GBS, 5),
+                               "traffic": (pmc.get(k) or {}).get("bytes_per_launch"),
+                               "kernel": KERNEL_OF_STAGE[k], "algorithmic_bytes_per_launch": b,
+                               "avg_launch_ms": round(per_stage[k], 5)}
+            if roof_all:
+                roof = roof_all[max(roof_all, key=lambda k: per_stage[k])]
         cpu = None
         if not args.no_cpu_baseline:
             v, n, dt = cpu_baseline(frames, pkw, args.cpu_seconds)
@@ -182,9 +192,11 @@ def main():
             "icp_integrate_ms_per_frame": None if icp_integ is None else round(icp_integ, 4),
             "stage_ms_per_frame": {k: (None if v is None else round(v, 4)) for k, v in per_stage.items()},
             "frames_ok": int(ok.sum()), "resets": int(st["n_resets"]),
+            "ok_frames_per_sec": round(int(ok.sum()) * (total_frames / args.steps) / elapsed_max, 2),
             "visible_blocks_last": st["noVisibleEntries"],
-            "allocated_blocks": tf.params().n_blocks - 1 - st["lastFreeBlockId"],
             "roofline": roof,
+            "roofline_stages": roof_all,
+            "icp_schedule": "persistent" if tf.icp_persistent() else "per_iteration",
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

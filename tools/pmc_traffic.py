@@ -1,0 +1,45 @@
+"""HBM-side traffic per launch of the bench's single-kernel stages, from the rocprofv3 PMC
+passes of tools/gpu_pmc.sh, corrected as MI355X_MICROARCH.md §HBM prescribes (gfx950
+FETCH_SIZE reports half the bytes of wide reads: x2; WRITE_SIZE as is; both in KiB).
+Writes profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
+
+    python tools/pmc_traffic.py gpurun_out/pmc_TAG [profiles/pmc_traffic.json]"""
+import csv, glob, json, os, sys
+from collections import defaultdict
+
+STAGE_OF = [("k_icp_frame", "icp"), ("k_raycast<2>", "raycast_render"), ("k_raycast<1>", "raycast_icp"),
+            ("k_integrate", "integrate")]
+
+
+def per_kernel(root, counter):
+    vals = defaultdict(list)
+    for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(path)):
+            if r["Counter_Name"] == counter:
+                vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    root = sys.argv[1]
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                            "profiles", "pmc_traffic.json")
+    fetch, write = per_kernel(root, "FETCH_SIZE"), per_kernel(root, "WRITE_SIZE")
+    res = {}
+    for key, stage in STAGE_OF:
+        f = [v for k, vs in fetch.items() if key in k for v in vs]
+        w = [v for k, vs in write.items() if key in k for v in vs]
+        if not f or not w:
+            continue
+        fb = sum(f) / len(f) * 1024 * 2
+        wb = sum(w) / len(w) * 1024
+        res[stage] = {"kernel": key, "fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb),
+                      "bytes_per_launch": round(fb + wb), "launches_sampled": len(f),
+                      "source": os.path.basename(os.path.normpath(root)),
+                      "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads), WRITE_SIZE x1, KiB->B"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

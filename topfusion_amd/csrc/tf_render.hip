@@ -164,6 +164,7 @@ struct RayArgs {
 // ROUND(pt) and, in the band, the interpolated read at pt.  ROUND(pt) is one of the eight
 // interpolation corners, so a step fetches the corners once (speculatively): one grid round
 // trip + one voxel round trip per step.
+template <bool MARK>
 __device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, int x, int y, float* pt)
 {
     int locId2 = (int)floorf((float)x / TF_SUBSAMPLE) + (int)floorf((float)y / TF_SUBSAMPLE) * a.W;
@@ -203,7 +204,7 @@ __device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, 
             k.bx = Ubx; k.by = Uby; k.bz = Ubz; k.voff = vu;
         }
         sdfValue = raw_sdf((unsigned)sel8(reinterpret_cast<const int(&)[8]>(q.raw), cu)) / 32767.0f;
-        if (a.visType && vmIndex) a.visType[vmIndex - 1] = 1;
+        if (MARK && vmIndex) a.visType[vmIndex - 1] = 1;
         if (!vmIndex) {
             stepLength = (float)TF_BLK;
         } else {
@@ -304,6 +305,10 @@ __device__ __forceinline__ int xcd_tile(int bid, int n)
     return t < n ? t : -1;
 }
 
+// MODE 0: castRay<false> -> point image; 1: castRay<true> (visibility marks) -> point image
+// (CreateICPMaps); 2: castRay<false> + renderGrey fused (renderImage in the frame path).
+// Distinct instantiations also give each use its own kernel name in rocprof.
+template <int MODE>
 __global__ void __launch_bounds__(256)
 k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles)
 {
@@ -313,8 +318,8 @@ k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles
     const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15), y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.H) return;
     float pt[3];
-    const float w = ray_march(a, st->M_ray, x, y, pt);
-    if (a.grey) {
+    const float w = ray_march<MODE == 1>(a, st->M_ray, x, y, pt);
+    if (MODE == 2) {
         // renderImage: lightSource = -Vector3f(pose.getColumn(2)) (VisualisationEngine_CUDA.cu:243)
         unsigned char v = 0;
         if (w > 0) v = grey_pixel(a.s, pt, -st->M_ray[8], -st->M_ray[9], -st->M_ray[10]);
@@ -335,10 +340,13 @@ static void ray_args(tf_ctx* c, RayArgs& a)
     a.oneOverVoxelSize = 1.0f / c->p.voxelSize; a.mu = c->p.mu;
 }
 
-static hipError_t launch_ray(tf_ctx* c, const RayArgs& a)
+static hipError_t launch_ray(tf_ctx* c, const RayArgs& a, int mode)
 {
     const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty;
-    hipLaunchKernelGGL(k_raycast, dim3((n + 7) / 8 * 8), dim3(256), 0, c->stream, a, c->st, tx, n);
+    const dim3 grid((n + 7) / 8 * 8);
+    if (mode == 0) hipLaunchKernelGGL(k_raycast<0>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
+    else if (mode == 1) hipLaunchKernelGGL(k_raycast<1>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
+    else hipLaunchKernelGGL(k_raycast<2>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
     return hipGetLastError();
 }
 
@@ -347,7 +355,7 @@ hipError_t tfk_raycast(tf_ctx* c, int update_visible)
     RayArgs a;
     ray_args(c, a);
     a.visType = update_visible ? c->visType : nullptr;
-    return launch_ray(c, a);
+    return launch_ray(c, a, update_visible ? 1 : 0);
 }
 
 // renderImage in the frame path: castRay<false> + renderGrey fused (the intermediate point
@@ -357,7 +365,7 @@ hipError_t tfk_raycast_grey(tf_ctx* c)
     RayArgs a;
     ray_args(c, a);
     a.grey = c->grey;
-    return launch_ray(c, a);
+    return launch_ray(c, a, 2);
 }
 
 
