@@ -184,6 +184,10 @@ typedef enum tf_stage_id {
     TF_STAGE_ICP_MAPS = 8         /* renderICP + resizePointsNormals */
 } tf_stage_id;
 tf_status tf_profile_enable(tf_ctx* ctx, int enable);
+/* time only the stages whose bit (1 << tf_stage_id) is set; 0 disables.  Each timed stage
+ * adds two event records per frame to the stream, which cost GPU time of their own, so a
+ * throughput measurement times only the stage it needs. */
+tf_status tf_profile_stages(tf_ctx* ctx, unsigned mask);
 tf_status tf_profile_reset(tf_ctx* ctx);
 /* ms[i] = accumulated milliseconds, counts[i] = frames measured, for i < n (n <= 9) */
 tf_status tf_profile_read(tf_ctx* ctx, double* ms, long long* counts, int n);

@@ -104,6 +104,7 @@ def load():
         "tf_set_pose": ([P, P], I),
         "tf_set_counters": ([P, I, I, I], I),
         "tf_profile_enable": ([P, I], I),
+        "tf_profile_stages": ([P, ctypes.c_uint], I),
         "tf_profile_reset": ([P], I),
         "tf_profile_read": ([P, P, P, I], I),
     }

@@ -91,17 +91,15 @@ static void ctx_free(tf_ctx* c)
     if (!c) return;
     void* bufs[] = { c->hash, c->excessList, c->vba, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->raycast, c->grey,
-                     c->blockBox, c->blockZ, c->blockTiles, c->blockKeep, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st };
+                     c->blockBox, c->blockZ, c->blockTiles, c->blockKeep, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
+                     c->frame_ok, c->frame_mode };
     for (void* b : bufs) if (b) (void)hipFree(b);
-    for (int l = 0; l < TF_LEVELS; ++l) {
-        if (c->depth_pyr[l]) (void)hipFree(c->depth_pyr[l]);
-        if (c->curr_pts[l]) (void)hipFree(c->curr_pts[l]);
-        if (c->curr_nrm[l]) (void)hipFree(c->curr_nrm[l]);
-        if (c->prev_pts[l]) (void)hipFree(c->prev_pts[l]);
-        if (c->prev_nrm[l]) (void)hipFree(c->prev_nrm[l]);
-    }
+    // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
+    float4* maps[4] = { c->curr_pts[0], c->curr_nrm[0], c->prev_pts[0], c->prev_nrm[0] };
+    for (float4* m : maps) if (m) (void)hipFree(m);
+    for (int l = 0; l < TF_LEVELS; ++l) if (c->depth_pyr[l]) (void)hipFree(c->depth_pyr[l]);
     if (c->st_host) (void)hipHostFree(c->st_host);
-    for (int i = 0; i < 2 * TF_NUM_STAGES; ++i) if (c->prof_ev[i]) (void)hipEventDestroy(c->prof_ev[i]);
+    for (int i = 0; i < 2 * TF_NUM_STAGES * TF_PROF_RING; ++i) if (c->prof_ev[i]) (void)hipEventDestroy(c->prof_ev[i]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -121,14 +119,22 @@ static tf_status sync_state(tf_ctx* c)
 
 // TopFu::reset (topfu.cpp:141-152): pose history -> [I], ResetScene.  The render state
 // (visible list / types / range image) is deliberately left as is, like the reference.
+__global__ void k_host_reset(TfDevState* st)
+{
+    if (st->frame_counter) st->n_resets++;
+    st->frame_counter = 0;
+    for (int i = 0; i < 12; ++i) st->pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+}
+
 static tf_status ctx_reset(tf_ctx* c)
 {
-    if (c->frame_counter) c->n_resets++;
-    c->frame_counter = 0;
-    float I[12] = { 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0 };
-    TF_CHECK(hipMemcpyAsync(c->st->pose, I, sizeof(I), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_host_reset, dim3(1), dim3(1), 0, c->stream, c->st);
+    TF_CHECK(hipGetLastError());
     TF_CHECK(tfk_reset_scene(c));
-    TF_CHECK(hipStreamSynchronize(c->stream));
+    const tf_status s = sync_state(c);
+    if (s != TF_OK) return s;
+    c->frame_counter = c->st_host->frame_counter;
+    c->n_resets = c->st_host->n_resets;
     return TF_OK;
 }
 
@@ -180,14 +186,22 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->blockKeep, (size_t)pin->vis_capacity);
     ALLOC(c->depth_in, sizeof(uint16_t) * npx);
     ALLOC(c->dists, sizeof(float) * npx);
-    for (int l = 0; l < TF_LEVELS; ++l) {
-        size_t n = (size_t)c->lw[l] * c->lh[l];
-        ALLOC(c->depth_pyr[l], sizeof(uint16_t) * n);
-        ALLOC(c->curr_pts[l], sizeof(float4) * n);
-        ALLOC(c->curr_nrm[l], sizeof(float4) * n);
-        ALLOC(c->prev_pts[l], sizeof(float4) * n);
-        ALLOC(c->prev_nrm[l], sizeof(float4) * n);
+    {   // each map's three pyramid levels are contiguous in one allocation
+        size_t ntot = 0;
+        for (int l = 0; l < TF_LEVELS; ++l) ntot += (size_t)c->lw[l] * c->lh[l];
+        ALLOC(c->curr_pts[0], sizeof(float4) * ntot);
+        ALLOC(c->curr_nrm[0], sizeof(float4) * ntot);
+        ALLOC(c->prev_pts[0], sizeof(float4) * ntot);
+        ALLOC(c->prev_nrm[0], sizeof(float4) * ntot);
+        for (int l = 1; l < TF_LEVELS; ++l) {
+            const size_t off = (size_t)c->lw[l - 1] * c->lh[l - 1];
+            c->curr_pts[l] = c->curr_pts[l - 1] + off; c->curr_nrm[l] = c->curr_nrm[l - 1] + off;
+            c->prev_pts[l] = c->prev_pts[l - 1] + off; c->prev_nrm[l] = c->prev_nrm[l - 1] + off;
+        }
+        for (int l = 0; l < TF_LEVELS; ++l) ALLOC(c->depth_pyr[l], sizeof(uint16_t) * (size_t)c->lw[l] * c->lh[l]);
     }
+    ALLOC(c->frame_ok, sizeof(int) * TF_PROF_RING);
+    ALLOC(c->frame_mode, sizeof(int) * TF_PROF_RING);
     ALLOC(c->icp_partial, sizeof(float) * 28 * 256);
     ALLOC(c->icp_ticket, 64);
     ALLOC(c->icp_tagged, sizeof(unsigned long long) * (256 * 28 + 16));
@@ -250,9 +264,17 @@ extern "C" tf_status tf_reset(tf_ctx* c)
     return ctx_reset(c);
 }
 
+// stage entry points run the tracking-path kernels unconditionally
+__global__ void k_stage_begin(TfDevState* st)
+{
+    st->abort = 0;
+    st->mode = 1;
+}
+
 static hipError_t clear_abort(tf_ctx* c)
 {
-    return hipMemsetAsync(&c->st->abort, 0, sizeof(int), c->stream);
+    hipLaunchKernelGGL(k_stage_begin, dim3(1), dim3(1), 0, c->stream, c->st);
+    return hipGetLastError();
 }
 
 static void swap_pyramids(tf_ctx* c)
@@ -264,83 +286,109 @@ static void swap_pyramids(tf_ctx* c)
 }
 
 // ---- per-stage event timing -----------------------------------------------------------
-#define STAGE(id, expr)                                                                     \
-    do {                                                                                    \
-        if (c->prof_enabled) TF_CHECK(hipEventRecord(c->prof_ev[2 * (id)], c->stream));    \
-        TF_CHECK(expr);                                                                     \
-        if (c->prof_enabled) {                                                              \
-            TF_CHECK(hipEventRecord(c->prof_ev[2 * (id) + 1], c->stream));                  \
-            c->prof_pending[id] = 1;                                                        \
-        }                                                                                   \
+// Events ring: TF_PROF_RING frames x (start, end) per stage.  Frames are attributed after a
+// sync, once their mode / ok flags are known, and only for the stages that did work.
+#define STAGE(id, expr)                                                                       \
+    do {                                                                                      \
+        const bool timed_ = c->prof_enabled && ((c->prof_mask >> (id)) & 1u);                 \
+        if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id)), c->stream));       \
+        TF_CHECK(expr);                                                                       \
+        if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id) + 1), c->stream));   \
     } while (0)
 
-static void prof_collect(tf_ctx* c)
+static hipEvent_t prof_event(tf_ctx* c, int slot, int k)
 {
-    if (!c->prof_enabled) return;
-    for (int i = 0; i < TF_NUM_STAGES; ++i) {
-        if (!c->prof_pending[i]) continue;
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, c->prof_ev[2 * i], c->prof_ev[2 * i + 1]) == hipSuccess) {
-            c->prof_ms[i] += ms;
-            c->prof_count[i] += 1;
-        }
-        c->prof_pending[i] = 0;
-    }
+    return c->prof_ev[(slot % TF_PROF_RING) * 2 * TF_NUM_STAGES + k];
 }
 
-// enqueue one TopFu::operator() frame; returns whether the frame took the tracking path
-static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, bool* tracked)
+static bool stage_ran(int stage, int mode, int ok)
 {
-    TF_CHECK(clear_abort(c));
-    STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch));     // topfu.cpp:166-197
-    if (c->frame_counter == 0) {                                     // topfu.cpp:200-209
-        TF_CHECK(tfk_frame0_matrices(c));
-        STAGE(TF_STAGE_ALLOC, tfk_alloc(c));
-        STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c));
-        swap_pyramids(c);
-        *tracked = false;
-        return TF_OK;
-    }
-    STAGE(TF_STAGE_ICP, tfk_icp(c, 1));                              // topfu.cpp:242-243
-    STAGE(TF_STAGE_ALLOC, tfk_alloc(c));                             // topfu.cpp:281
-    STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c));                     // topfu.cpp:282
+    if (stage == TF_STAGE_PREPROCESS) return true;
+    if (stage == TF_STAGE_ICP) return mode == 1;
+    if (stage == TF_STAGE_ALLOC || stage == TF_STAGE_INTEGRATE) return mode == 0 || ok == 1;
+    if (stage == TF_STAGE_GREY) return false;                      // fused into RAYCAST_RENDER
+    return mode == 1 && ok == 1;
+}
+
+// attribute the timed stages of batch slots [first, first+n) (their events must be complete)
+static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const int* mode)
+{
+    if (!c->prof_enabled) return TF_OK;
+    for (int f = 0; f < n; ++f)
+        for (int i = 0; i < TF_NUM_STAGES; ++i) {
+            if (!((c->prof_mask >> i) & 1u) || !stage_ran(i, mode[f], ok[f])) continue;
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, prof_event(c, first + f, 2 * i), prof_event(c, first + f, 2 * i + 1)) == hipSuccess) {
+                c->prof_ms[i] += ms;
+                c->prof_count[i] += 1;
+            }
+        }
+    return TF_OK;
+}
+
+// enqueue one TopFu::operator() frame into batch slot `slot` (no host synchronisation).
+// The frame's branches (frame 0 / tracking / ICP failure -> reset, topfu.cpp:161-330) are
+// decided on the device: the preprocess kernel starts the frame (tf_frame_begin sets
+// st->mode), every later kernel checks st->mode / st->abort, and the gated reset kernel ends
+// it (frame counters, per-slot ok flag).  A batch is therefore enqueued back to back.
+static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, int slot)
+{
+    STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, 1));  // topfu.cpp:166-197 (+ frame begin)
+    STAGE(TF_STAGE_ICP, tfk_icp(c, 1));                              // topfu.cpp:242-243 (tracking only)
+    STAGE(TF_STAGE_ALLOC, tfk_alloc(c));                             // topfu.cpp:202 / 281
+    STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1));                  // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
     STAGE(TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c));            // renderImage (raycast + grey), topfu.cpp:284-285
     STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c));         // topfu.cpp:306
     STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));                  // CreateICPMaps, topfu.cpp:307
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps(c));                       // + resizePointsNormals :308-309
-    *tracked = true;
+    TF_CHECK(tfk_reset_scene_on_failure(c, slot));                   // frame end; topfu.cpp:263-264
     return TF_OK;
 }
 
-static tf_status finish_frame(tf_ctx* c, bool tracked)
+// sync, read back slots [first, first+n) and the state; ok_out gets 1/0 per frame
+static tf_status finish_frames(tf_ctx* c, int first, int n, int* ok_out)
 {
+    int okb[TF_PROF_RING], modeb[TF_PROF_RING];
+    TF_CHECK(hipMemcpyAsync(okb, c->frame_ok + first, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+    TF_CHECK(hipMemcpyAsync(modeb, c->frame_mode + first, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
-    prof_collect(c);
-    if (c->st_host->icp_ok < 0) return TF_HIP_ERROR;                  // persistent ICP lost a peer
-    if (tracked && !c->st_host->icp_ok) {                            // topfu.cpp:263-264
-        s = ctx_reset(c);
-        if (s != TF_OK) return s;
-        return TF_ICP_FAIL;
+    c->frame_counter = c->st_host->frame_counter;
+    c->n_resets = c->st_host->n_resets;
+    prof_collect(c, first, n, okb, modeb);
+    tf_status r = TF_OK;
+    for (int i = 0; i < n; ++i) {
+        if (okb[i] < 0) return TF_HIP_ERROR;
+        if (ok_out) ok_out[i] = okb[i];
+        if (okb[i] == 0) r = TF_ICP_FAIL;
     }
-    c->frame_counter++;
-    return TF_OK;
+    return r;
 }
 
 extern "C" tf_status tf_profile_enable(tf_ctx* c, int enable)
 {
     if (!c) return TF_INVALID_ARG;
     if (enable && !c->prof_ev[0]) {
-        for (int i = 0; i < 2 * TF_NUM_STAGES; ++i) TF_CHECK(hipEventCreate(&c->prof_ev[i]));
+        for (int i = 0; i < 2 * TF_NUM_STAGES * TF_PROF_RING; ++i) TF_CHECK(hipEventCreate(&c->prof_ev[i]));
     }
     c->prof_enabled = enable ? 1 : 0;
+    c->prof_mask = (1u << TF_NUM_STAGES) - 1;
+    return TF_OK;
+}
+
+extern "C" tf_status tf_profile_stages(tf_ctx* c, unsigned mask)
+{
+    if (!c) return TF_INVALID_ARG;
+    tf_status s = tf_profile_enable(c, mask != 0);
+    if (s != TF_OK) return s;
+    c->prof_mask = mask;
     return TF_OK;
 }
 
 extern "C" tf_status tf_profile_reset(tf_ctx* c)
 {
     if (!c) return TF_INVALID_ARG;
-    for (int i = 0; i < TF_NUM_STAGES; ++i) { c->prof_ms[i] = 0; c->prof_count[i] = 0; c->prof_pending[i] = 0; }
+    for (int i = 0; i < TF_NUM_STAGES; ++i) { c->prof_ms[i] = 0; c->prof_count[i] = 0; }
     return TF_OK;
 }
 
@@ -362,7 +410,7 @@ static void fill_stats(tf_ctx* c, tf_stats* st)
     st->lastFreeExcessListId = d->lastFreeExcessListId;
     st->noVisibleEntries = d->noVisibleEntries;
     st->noTotalBlocks = d->noTotalBlocks;
-    st->frame_counter = c->frame_counter;
+    st->frame_counter = c->frame_counter;   // mirrors of the device counters (last sync)
     st->icp_iterations = d->icp_iters;
     st->icp_ok = d->icp_ok;
     st->n_resets = c->n_resets;
@@ -373,16 +421,10 @@ extern "C" tf_status tf_process_frame(tf_ctx* c, const uint16_t* dev_depth, size
 {
     if (!c || !dev_depth) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
-    bool tracked = false;
-    tf_status s = enqueue_frame(c, dev_depth, pitch, &tracked);
+    tf_status s = enqueue_frame(c, dev_depth, pitch, 0);
     if (s != TF_OK) return s;
-    s = finish_frame(c, tracked);
+    s = finish_frames(c, 0, 1, nullptr);
     if (s != TF_OK && s != TF_ICP_FAIL) return s;
-    if (s == TF_ICP_FAIL) {
-        tf_status s2 = sync_state(c);
-        if (s2 != TF_OK) return s2;
-        c->st_host->icp_ok = 0;
-    }
     if (pose_out) memcpy(pose_out, c->st_host->pose, sizeof(float) * 12);
     fill_stats(c, stats);
     return s;
@@ -398,14 +440,20 @@ extern "C" tf_status tf_process_frame_host(tf_ctx* c, const uint16_t* host_depth
     return tf_process_frame(c, c->depth_in, (size_t)c->W * 2, pose_out, stats);
 }
 
+// a batch of device-resident frames: enqueued TF_PROF_RING at a time with no host round trip
+// inside a group (the frame's branches are decided on the device)
 extern "C" tf_status tf_process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t stride, int n, int* ok_out)
 {
     if (!c || !dev_frames || n < 0) return TF_INVALID_ARG;
-    for (int i = 0; i < n; ++i) {
-        const uint16_t* f = (const uint16_t*)((const char*)dev_frames + (size_t)i * stride);
-        tf_status s = tf_process_frame(c, f, (size_t)c->W * 2, nullptr, nullptr);
+    for (int first = 0; first < n; first += TF_PROF_RING) {
+        const int m = n - first < TF_PROF_RING ? n - first : TF_PROF_RING;
+        for (int i = 0; i < m; ++i) {
+            const uint16_t* f = (const uint16_t*)((const char*)dev_frames + (size_t)(first + i) * stride);
+            tf_status s = enqueue_frame(c, f, (size_t)c->W * 2, i);
+            if (s != TF_OK) return s;
+        }
+        tf_status s = finish_frames(c, 0, m, ok_out ? ok_out + first : nullptr);
         if (s != TF_OK && s != TF_ICP_FAIL) return s;
-        if (ok_out) ok_out[i] = (s == TF_OK);
     }
     return TF_OK;
 }
@@ -492,6 +540,7 @@ extern "C" tf_status tf_stage_preprocess_host(tf_ctx* c, const uint16_t* host_de
 extern "C" tf_status tf_stage_icp(tf_ctx* c, float affine_rt[12], int* ok, int* iterations)
 {
     if (!c) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     TF_CHECK(tfk_icp(c, 0));
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
@@ -506,6 +555,7 @@ extern "C" tf_status tf_stage_icp(tf_ctx* c, float affine_rt[12], int* ok, int* 
 extern "C" tf_status tf_stage_alloc(tf_ctx* c, const float pose_rt[12])
 {
     if (!c || !pose_rt) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_alloc(c));
@@ -516,6 +566,7 @@ extern "C" tf_status tf_stage_alloc(tf_ctx* c, const float pose_rt[12])
 extern "C" tf_status tf_stage_integrate(tf_ctx* c, const float pose_rt[12])
 {
     if (!c || !pose_rt) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_integrate(c));
@@ -526,6 +577,7 @@ extern "C" tf_status tf_stage_integrate(tf_ctx* c, const float pose_rt[12])
 extern "C" tf_status tf_stage_expected_depths(tf_ctx* c, const float pose_rt[12])
 {
     if (!c || !pose_rt) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_expected_depths(c));
@@ -536,6 +588,7 @@ extern "C" tf_status tf_stage_expected_depths(tf_ctx* c, const float pose_rt[12]
 extern "C" tf_status tf_stage_raycast(tf_ctx* c, const float invM_rt[12], int update_visible)
 {
     if (!c || !invM_rt) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, invM_rt, 0);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_raycast(c, update_visible));
@@ -546,6 +599,7 @@ extern "C" tf_status tf_stage_raycast(tf_ctx* c, const float invM_rt[12], int up
 extern "C" tf_status tf_stage_icp_maps(tf_ctx* c, const float invM_rt[12])
 {
     if (!c || !invM_rt) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, invM_rt, 0);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_icp_maps(c));
@@ -556,6 +610,7 @@ extern "C" tf_status tf_stage_icp_maps(tf_ctx* c, const float invM_rt[12])
 extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
 {
     if (!c || !invM_rt) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, invM_rt, 0);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_render_grey(c));

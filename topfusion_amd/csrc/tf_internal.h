@@ -19,6 +19,7 @@
 #define TF_RB_SIZE 16           // renderingBlockSizeX/Y (VisualisationEngine_Shared.hpp:25-26)
 #define TF_LEVELS 3
 #define TF_NUM_STAGES 9     // tf_stage_id in include/tfusion_hip.h
+#define TF_PROF_RING 32     // frames enqueued between host syncs (and timing-event ring slots)
 
 // HashEntry, VoxelBlockHash.hpp:32-44 (16 B; one dwordx4 probe)
 struct __attribute__((aligned(16))) TfHashEntry {
@@ -54,6 +55,14 @@ struct TfDevState {
     unsigned tiles_total;    // rendering tiles requested (before the MAX cap)
     int pad_[2];             // alloc totals (tf_scene.hip)
     unsigned icp_gen;        // last generation tag used by the persistent ICP kernel
+    // device-driven frame control (TopFu::operator() branches decided on the device, so a
+    // batch of frames is enqueued without host round trips)
+    int mode;                // this frame: 0 = frame-0 path (integrate only), 1 = tracking path
+    int frame_counter;       // TopFu::frame_counter_
+    int n_resets;            // resets taken after ICP failures
+    unsigned ed_ticket;      // CreateExpectedDepths: last-workgroup ticket (zero between launches)
+    int ed_capped;           // tiles exceeded MAX_RENDERING_BLOCKS this frame
+    int pad2_[3];
 };
 
 // ---------------------------------------------------------------------------------------
@@ -208,14 +217,16 @@ struct tf_ctx {
     // device state
     TfDevState* st;
     TfDevState* st_host;     // pinned mirror
-    int frame_counter;       // host mirror of TopFu::frame_counter_
-    int n_resets;
+    int frame_counter;       // host mirror of st->frame_counter (updated at every sync)
+    int n_resets;            // host mirror of st->n_resets
+    int* frame_ok;           // per enqueued frame of a batch: 1 ok, 0 ICP failure (reset), -1 error
+    int* frame_mode;         // per enqueued frame of a batch: st->mode it ran with
     int alloc_chunks;        // N_tot / 4096
     int vis_chunks;
     // per-stage HIP-event timing on the context stream (tf_profile_*)
     int prof_enabled;
-    hipEvent_t prof_ev[2 * TF_NUM_STAGES];
-    int prof_pending[TF_NUM_STAGES];
+    unsigned prof_mask;      // stages timed (bit = tf_stage_id)
+    hipEvent_t prof_ev[2 * TF_NUM_STAGES * TF_PROF_RING];
     double prof_ms[TF_NUM_STAGES];
     long long prof_count[TF_NUM_STAGES];
 };
@@ -223,14 +234,15 @@ struct tf_ctx {
 // ---------------------------------------------------------------------------------------
 // launchers (one per kernel family); all enqueue on ctx->stream
 // ---------------------------------------------------------------------------------------
-hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch);
+hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, int frame_begin = 0);
 hipError_t tfk_icp(tf_ctx* c, int pose_update);
 int tfk_icp_persistent_ok(tf_ctx* c);      // k_icp_frame fits (co-residency, slot count)
 hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / raycast matrices
 hipError_t tfk_reset_scene(tf_ctx* c);
+hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot);   // frame end + ResetScene if ICP failed
 hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a hash upload)
 hipError_t tfk_alloc(tf_ctx* c);
-hipError_t tfk_integrate(tf_ctx* c);
+hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_grey(tf_ctx* c);
 hipError_t tfk_raycast_grey(tf_ctx* c);    // renderImage raycast + grey, fused (frame path)

@@ -312,7 +312,7 @@ template <int MODE>
 __global__ void __launch_bounds__(256)
 k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles)
 {
-    if (st->abort) return;
+    if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int tile = xcd_tile(blockIdx.x, n_tiles);     // grid padded to a multiple of 8
     if (tile < 0) return;
     const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15), y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
@@ -372,7 +372,7 @@ hipError_t tfk_raycast_grey(tf_ctx* c)
 __global__ void __launch_bounds__(256)
 k_grey(SceneView s, const float4* __restrict__ ray, int n, const TfDevState* __restrict__ st, uchar4* __restrict__ out)
 {
-    if (st->abort) return;
+    if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     // lightSource = -Vector3f(pose.getColumn(2)) (VisualisationEngine_CUDA.cu:243)
@@ -460,7 +460,7 @@ __device__ __forceinline__ void resize4(const float4* v, const float4* n, float4
 __global__ void __launch_bounds__(256)
 k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
 {
-    if (st->abort) return;
+    if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int l = blockIdx.z;
     const int lw = a.W >> l, lh = a.H >> l;
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -520,7 +520,7 @@ struct EdArgs {
 __global__ void __launch_bounds__(256)
 k_ed_project(EdArgs a, TfDevState* __restrict__ st)
 {
-    if (st->abort) return;
+    if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int tid = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
     const int npx = a.W * a.H;
     for (int i = tid; i < npx; i += stride) a.range[i] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
@@ -569,45 +569,54 @@ k_ed_project(EdArgs a, TfDevState* __restrict__ st)
         a.box[i] = box; a.z[i] = zr; a.tiles[i] = ntiles;
         if (ntiles) atomicAdd(&st->tiles_total, (unsigned)ntiles);
     }
-}
-
-// MAX_RENDERING_BLOCKS handling (VisualisationHelper.cu:70-74): blocks whose tiles do not fit
-// are dropped, in visible-list order.  Only does work when the cap is exceeded.
-__global__ void k_ed_cap(EdArgs a, TfDevState* __restrict__ st)
-{
-    if (st->abort) return;
-    unsigned total = st->tiles_total;
-    if (threadIdx.x == 0) st->noTotalBlocks = (int)(total > a.cap ? a.cap : total);
-    if (total <= a.cap) return;
-    if (threadIdx.x != 0) return;
-    const int n = st->noVisibleEntries;
-    unsigned off = 0;
-    for (int i = 0; i < n; ++i) {
-        unsigned need = (unsigned)a.tiles[i];
-        a.keep[i] = (need && off + need <= a.cap) ? 1 : 0;
-        off += need;
+    // the last workgroup to finish applies MAX_RENDERING_BLOCKS (VisualisationHelper.cu:70-74):
+    // blocks whose tiles do not fit are dropped in visible-list order (serial; only when the
+    // cap is exceeded), then re-arms the counters for the next frame
+    __shared__ int last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(&st->ed_ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last || threadIdx.x != 0) return;
+    __threadfence();
+    const unsigned total = __hip_atomic_load(&st->tiles_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st->noTotalBlocks = (int)(total > a.cap ? a.cap : total);
+    st->ed_capped = total > a.cap;
+    if (total > a.cap) {
+        unsigned off = 0;
+        for (int i = 0; i < n; ++i) {
+            unsigned need = (unsigned)a.tiles[i];
+            a.keep[i] = (need && off + need <= a.cap) ? 1 : 0;
+            off += need;
+        }
     }
+    st->tiles_total = 0;
+    st->ed_ticket = 0;
 }
 
-// fillBlocks_device (VisualisationHelper.cu:105-121): per-pixel min/max of the block z-range
+// fillBlocks_device (VisualisationHelper.cu:105-121): per-pixel min/max of the block z-range.
+// One workgroup per block (grid-strided), its threads over the block's pixel box, so a huge
+// box (a block just in front of the camera spans the whole image) costs one workgroup a few
+// thousand no-return atomics instead of one thread ~10^5 serial ones.
 __global__ void __launch_bounds__(256)
 k_ed_fill(EdArgs a, const TfDevState* __restrict__ st)
 {
-    if (st->abort) return;
+    if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int n = st->noVisibleEntries;
-    const bool capped = st->tiles_total > a.cap;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        int4 b = a.box[i];
+    const bool capped = st->ed_capped;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int4 b = a.box[i];
         if (b.x < 0) continue;
         if (capped && !a.keep[i]) continue;
-        float2 zr = a.z[i];
-        int zmin = __float_as_int(zr.x), zmax = __float_as_int(zr.y);   // positive floats order as ints
-        for (int y = b.y; y <= b.w; ++y)
-            for (int x = b.x; x <= b.z; ++x) {
-                int* px = (int*)(a.range + x + y * a.W);
-                atomicMin(px, zmin);
-                atomicMax(px + 1, zmax);
-            }
+        const float2 zr = a.z[i];
+        const int zmin = __float_as_int(zr.x), zmax = __float_as_int(zr.y);   // positive floats order as ints
+        const int bw = b.z - b.x + 1, npx = bw * (b.w - b.y + 1);
+        for (int k = threadIdx.x; k < npx; k += 256) {
+            const int y = b.y + k / bw, x = b.x + k % bw;
+            int* px = (int*)(a.range + x + y * a.W);
+            atomicMin(px, zmin);
+            atomicMax(px + 1, zmax);
+        }
     }
 }
 
@@ -619,10 +628,8 @@ hipError_t tfk_expected_depths(tf_ctx* c)
     a.W = c->W; a.H = c->H;
     a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy; a.voxelSize = c->p.voxelSize;
     a.cap = (unsigned)c->p.max_render_blocks;
-    hipError_t e = hipMemsetAsync(&c->st->tiles_total, 0, sizeof(unsigned), c->stream);
-    if (e != hipSuccess) return e;
+    // st->tiles_total / ed_ticket are zero between launches (tf_create, re-armed by k_ed_project)
     hipLaunchKernelGGL(k_ed_project, dim3(1024), dim3(256), 0, c->stream, a, c->st);
-    hipLaunchKernelGGL(k_ed_cap, dim3(1), dim3(64), 0, c->stream, a, c->st);
-    hipLaunchKernelGGL(k_ed_fill, dim3(256), dim3(256), 0, c->stream, a, c->st);
+    hipLaunchKernelGGL(k_ed_fill, dim3(512), dim3(256), 0, c->stream, a, c->st);
     return hipGetLastError();
 }

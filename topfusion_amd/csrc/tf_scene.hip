@@ -29,8 +29,26 @@ __device__ __forceinline__ void load16(const unsigned char* p, unsigned long lon
 // ResetScene (SceneReconstructionEngine_host.cu:51-73)
 // ---------------------------------------------------------------------------------------
 __global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_blocks, TfHashEntry* hash,
-                              int n_total, int* excessList, int n_excess, TfDevState* st, int2* grid)
+                              int n_total, int* excessList, int n_excess, TfDevState* st, int2* grid, int on_failure,
+                              int* frame_ok, int* frame_mode, int slot)
 {
+    if (on_failure && blockIdx.x == 0 && threadIdx.x == 0) {
+        // end of the device-driven frame (return values of topfu.cpp:209 / 264 / 329); only
+        // frame_counter / n_resets / pose change here, never the mode / icp_ok read below
+        const int mode = st->mode, icp_ok = st->icp_ok;
+        int ok;
+        if (mode == 0) { st->frame_counter = 1; ok = 1; }
+        else if (icp_ok < 0) ok = -1;                       // persistent ICP lost a peer
+        else if (icp_ok == 0) {                             // return reset(), false
+            st->n_resets++;
+            st->frame_counter = 0;
+            for (int i = 0; i < 12; ++i) st->pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+            ok = 0;
+        } else { st->frame_counter++; ok = 1; }
+        frame_ok[slot] = ok;
+        frame_mode[slot] = mode;
+    }
+    if (on_failure && !(st->mode == 1 && st->icp_ok == 0)) return;   // topfu.cpp:263-264 only
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     uint4 vfill = make_uint4(32767u, 32767u, 32767u, 32767u);   // Voxel_s(): sdf 32767, w 0
@@ -53,7 +71,16 @@ __global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_
 hipError_t tfk_reset_scene(tf_ctx* c)
 {
     hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, c->vba, (size_t)c->p.n_blocks * TF_BLK3,
-                       c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st, c->bgrid);
+                       c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st, c->bgrid, 0,
+                       nullptr, nullptr, 0);
+    return hipGetLastError();
+}
+
+hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot)
+{
+    hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, c->vba, (size_t)c->p.n_blocks * TF_BLK3,
+                       c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st, c->bgrid, 1,
+                       c->frame_ok, c->frame_mode, slot);
     return hipGetLastError();
 }
 
@@ -497,6 +524,10 @@ struct IntegArgs {
     float fx, fy, cx, cy;
     float voxelSize, mu;
     int maxW;
+    // frame 0 of the device-driven frame: prev_ = curr_ (topfu.cpp:205 swaps the pyramids;
+    // copying keeps the buffer pointers fixed); levels contiguous, n_maps float4 per map
+    const float4* curr_pts; const float4* curr_nrm; float4* prev_pts; float4* prev_nrm;
+    int n_maps;
 };
 
 __device__ __forceinline__ unsigned integ_voxel(unsigned vox, float px, float py, float pz, const float* M,
@@ -530,6 +561,13 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
             const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba)
 {
     if (st->abort) return;
+    if (a.n_maps > 0 && st->mode == 0) {
+        const int stride = gridDim.x * 256;
+        for (int k = blockIdx.x * 256 + threadIdx.x; k < a.n_maps; k += stride) {
+            a.prev_pts[k] = a.curr_pts[k];
+            a.prev_nrm[k] = a.curr_nrm[k];
+        }
+    }
     const int n = st->noVisibleEntries;
     float M[16];
 #pragma unroll
@@ -552,9 +590,13 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
     }
 }
 
-hipError_t tfk_integrate(tf_ctx* c)
+hipError_t tfk_integrate(tf_ctx* c, int frame_path)
 {
     IntegArgs a;
+    a.curr_pts = c->curr_pts[0]; a.curr_nrm = c->curr_nrm[0]; a.prev_pts = c->prev_pts[0]; a.prev_nrm = c->prev_nrm[0];
+    a.n_maps = 0;
+    if (frame_path)
+        for (int l = 0; l < TF_LEVELS; ++l) a.n_maps += c->lw[l] * c->lh[l];
     a.dists = c->dists; a.W = c->W; a.H = c->H;
     a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy;
     a.voxelSize = c->p.voxelSize; a.mu = c->p.mu; a.maxW = c->p.maxW;

@@ -125,8 +125,16 @@ class TopFu:
         return bool(v.value)
 
     # -- per-stage HIP-event timing ----------------------------------------------------
-    def profile(self, enable=True):
-        L.check(L.load().tf_profile_enable(self._h, int(enable)), "tf_profile_enable")
+    def profile(self, enable=True, stages=None):
+        """Time every stage (enable=True), none, or only the named stages (HIP events on the
+        context stream; each timed stage costs GPU time of its own)."""
+        if stages is None:
+            L.check(L.load().tf_profile_enable(self._h, int(enable)), "tf_profile_enable")
+        else:
+            mask = 0
+            for s in stages:
+                mask |= 1 << L.STAGE_NAMES.index(s)
+            L.check(L.load().tf_profile_stages(self._h, mask if enable else 0), "tf_profile_stages")
         L.check(L.load().tf_profile_reset(self._h), "tf_profile_reset")
 
     def profile_read(self):
