@@ -31,15 +31,27 @@ KERNEL_OF_STAGE = {"icp": "k_icp_frame", "raycast_render": "k_raycast<2> (raycas
                    "raycast_icp": "k_raycast<1>", "integrate": "k_integrate"}
 SINGLE_KERNEL_STAGES = tuple(KERNEL_OF_STAGE)
 
+# SURVEY.md §8d configs.  C3 raises the capacities past the reference's (2^21 blocks = 4 GiB of
+# voxels, 2^22 buckets, 2^20 excess) -- sized for 288 GB of HBM, not for the reference's GPU.
+CONFIGS = {
+    "C2": dict(cols=640, rows=480, voxel=0.005, capacity={}),
+    "C3": dict(cols=1280, rows=960, voxel=0.002,
+               capacity=dict(n_buckets=1 << 22, n_excess=1 << 20, n_blocks=1 << 21, vis_capacity=1 << 21,
+                             max_render_blocks=1 << 20)),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--cols", type=int, default=640)
-    ap.add_argument("--rows", type=int, default=480)
-    ap.add_argument("--voxel", type=float, default=0.005)
+    ap.add_argument("--config", choices=["C2", "C3"], default="C2",
+                    help="C2: 640x480 orbit, 5 mm (BASELINE configs[1], the headline); "
+                         "C3: 1280x960, 2 mm, capacities beyond the reference's (configs[2])")
+    ap.add_argument("--cols", type=int, default=None)
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--voxel", type=float, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample length")
     ap.add_argument("--no-profile", action="store_true", help="disable the per-stage HIP-event timing")
@@ -108,9 +120,13 @@ def main():
         torch.cuda.set_device(0)
     from topfusion_amd import TopFu, default_params, synth
 
-    W, H = args.cols, args.rows
+    cfg = CONFIGS[args.config]
+    W = args.cols or cfg["cols"]
+    H = args.rows or cfg["rows"]
+    if args.voxel is None:
+        args.voxel = cfg["voxel"]
     fx, fy, cx, cy = synth.intrinsics(W, H)
-    pkw = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=args.voxel)
+    pkw = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=args.voxel, **cfg["capacity"])
     n_breakdown = 0 if args.no_profile else min(args.breakdown_frames, args.steps)
     n_frames = args.warmup + args.steps
     frames = synth.orbit_sequence(n_frames, W, H, seed=7 + rank)
@@ -178,7 +194,7 @@ def main():
             pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
             if os.path.exists(pmc_path):
                 try:
-                    pmc = json.load(open(pmc_path))
+                    pmc = json.load(open(pmc_path)).get(args.config, {})
                 except Exception:
                     pmc = {}
             nvis = st["noVisibleEntries"]
@@ -204,7 +220,7 @@ def main():
                    "sample": f"oracle (serial C restatement) on frames 0..{n - 1} of the same C2 stream, "
                              f"{W}x{H}, {dt:.1f} s, 1 thread, host CPU of the GPU box"}
         out = {
-            "metric": "fused frames/sec @640x480, 5 mm voxel hash; ICP+integrate ms/frame",
+            "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame",
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -216,10 +232,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"C2 orbit, {W}x{H}, {args.voxel * 1000:g} mm voxels, 8^3 blocks, "
+            "config": {"workload": f"{args.config} orbit, {W}x{H}, {args.voxel * 1000:g} mm voxels, 8^3 blocks, "
                                    "3-level ICP (10/5/4) + alloc + integrate + renderImage + expected depths + "
                                    "ICP-map raycast; one independent stream per GPU",
-                       "cols": W, "rows": H, "voxel_m": args.voxel, "parallelism": f"replicas{world}"},
+                       "cols": W, "rows": H, "voxel_m": args.voxel, "parallelism": f"replicas{world}",
+                       "capacity": cfg["capacity"] or "reference defaults"},
             "icp_integrate_ms_per_frame": None if icp_integ is None else round(icp_integ, 4),
             "stage_ms_per_frame": {k: (None if v is None else round(v, 4)) for k, v in per_stage.items()},
             "stage_breakdown": (f"separate replay of the timed region's first {n_breakdown} frames in a fresh context, "

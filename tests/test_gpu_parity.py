@@ -141,15 +141,17 @@ def test_icp_stage(oracle_mod, icp_schedule):
     assert_bit_exact("icp affine", aff.reshape(12), affine)
 
 
-@pytest.fixture(params=["persistent", "per_iteration"])
+@pytest.fixture(params=["persistent", "persistent_allgather", "per_iteration"])
 def icp_schedule(request, monkeypatch):
-    """Run a test under both ICP schedules (tf_create reads TFUSION_ICP_PERSISTENT)."""
-    monkeypatch.setenv("TFUSION_ICP_PERSISTENT", "1" if request.param == "persistent" else "0")
+    """Run a test under every ICP schedule (tf_create reads TFUSION_ICP_PERSISTENT and
+    TFUSION_ICP_ALLGATHER)."""
+    monkeypatch.setenv("TFUSION_ICP_PERSISTENT", "0" if request.param == "per_iteration" else "1")
+    monkeypatch.setenv("TFUSION_ICP_ALLGATHER", "1" if request.param == "persistent_allgather" else "0")
     return request.param
 
 
 def _check_schedule(g, sched):
-    assert g.icp_persistent() == (sched == "persistent")
+    assert g.icp_persistent() == (sched != "per_iteration")
 
 
 def _cosf(x):
@@ -185,6 +187,24 @@ def test_sequence(oracle_mod, cols, rows, nframes, icp_schedule):
         op, on = o.prev_maps(l)
         assert_bit_exact(f"final prev points L{l}", gp, op)
         assert_bit_exact(f"final prev normals L{l}", gn, on)
+
+
+def test_sequence_c3_geometry(oracle_mod):
+    """C3 geometry: 1280x960, 2 mm voxels, capacities past the reference's; the
+    persistent ICP re-reads the current maps of the CTA slots beyond its register-resident ones."""
+    cols, rows = 1280, 960
+    g, o = make_pair(oracle_mod, cols, rows, voxelSize=0.002, n_blocks=1 << 17)
+    seq = synth.orbit_sequence(3, cols, rows, seed=7)
+    for k in range(3):
+        okg, oko = g(seq[k]), o(seq[k])
+        assert okg == oko, f"frame {k}: ok gpu {okg} oracle {oko}"
+        sg, so = g.last_stats, o.counters()
+        for key in ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries", "icp_iterations"):
+            assert sg[key] == so[key], f"frame {k} {key}: gpu {sg[key]} oracle {so[key]}"
+        assert_bit_exact(f"frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
+    assert o.params.n_blocks - 1 - o.counters()["lastFreeBlockId"] > 20000      # a C3-sized scene
+    compare_scene(g, o, "C3 final")
+    assert_bit_exact("C3 final raycast", g.raycast_result(), o.raycast_result())
 
 
 def test_icp_failure_reset(oracle_mod, icp_schedule):

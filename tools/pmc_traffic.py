@@ -3,7 +3,9 @@ passes of tools/gpu_pmc.sh, corrected as MI355X_MICROARCH.md §HBM prescribes (g
 FETCH_SIZE reports half the bytes of wide reads: x2; WRITE_SIZE as is; both in KiB).
 Writes profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
 
-    python tools/pmc_traffic.py gpurun_out/pmc_TAG [profiles/pmc_traffic.json]"""
+    python tools/pmc_traffic.py gpurun_out/pmc_TAG [CONFIG=C2] [profiles/pmc_traffic.json]
+
+The output holds one entry per bench config (C2, C3); an existing file is updated in place."""
 import csv, glob, json, os, sys
 from collections import defaultdict
 
@@ -22,7 +24,8 @@ def per_kernel(root, counter):
 
 def main():
     root = sys.argv[1]
-    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+    config = sys.argv[2] if len(sys.argv) > 2 else "C2"
+    out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                             "profiles", "pmc_traffic.json")
     fetch, write = per_kernel(root, "FETCH_SIZE"), per_kernel(root, "WRITE_SIZE")
     res = {}
@@ -37,7 +40,13 @@ def main():
                       "bytes_per_launch": round(fb + wb), "launches_sampled": len(f),
                       "source": os.path.basename(os.path.normpath(root)),
                       "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads), WRITE_SIZE x1, KiB->B"}
-    json.dump(res, open(out, "w"), indent=1)
+    allcfg = {}
+    if os.path.exists(out):
+        allcfg = json.load(open(out))
+        if allcfg and "C2" not in allcfg and "C3" not in allcfg:     # old flat layout
+            allcfg = {}
+    allcfg[config] = res
+    json.dump(allcfg, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 

@@ -204,7 +204,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->frame_mode, sizeof(int) * TF_PROF_RING);
     ALLOC(c->icp_partial, sizeof(float) * 28 * 256);
     ALLOC(c->icp_ticket, 64);
-    ALLOC(c->icp_tagged, sizeof(unsigned long long) * (256 * 28 + 16));
+    ALLOC(c->icp_tagged, sizeof(unsigned long long) * (2 * 256 * 28 + 16));
     ALLOC(c->st, sizeof(TfDevState));
 #undef ALLOC
     e = hipHostMalloc((void**)&c->st_host, sizeof(TfDevState), hipHostMallocDefault);
@@ -217,7 +217,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     e = hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_ticket, 0, 64, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->bgrid, 0xff, sizeof(int2) * (size_t)TF_GRID_DIM * TF_GRID_DIM * TF_GRID_DIM, c->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(c->icp_tagged, 0, sizeof(unsigned long long) * (256 * 28 + 16), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->icp_tagged, 0, sizeof(unsigned long long) * (2 * 256 * 28 + 16), c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->allocType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->winnerKey, 0xff, sizeof(int) * ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->visType, 0, ntot_pad, c->stream);
@@ -246,6 +246,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     {   // ICP schedule: one persistent launch per frame when all its workgroups fit at once
         const char* env = getenv("TFUSION_ICP_PERSISTENT");
         c->icp_persistent = (env && env[0] == '0') ? 0 : tfk_icp_persistent_ok(c);
+        const char* ag = getenv("TFUSION_ICP_ALLGATHER");
+        c->icp_allgather = (ag && ag[0] == '1') ? 1 : 0;
     }
     *out = c;
     return TF_OK;

@@ -448,7 +448,7 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 #define IP_WAVES 8
 #define IP_SREG 1                       // CTA slots kept in registers per wave (8 per WG; larger images use k_icp_iter)
 #define IP_SPIN_LIMIT (1u << 21)
-#define IP_BCAST (ICP_NWG * ICP_T_STRIDE)
+#define IP_BCAST (2 * ICP_NWG * ICP_T_STRIDE)   // column slots are double-buffered by generation parity
 #define IP_LDS_PAD (56 * 1024)
 
 struct IcpFrameArgs {
@@ -576,10 +576,14 @@ __device__ __forceinline__ void ip_unpack(const float (&sm)[27], float (&Am)[6][
         }
 }
 
+// ALLGATHER = false: workgroup 0 gathers, solves and broadcasts the new affine (two hops per
+// iteration).  ALLGATHER = true: every workgroup gathers the 256 column sums and runs the
+// (deterministic, bit-identical) tail itself -- one hop per iteration, no broadcast.
+template <bool ALLGATHER>
 __global__ void __launch_bounds__(64 * IP_WAVES)
 k_icp_frame(IcpFrameArgs a)
 {
-    __shared__ float red[IP_WAVES * IP_SREG][ICP_T_STRIDE];
+    __shared__ float red[ICP_MAX_SLOTS][ICP_T_STRIDE];
     __shared__ float tv[27][ICP_NWG];
     __shared__ float aff_s[12];
     __shared__ int status_s, det_ok_s;
@@ -637,6 +641,29 @@ k_icp_frame(IcpFrameArgs a)
                     if (!(lane & 1) && (lane >> 1) < 27) red[sl][lane >> 1] = tot;
                 }
             }
+            // slots beyond the register-resident ones (large images): current maps re-read
+#pragma unroll 1
+            for (int sl = wave + IP_WAVES * IP_SREG; sl < slots; sl += IP_WAVES) {
+                const int cta = wg + ICP_NWG * sl;
+                if (cta >= L.nct) break;
+                IpPix q[4];
+                int qxy[4];
+                const int bx = cta % L.gx, by = cta / L.gx;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int t = lane + 64 * j;
+                    const int x = bx * 32 + (t & 31), y = by * 8 + (t >> 5);
+                    const bool in = x < L.W && y < L.H;
+                    qxy[j] = in ? 1 : -1;
+                    const float4 v = in ? L.vcurr[y * L.W + x] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float4 n = in ? L.ncurr[y * L.W + x] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    q[j].vx = v.x; q[j].vy = v.y; q[j].vz = v.z; q[j].nx = n.x; q[j].ny = n.y; q[j].nz = n.z;
+                }
+                float r[4][7];
+                ip_rows4(L, aff, q, qxy, r);
+                const float tot = ip_cta_reduce(r, lane);
+                if (!(lane & 1) && (lane >> 1) < 27) red[sl][lane >> 1] = tot;
+            }
             __syncthreads();
             if (tid < 27) {
                 float sum = 0.f;                                   // 0 + P[w] + P[w+256] + ...
@@ -644,10 +671,10 @@ k_icp_frame(IcpFrameArgs a)
                     if (wg + ICP_NWG * sl >= L.nct) break;
                     sum += red[sl][tid];
                 }
-                ip_store(&tag[wg * ICP_T_STRIDE + tid], ip_pack(gen, sum));
+                ip_store(&tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE + wg * ICP_T_STRIDE + tid], ip_pack(gen, sum));
             }
             IPT_REC(done, ICP_NWG + wg);
-            if (wg == 0) {
+            if (ALLGATHER || wg == 0) {
                 // ---- gather the 256 column sums (tagged polling; all loads in flight at once)
                 constexpr int PER = (ICP_NWG * 27 + 64 * IP_WAVES - 1) / (64 * IP_WAVES);
                 unsigned long long v[PER];
@@ -655,7 +682,7 @@ k_icp_frame(IcpFrameArgs a)
                 for (int k = 0; k < PER; ++k) {
                     const int e = tid + 64 * IP_WAVES * k;
                     const int col = e / 27, q = e - col * 27;
-                    v[k] = e < ICP_NWG * 27 ? ip_load(&tag[col * ICP_T_STRIDE + q]) : ((unsigned long long)gen << 32);
+                    v[k] = e < ICP_NWG * 27 ? ip_load(&tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE + col * ICP_T_STRIDE + q]) : ((unsigned long long)gen << 32);
                 }
                 bool timeout = false;
                 for (unsigned spins = 0;; ++spins) {
@@ -666,7 +693,7 @@ k_icp_frame(IcpFrameArgs a)
                             ready = false;
                             const int e = tid + 64 * IP_WAVES * k;
                             const int col = e / 27, q = e - col * 27;
-                            v[k] = ip_load(&tag[col * ICP_T_STRIDE + q]);
+                            v[k] = ip_load(&tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE + col * ICP_T_STRIDE + q]);
                         }
                     }
                     if (ready) break;
@@ -718,7 +745,7 @@ k_icp_frame(IcpFrameArgs a)
                 }
                 IPT_REC(done, 2 * ICP_NWG + 1);
                 status = any_timeout ? 2 : (det_ok_s ? 1 : 0);
-                if (wave == 0 && lane <= 12) {                          // broadcast affine + status
+                if (!ALLGATHER && wave == 0 && lane <= 12) {            // broadcast affine + status
                     const float v = lane < 12 ? aff_s[lane] : (float)status;
                     ip_store(&tag[IP_BCAST + lane], ip_pack(gen, v));
                 }
@@ -844,13 +871,13 @@ static int icp_used_levels(const tf_params& p)
 int tfk_icp_persistent_ok(tf_ctx* c)
 {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame, 64 * IP_WAVES, IP_LDS_PAD) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame<false>, 64 * IP_WAVES, IP_LDS_PAD) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) return 0;
     if (per_cu * cus < ICP_NWG) return 0;
     for (int l = 0; l < TF_LEVELS; ++l) {
         IcpLevel L;
         icp_level(c, l, L);
-        if ((L.nct + ICP_NWG - 1) / ICP_NWG > IP_WAVES * IP_SREG) return 0;
+        if ((L.nct + ICP_NWG - 1) / ICP_NWG > ICP_MAX_SLOTS) return 0;
     }
     return 1;
 }
@@ -876,7 +903,10 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update)
         a.tag = c->icp_tagged;
         // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
         // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up
-        hipLaunchKernelGGL(k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
+        if (c->icp_allgather)
+            hipLaunchKernelGGL(k_icp_frame<true>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
+        else
+            hipLaunchKernelGGL(k_icp_frame<false>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, c->stream, c->st);

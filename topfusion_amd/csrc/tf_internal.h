@@ -212,6 +212,7 @@ struct tf_ctx {
     unsigned* icp_ticket;    // last-workgroup ticket (zero between launches)
     unsigned long long* icp_tagged;   // persistent ICP: [256][28] tagged column sums + [16] broadcast
     int icp_persistent;      // 1: one launch per frame (k_icp_frame), 0: one launch per iteration
+    int icp_allgather;       // persistent ICP: every workgroup gathers + solves (no broadcast hop)
     int icp_max_cta;
     float min_cosine, dist2_thres;
     // device state
