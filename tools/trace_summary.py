@@ -1,5 +1,12 @@
+"""Per-kernel summary of a rocprofv3 --kernel-trace CSV (the committed profiles/rNN_kernel_trace_summary.txt).
+
+The device-driven frame loop enqueues every stage of every frame; on frames where the device
+decided a stage does not run (frame-0 path after a reset, ICP failure) the launch exits at
+once (~1.5 us).  `avg_exec` averages only the launches that did work (> EARLY_US), which is
+what bench.py's HIP events report ("averages per executed launch")."""
 import csv, sys
 from collections import defaultdict
+EARLY_US = 3.0
 path = sys.argv[1]
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -9,7 +16,10 @@ for r in rows:
     by[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000)
 tot = sum(sum(v) for v in by.values())
 for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
-    print(f"{k[0]:24s} grid={k[1]:>8} n={len(v):5d} avg={sum(v)/len(v):8.2f}us min={min(v):8.2f} tot%={100*sum(v)/tot:5.1f}")
+    ex = [x for x in v if x > EARLY_US]
+    avg_ex = sum(ex) / len(ex) if ex else 0.0
+    print(f"{k[0]:24s} grid={k[1]:>8} n={len(v):5d} avg={sum(v)/len(v):8.2f}us n_exec={len(ex):5d} "
+          f"avg_exec={avg_ex:8.2f}us min={min(v):8.2f} tot%={100*sum(v)/tot:5.1f}")
 gaps = defaultdict(list)
 for a, b in zip(rows, rows[1:]):
     gaps[a["Kernel_Name"].split("(")[0] + "->" + b["Kernel_Name"].split("(")[0]].append((int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1000)
