@@ -34,3 +34,28 @@ def hash_block_set(h):
     """Allocated blocks as a sorted set of positions (order-free view of the hash table)."""
     alloc = h[h["ptr"] >= 0]
     return sorted(zip(alloc["x"].tolist(), alloc["y"].tolist(), alloc["z"].tolist()))
+
+
+class DeviceFrames:
+    """Device copy of a host array through the HIP runtime libtfusion_hip.so itself links
+    (no torch: torch ships its own HIP runtime, and two runtimes in one process do not share
+    a device context in every initialisation order)."""
+
+    def __init__(self, arr):
+        import ctypes
+        from topfusion_amd import _lib
+        _lib.load()                                   # the product library (and its libamdhip64)
+        self._hip = ctypes.CDLL("libamdhip64.so.7")
+        a = np.ascontiguousarray(arr)
+        self.nbytes = a.nbytes
+        p = ctypes.c_void_p()
+        assert self._hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(a.nbytes)) == 0, "hipMalloc"
+        self.ptr = p.value
+        assert self._hip.hipMemcpy(ctypes.c_void_p(self.ptr), a.ctypes.data_as(ctypes.c_void_p),
+                                   ctypes.c_size_t(a.nbytes), 1) == 0, "hipMemcpy H2D"   # hipMemcpyHostToDevice
+
+    def free(self):
+        import ctypes
+        if self.ptr:
+            self._hip.hipFree(ctypes.c_void_p(self.ptr))
+            self.ptr = None

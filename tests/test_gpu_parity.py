@@ -244,3 +244,35 @@ def test_capacity_exhaustion(oracle_mod):
         assert sg["lastFreeBlockId"] == so["lastFreeBlockId"]
         assert sg["lastFreeExcessListId"] == so["lastFreeExcessListId"]
     compare_scene(g, o, "exhausted")
+
+
+@pytest.mark.parametrize("render_late", ["0", "1"])
+def test_batched_frames_overlap(oracle_mod, monkeypatch, render_late):
+    """The device-driven batch path (tf_process_frames): frames enqueued back to back with no
+    host sync, renderImage on the render stream overlapping the frame's tail and the next
+    frame's ICP (TFUSION_RENDER_LATE selects which).  Per-frame results, the last frame's grey
+    image, the final pose and the whole scene match the oracle run frame by frame."""
+    from parity_util import DeviceFrames
+    from topfusion_amd import TopFu, default_params
+    monkeypatch.setenv("TFUSION_RENDER_LATE", render_late)
+    cols, rows, n = 320, 240, 40          # 40 frames > one 32-frame enqueue group
+    fx, fy, cx, cy = synth.intrinsics(cols, rows)
+    args = dict(cols=cols, rows=rows, fx=fx, fy=fy, cx=cx, cy=cy)
+    g = TopFu(default_params(**args))
+    o = oracle_mod.Oracle(oracle_mod.default_params(**args))
+    seq = synth.orbit_sequence(n, cols, rows, seed=7)
+    dev = DeviceFrames(seq)
+    okg = g.process_frames(dev.ptr, n)
+    oko = np.array([o(seq[k]) for k in range(n)])
+    assert np.array_equal(okg, oko), (okg, oko)
+    assert (~oko).sum() >= 1, "sequence should include an ICP-failure reset"
+    sg, so = g.stats(), o.counters()
+    for key in ("frame_counter", "n_resets", "icp_iterations"):
+        assert sg[key] == so[key], f"{key}: gpu {sg[key]} oracle {so[key]}"
+    assert_bit_exact("batched final pose", g.getCameraPose()[:3, :4], o.pose())
+    if oko[-1]:
+        assert_bit_exact("batched last renderImage grey", g.frame_grey(), o.frame_grey())
+    compare_scene(g, o, "batched")
+    assert_bit_exact("batched final raycast", g.raycast_result(), o.raycast_result())
+    g.close()
+    dev.free()

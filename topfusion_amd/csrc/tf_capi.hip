@@ -90,8 +90,8 @@ static void ctx_free(tf_ctx* c)
 {
     if (!c) return;
     void* bufs[] = { c->hash, c->excessList, c->vba, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
-                     c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->raycast, c->grey,
-                     c->blockBox, c->blockZ, c->blockTiles, c->blockKeep, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
+                     c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
+                     c->blockBox, c->blockZ, c->blockTiles, c->blockOff, c->edChunk, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->frame_ok, c->frame_mode };
     for (void* b : bufs) if (b) (void)hipFree(b);
     // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
@@ -100,6 +100,9 @@ static void ctx_free(tf_ctx* c)
     for (int l = 0; l < TF_LEVELS; ++l) if (c->depth_pyr[l]) (void)hipFree(c->depth_pyr[l]);
     if (c->st_host) (void)hipHostFree(c->st_host);
     for (int i = 0; i < 2 * TF_NUM_STAGES * TF_PROF_RING; ++i) if (c->prof_ev[i]) (void)hipEventDestroy(c->prof_ev[i]);
+    if (c->ev_integrated) (void)hipEventDestroy(c->ev_integrated);
+    if (c->ev_rendered) (void)hipEventDestroy(c->ev_rendered);
+    if (c->rstream) (void)hipStreamDestroy(c->rstream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -110,8 +113,16 @@ static hipError_t dalloc(T** p, size_t bytes)
     return hipMalloc((void**)p, bytes < 16 ? 16 : bytes);
 }
 
+// the main stream waits for the last enqueued renderImage (render stream): every entry point
+// that reads or writes what a render may still be reading or writing joins it first
+static hipError_t join_render(tf_ctx* c)
+{
+    return hipStreamWaitEvent(c->stream, c->ev_rendered, 0);
+}
+
 static tf_status sync_state(tf_ctx* c)
 {
+    TF_CHECK(join_render(c));
     TF_CHECK(hipMemcpyAsync(c->st_host, c->st, sizeof(TfDevState), hipMemcpyDeviceToHost, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
@@ -128,6 +139,7 @@ __global__ void k_host_reset(TfDevState* st)
 
 static tf_status ctx_reset(tf_ctx* c)
 {
+    TF_CHECK(join_render(c));
     hipLaunchKernelGGL(k_host_reset, dim3(1), dim3(1), 0, c->stream, c->st);
     TF_CHECK(hipGetLastError());
     TF_CHECK(tfk_reset_scene(c));
@@ -164,6 +176,10 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     c->dist2_thres = pin->icp_dist_thres * pin->icp_dist_thres;
 #define ALLOC(ptr, bytes) do { e = dalloc(&(ptr), (bytes)); if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); } } while (0)
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_integrated, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_rendered, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(c->ev_rendered, c->rstream);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     ALLOC(c->hash, sizeof(TfHashEntry) * (size_t)c->n_total);
     ALLOC(c->excessList, sizeof(int) * (size_t)pin->n_excess);
@@ -178,12 +194,14 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->visibleIds, sizeof(int) * (size_t)pin->vis_capacity);
     ALLOC(c->visType, ntot_pad);
     ALLOC(c->range, sizeof(float) * 2 * npx);
+    ALLOC(c->range_render, sizeof(float) * 2 * npx);
     ALLOC(c->raycast, sizeof(float) * 4 * npx);
     ALLOC(c->grey, sizeof(uchar4) * npx);
     ALLOC(c->blockBox, sizeof(int4) * (size_t)pin->vis_capacity);
     ALLOC(c->blockZ, sizeof(float2) * (size_t)pin->vis_capacity);
     ALLOC(c->blockTiles, sizeof(int) * (size_t)pin->vis_capacity);
-    ALLOC(c->blockKeep, (size_t)pin->vis_capacity);
+    ALLOC(c->blockOff, sizeof(int) * (size_t)pin->vis_capacity);
+    ALLOC(c->edChunk, sizeof(int) * ((size_t)pin->vis_capacity / 256 + 1));
     ALLOC(c->depth_in, sizeof(uint16_t) * npx);
     ALLOC(c->dists, sizeof(float) * npx);
     {   // each map's three pyramid levels are contiguous in one allocation
@@ -248,6 +266,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         c->icp_persistent = (env && env[0] == '0') ? 0 : tfk_icp_persistent_ok(c);
         const char* ag = getenv("TFUSION_ICP_ALLGATHER");
         c->icp_allgather = (ag && ag[0] == '1') ? 1 : 0;
+        const char* rl = getenv("TFUSION_RENDER_LATE");
+        c->render_late = (rl && rl[0] == '1') ? 1 : 0;
     }
     *out = c;
     return TF_OK;
@@ -256,6 +276,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
 extern "C" void tf_destroy(tf_ctx* c)
 {
     if (!c) return;
+    (void)hipStreamSynchronize(c->rstream);
     (void)hipStreamSynchronize(c->stream);
     ctx_free(c);
 }
@@ -275,6 +296,8 @@ __global__ void k_stage_begin(TfDevState* st)
 
 static hipError_t clear_abort(tf_ctx* c)
 {
+    hipError_t e = join_render(c);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_stage_begin, dim3(1), dim3(1), 0, c->stream, c->st);
     return hipGetLastError();
 }
@@ -290,13 +313,14 @@ static void swap_pyramids(tf_ctx* c)
 // ---- per-stage event timing -----------------------------------------------------------
 // Events ring: TF_PROF_RING frames x (start, end) per stage.  Frames are attributed after a
 // sync, once their mode / ok flags are known, and only for the stages that did work.
-#define STAGE(id, expr)                                                                       \
+#define STAGE_ON(strm, id, expr)                                                              \
     do {                                                                                      \
         const bool timed_ = c->prof_enabled && ((c->prof_mask >> (id)) & 1u);                 \
-        if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id)), c->stream));       \
+        if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id)), (strm)));          \
         TF_CHECK(expr);                                                                       \
-        if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id) + 1), c->stream));   \
+        if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id) + 1), (strm)));      \
     } while (0)
+#define STAGE(id, expr) STAGE_ON(c->stream, id, expr)
 
 static hipEvent_t prof_event(tf_ctx* c, int slot, int k)
 {
@@ -337,12 +361,29 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
 {
     STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, 1));  // topfu.cpp:166-197 (+ frame begin)
     STAGE(TF_STAGE_ICP, tfk_icp(c, 1));                              // topfu.cpp:242-243 (tracking only)
+    // the previous frame's renderImage (render stream) must be done before the scene changes
+    TF_CHECK(join_render(c));
+    TF_CHECK(tfk_render_prologue(c));
     STAGE(TF_STAGE_ALLOC, tfk_alloc(c));                             // topfu.cpp:202 / 281
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1));                  // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
-    STAGE(TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c));            // renderImage (raycast + grey), topfu.cpp:284-285
+    // renderImage (raycast + grey, topfu.cpp:284-285) on the render stream, behind integration;
+    // it overlaps CreateExpectedDepths / CreateICPMaps and the next frame's preprocessing + ICP,
+    // none of which writes what it reads (the scene, the range snapshot, M_render)
+    if (!c->render_late) {
+        TF_CHECK(hipEventRecord(c->ev_integrated, c->stream));
+        TF_CHECK(hipStreamWaitEvent(c->rstream, c->ev_integrated, 0));
+        STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c));
+        TF_CHECK(hipEventRecord(c->ev_rendered, c->rstream));
+    }
     STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c));         // topfu.cpp:306
     STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));                  // CreateICPMaps, topfu.cpp:307
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps(c));                       // + resizePointsNormals :308-309
+    if (c->render_late) {   // render behind the frame's tail: it overlaps the next frame's ICP
+        TF_CHECK(hipEventRecord(c->ev_integrated, c->stream));
+        TF_CHECK(hipStreamWaitEvent(c->rstream, c->ev_integrated, 0));
+        STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c));
+        TF_CHECK(hipEventRecord(c->ev_rendered, c->rstream));
+    }
     TF_CHECK(tfk_reset_scene_on_failure(c, slot));                   // frame end; topfu.cpp:263-264
     return TF_OK;
 }
@@ -623,6 +664,7 @@ extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
 extern "C" tf_status tf_stage_reset_scene(tf_ctx* c)
 {
     if (!c) return TF_INVALID_ARG;
+    TF_CHECK(join_render(c));
     TF_CHECK(tfk_reset_scene(c));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
@@ -669,6 +711,7 @@ extern "C" tf_status tf_buffer_bytes(tf_ctx* c, int which, int level, size_t* by
 extern "C" tf_status tf_download(tf_ctx* c, int which, int level, void* host, size_t bytes)
 {
     if (!c || !host) return TF_INVALID_ARG;
+    TF_CHECK(join_render(c));
     size_t n;
     void* p = buffer_ptr(c, which, level, &n);
     if (!p || n != bytes) return TF_INVALID_ARG;
@@ -680,6 +723,7 @@ extern "C" tf_status tf_download(tf_ctx* c, int which, int level, void* host, si
 extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host, size_t bytes)
 {
     if (!c || !host) return TF_INVALID_ARG;
+    TF_CHECK(join_render(c));
     size_t n;
     void* p = buffer_ptr(c, which, level, &n);
     if (!p || n != bytes) return TF_INVALID_ARG;
@@ -692,6 +736,7 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
 extern "C" tf_status tf_set_pose(tf_ctx* c, const float rt[12])
 {
     if (!c || !rt) return TF_INVALID_ARG;
+    TF_CHECK(join_render(c));
     TF_CHECK(hipMemcpyAsync(c->st->pose, rt, sizeof(float) * 12, hipMemcpyHostToDevice, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;

@@ -52,7 +52,7 @@ struct TfDevState {
     int noVisibleEntries;
     int noTotalBlocks;
     int alloc_exhausted;     // capacity exhausted this frame -> serial allocation
-    unsigned tiles_total;    // rendering tiles requested (before the MAX cap)
+    unsigned pad_tiles_;
     int pad_[2];             // alloc totals (tf_scene.hip)
     unsigned icp_gen;        // last generation tag used by the persistent ICP kernel
     // device-driven frame control (TopFu::operator() branches decided on the device, so a
@@ -60,9 +60,13 @@ struct TfDevState {
     int mode;                // this frame: 0 = frame-0 path (integrate only), 1 = tracking path
     int frame_counter;       // TopFu::frame_counter_
     int n_resets;            // resets taken after ICP failures
-    unsigned ed_ticket;      // CreateExpectedDepths: last-workgroup ticket (zero between launches)
-    int ed_capped;           // tiles exceeded MAX_RENDERING_BLOCKS this frame
-    int pad2_[3];
+    int pad2_[5];
+    // renderImage of the frame runs on the context's render stream, overlapping the rest of
+    // the frame and the next frame's preprocessing/ICP; it reads only this snapshot (taken on
+    // the main stream once the previous render has finished: k_render_prologue)
+    float M_render[16];      // M_ray of the frame being rendered
+    int render_go;           // the frame took the tracking path (mode 1, ICP ok)
+    int pad3_[3];
 };
 
 // ---------------------------------------------------------------------------------------
@@ -173,6 +177,9 @@ struct tf_ctx {
     tf_params p;
     int device;
     hipStream_t stream;
+    hipStream_t rstream;     // renderImage stream (tf_capi.hip: enqueue_frame)
+    hipEvent_t ev_integrated, ev_rendered;
+    int render_late;         // 1: renderImage enqueued behind the frame's tail (overlaps the next ICP)
     int n_total;
     int W, H;
     int lw[TF_LEVELS], lh[TF_LEVELS];
@@ -192,13 +199,15 @@ struct tf_ctx {
     int* visibleIds;
     unsigned char* visType;
     float* range;            // float2
+    float* range_render;     // float2: snapshot of range's ÷8 region for the frame's renderImage
     float* raycast;          // float4
     uchar4* grey;
     // expected-depths scratch
     int4* blockBox;          // per visible entry: ulx, uly, lrx, lry (ulx < 0 -> invalid)
     float2* blockZ;
     int* blockTiles;
-    unsigned char* blockKeep;
+    int* blockOff;           // exclusive tile offset inside the entry's 256-entry chunk
+    int* edChunk;            // tile total per chunk
     // frame buffers
     uint16_t* depth_in;      // staging for host uploads / pitched input
     float* dists;
@@ -246,7 +255,8 @@ hipError_t tfk_alloc(tf_ctx* c);
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_grey(tf_ctx* c);
-hipError_t tfk_raycast_grey(tf_ctx* c);    // renderImage raycast + grey, fused (frame path)
+hipError_t tfk_raycast_grey(tf_ctx* c);    // renderImage raycast + grey, fused (frame path, render stream)
+hipError_t tfk_render_prologue(tf_ctx* c); // snapshot for the frame's renderImage (main stream)
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_expected_depths(tf_ctx* c);
 hipError_t tfk_frame0_matrices(tf_ctx* c);

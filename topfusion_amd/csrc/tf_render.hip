@@ -312,17 +312,19 @@ template <int MODE>
 __global__ void __launch_bounds__(256)
 k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles)
 {
-    if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
+    // the frame's renderImage (MODE 2, render stream) reads the snapshot k_render_prologue took
+    if (MODE == 2 ? !st->render_go : (st->abort || st->mode == 0)) return;   // ICP failed, or frame 0
     const int tile = xcd_tile(blockIdx.x, n_tiles);     // grid padded to a multiple of 8
     if (tile < 0) return;
     const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15), y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.H) return;
+    const float* M = MODE == 2 ? st->M_render : st->M_ray;
     float pt[3];
-    const float w = ray_march<MODE == 1>(a, st->M_ray, x, y, pt);
+    const float w = ray_march<MODE == 1>(a, M, x, y, pt);
     if (MODE == 2) {
         // renderImage: lightSource = -Vector3f(pose.getColumn(2)) (VisualisationEngine_CUDA.cu:243)
         unsigned char v = 0;
-        if (w > 0) v = grey_pixel(a.s, pt, -st->M_ray[8], -st->M_ray[9], -st->M_ray[10]);
+        if (w > 0) v = grey_pixel(a.s, pt, -M[8], -M[9], -M[10]);
         a.grey[x + y * a.W] = make_uchar4(v, v, v, v);
     } else {
         a.out[x + y * a.W] = make_float4(pt[0], pt[1], pt[2], w);
@@ -346,7 +348,7 @@ static hipError_t launch_ray(tf_ctx* c, const RayArgs& a, int mode)
     const dim3 grid((n + 7) / 8 * 8);
     if (mode == 0) hipLaunchKernelGGL(k_raycast<0>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
     else if (mode == 1) hipLaunchKernelGGL(k_raycast<1>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
-    else hipLaunchKernelGGL(k_raycast<2>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
+    else hipLaunchKernelGGL(k_raycast<2>, grid, dim3(256), 0, c->rstream, a, c->st, tx, n);
     return hipGetLastError();
 }
 
@@ -359,13 +361,40 @@ hipError_t tfk_raycast(tf_ctx* c, int update_visible)
 }
 
 // renderImage in the frame path: castRay<false> + renderGrey fused (the intermediate point
-// image is overwritten by CreateICPMaps before anything can observe it)
+// image is overwritten by CreateICPMaps before anything can observe it).  It is enqueued on
+// the render stream behind the frame's integration and reads the range-image snapshot.
 hipError_t tfk_raycast_grey(tf_ctx* c)
 {
     RayArgs a;
     ray_args(c, a);
+    a.range = (const float2*)c->range_render;
     a.grey = c->grey;
     return launch_ray(c, a, 2);
+}
+
+// Main stream, after the previous frame's renderImage has finished and this frame's ICP has
+// set the pose: snapshot what renderImage reads and later stages of this frame or the next
+// overwrite -- the raycast matrix, the go flag, and the ÷8 region castRay reads of the range
+// image (range[x/8 + (y/8)*W], VisualisationEngine_Shared.hpp:104-106) that
+// CreateExpectedDepths rewrites before the render may have run.
+__global__ void __launch_bounds__(256)
+k_render_prologue(TfDevState* __restrict__ st, const float2* __restrict__ range, float2* __restrict__ snap, int W, int H)
+{
+    if (threadIdx.x < 16) st->M_render[threadIdx.x] = st->M_ray[threadIdx.x];
+    if (threadIdx.x == 0) st->render_go = (st->mode != 0 && !st->abort) ? 1 : 0;
+    if (st->mode == 0 || st->abort) return;
+    const int rc = (W - 1) / TF_SUBSAMPLE + 1, rr = (H - 1) / TF_SUBSAMPLE + 1;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < rc * rr; i += gridDim.x * 256) {
+        const int y = i / rc, x = i - y * rc;
+        snap[x + y * W] = range[x + y * W];
+    }
+}
+
+hipError_t tfk_render_prologue(tf_ctx* c)
+{
+    hipLaunchKernelGGL(k_render_prologue, dim3(8), dim3(256), 0, c->stream, c->st, (const float2*)c->range,
+                       (float2*)c->range_render, c->W, c->H);
+    return hipGetLastError();
 }
 
 
@@ -510,104 +539,131 @@ struct EdArgs {
     const TfHashEntry* hash;
     const int* visibleIds;
     float2* range;
-    int4* box; float2* z; int* tiles; unsigned char* keep;
+    int4* box; float2* z; int* tiles; int* off; int* chunk;
     int W, H;
     float fx, fy, cx, cy, voxelSize;
     unsigned cap;
 };
 
-// memsetKernel(FAR_AWAY, VERY_CLOSE) + ProjectSingleBlock (VisualisationEngine_Shared.hpp:33-77)
+#define ED_CHUNK 256     // visible entries per projection chunk (one workgroup pass)
+
+// memsetKernel(FAR_AWAY, VERY_CLOSE) + ProjectSingleBlock (VisualisationEngine_Shared.hpp:33-77).
+// Visible entries are processed in chunks of 256 (thread t of a chunk pass = entry
+// chunk*256 + t).  Each chunk stores its tile total and every entry its exclusive tile offset
+// inside the chunk, so the MAX_RENDERING_BLOCKS cap (VisualisationHelper.cu:70-74) is applied
+// by k_ed_fill from plain prefix sums: no counter atomics, no last-workgroup ticket, no fence.
 __global__ void __launch_bounds__(256)
-k_ed_project(EdArgs a, TfDevState* __restrict__ st)
+k_ed_project(EdArgs a, const TfDevState* __restrict__ st)
 {
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int tid = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
-    const int npx = a.W * a.H;
-    for (int i = tid; i < npx; i += stride) a.range[i] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
+    {   // range image init, two pixels per 16-byte store
+        const int npx = a.W * a.H;
+        float4* r4 = (float4*)a.range;
+        for (int i = tid; i < (npx >> 1); i += stride) r4[i] = make_float4(TF_FAR_AWAY, TF_VERY_CLOSE, TF_FAR_AWAY, TF_VERY_CLOSE);
+        if ((npx & 1) && tid == 0) a.range[npx - 1] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
+    }
+    __shared__ int wsum[4];
     const int n = st->noVisibleEntries;
+    const int nchunks = (n + ED_CHUNK - 1) / ED_CHUNK;
     const float* M = st->M_alloc;          // pose.inv() (topfu.cpp:306)
-    for (int i = tid; i < n; i += stride) {
-        TfHashEntry e = a.hash[a.visibleIds[i]];
-        int4 box = make_int4(-1, -1, -1, -1);
-        float2 zr = make_float2(0.f, 0.f);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        const int i = ch * ED_CHUNK + threadIdx.x;
         int ntiles = 0;
-        if (e.ptr >= 0) {
-            int ulx = a.W / TF_SUBSAMPLE, uly = a.H / TF_SUBSAMPLE, lrx = -1, lry = -1;
-            float zmin = TF_FAR_AWAY, zmax = TF_VERY_CLOSE;
-            for (int corner = 0; corner < 8; ++corner) {
-                short tx = (short)(e.x + ((corner & 1) ? 1 : 0));
-                short ty = (short)(e.y + ((corner & 2) ? 1 : 0));
-                short tz = (short)(e.z + ((corner & 4) ? 1 : 0));
-                float q[3];
-                tf_m4v3(M, (float)tx * (float)TF_BLK * a.voxelSize, (float)ty * (float)TF_BLK * a.voxelSize,
-                        (float)tz * (float)TF_BLK * a.voxelSize, 1.0f, q);
-                if ((double)q[2] < 1e-6) continue;
-                float p2x = (a.fx * q[0] / q[2] + a.cx) / (float)TF_SUBSAMPLE;
-                float p2y = (a.fy * q[1] / q[2] + a.cy) / (float)TF_SUBSAMPLE;
-                if ((float)ulx > floorf(p2x)) ulx = (int)floorf(p2x);
-                if ((float)lrx < ceilf(p2x)) lrx = (int)ceilf(p2x);
-                if ((float)uly > floorf(p2y)) uly = (int)floorf(p2y);
-                if ((float)lry < ceilf(p2y)) lry = (int)ceilf(p2y);
-                if (zmin > q[2]) zmin = q[2];
-                if (zmax < q[2]) zmax = q[2];
+        if (i < n) {
+            TfHashEntry e = a.hash[a.visibleIds[i]];
+            int4 box = make_int4(-1, -1, -1, -1);
+            float2 zr = make_float2(0.f, 0.f);
+            if (e.ptr >= 0) {
+                int ulx = a.W / TF_SUBSAMPLE, uly = a.H / TF_SUBSAMPLE, lrx = -1, lry = -1;
+                float zmin = TF_FAR_AWAY, zmax = TF_VERY_CLOSE;
+                for (int corner = 0; corner < 8; ++corner) {
+                    short tx = (short)(e.x + ((corner & 1) ? 1 : 0));
+                    short ty = (short)(e.y + ((corner & 2) ? 1 : 0));
+                    short tz = (short)(e.z + ((corner & 4) ? 1 : 0));
+                    float q[3];
+                    tf_m4v3(M, (float)tx * (float)TF_BLK * a.voxelSize, (float)ty * (float)TF_BLK * a.voxelSize,
+                            (float)tz * (float)TF_BLK * a.voxelSize, 1.0f, q);
+                    if ((double)q[2] < 1e-6) continue;
+                    float p2x = (a.fx * q[0] / q[2] + a.cx) / (float)TF_SUBSAMPLE;
+                    float p2y = (a.fy * q[1] / q[2] + a.cy) / (float)TF_SUBSAMPLE;
+                    if ((float)ulx > floorf(p2x)) ulx = (int)floorf(p2x);
+                    if ((float)lrx < ceilf(p2x)) lrx = (int)ceilf(p2x);
+                    if ((float)uly > floorf(p2y)) uly = (int)floorf(p2y);
+                    if ((float)lry < ceilf(p2y)) lry = (int)ceilf(p2y);
+                    if (zmin > q[2]) zmin = q[2];
+                    if (zmax < q[2]) zmax = q[2];
+                }
+                if (ulx < 0) ulx = 0;
+                if (uly < 0) uly = 0;
+                if (lrx >= a.W) lrx = a.W - 1;
+                if (lry >= a.H) lry = a.H - 1;
+                bool valid = !(ulx > lrx || uly > lry);
+                if (valid && zmin < TF_VERY_CLOSE) zmin = TF_VERY_CLOSE;
+                if (valid && zmax < TF_VERY_CLOSE) valid = false;
+                if (valid) {
+                    int nbx = (int)ceilf((float)(lrx - ulx + 1) / TF_RB_SIZE);
+                    int nby = (int)ceilf((float)(lry - uly + 1) / TF_RB_SIZE);
+                    ntiles = nbx * nby;
+                    box = make_int4(ulx, uly, lrx, lry);
+                    zr = make_float2(zmin, zmax);
+                }
             }
-            if (ulx < 0) ulx = 0;
-            if (uly < 0) uly = 0;
-            if (lrx >= a.W) lrx = a.W - 1;
-            if (lry >= a.H) lry = a.H - 1;
-            bool valid = !(ulx > lrx || uly > lry);
-            if (valid && zmin < TF_VERY_CLOSE) zmin = TF_VERY_CLOSE;
-            if (valid && zmax < TF_VERY_CLOSE) valid = false;
-            if (valid) {
-                int nbx = (int)ceilf((float)(lrx - ulx + 1) / TF_RB_SIZE);
-                int nby = (int)ceilf((float)(lry - uly + 1) / TF_RB_SIZE);
-                ntiles = nbx * nby;
-                box = make_int4(ulx, uly, lrx, lry);
-                zr = make_float2(zmin, zmax);
-            }
+            a.box[i] = box; a.z[i] = zr; a.tiles[i] = ntiles;
         }
-        a.box[i] = box; a.z[i] = zr; a.tiles[i] = ntiles;
-        if (ntiles) atomicAdd(&st->tiles_total, (unsigned)ntiles);
-    }
-    // the last workgroup to finish applies MAX_RENDERING_BLOCKS (VisualisationHelper.cu:70-74):
-    // blocks whose tiles do not fit are dropped in visible-list order (serial; only when the
-    // cap is exceeded), then re-arms the counters for the next frame
-    __shared__ int last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(&st->ed_ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last || threadIdx.x != 0) return;
-    __threadfence();
-    const unsigned total = __hip_atomic_load(&st->tiles_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    st->noTotalBlocks = (int)(total > a.cap ? a.cap : total);
-    st->ed_capped = total > a.cap;
-    if (total > a.cap) {
-        unsigned off = 0;
-        for (int i = 0; i < n; ++i) {
-            unsigned need = (unsigned)a.tiles[i];
-            a.keep[i] = (need && off + need <= a.cap) ? 1 : 0;
-            off += need;
+        // exclusive prefix of the tile counts inside the chunk (wave scan + 4 wave totals)
+        int incl = ntiles;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            int v = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += v;
         }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int base = 0;
+        for (int w = 0; w < wv; ++w) base += wsum[w];
+        if (i < n) a.off[i] = base + incl - ntiles;
+        if (threadIdx.x == 0) a.chunk[ch] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
     }
-    st->tiles_total = 0;
-    st->ed_ticket = 0;
 }
 
 // fillBlocks_device (VisualisationHelper.cu:105-121): per-pixel min/max of the block z-range.
 // One workgroup per block (grid-strided), its threads over the block's pixel box, so a huge
 // box (a block just in front of the camera spans the whole image) costs one workgroup a few
-// thousand no-return atomics instead of one thread ~10^5 serial ones.
+// thousand no-return atomics instead of one thread ~10^5 serial ones.  The tile total is the
+// sum of the chunk totals; past the cap, blocks whose tiles do not fit are dropped in
+// visible-list order (the serial semantics of the reference's atomicAdd offsets).
 __global__ void __launch_bounds__(256)
-k_ed_fill(EdArgs a, const TfDevState* __restrict__ st)
+k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
 {
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int n = st->noVisibleEntries;
-    const bool capped = st->ed_capped;
+    const int nchunks = (n + ED_CHUNK - 1) / ED_CHUNK;
+    __shared__ unsigned red[256];
+    unsigned part = 0;
+    for (int c = threadIdx.x; c < nchunks; c += 256) part += (unsigned)a.chunk[c];
+    red[threadIdx.x] = part;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    const unsigned total = red[0];
+    const bool capped = total > a.cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->noTotalBlocks = (int)(capped ? a.cap : total);
+    unsigned cprefix = 0;                    // tiles of chunks [0, cdone)
+    int cdone = 0;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int4 b = a.box[i];
         if (b.x < 0) continue;
-        if (capped && !a.keep[i]) continue;
+        if (capped) {
+            const int ch = i / ED_CHUNK;     // i grows monotonically: extend the chunk prefix
+            while (cdone < ch) cprefix += (unsigned)a.chunk[cdone++];
+            const unsigned need = (unsigned)a.tiles[i], off = cprefix + (unsigned)a.off[i];
+            if (!(need && off + need <= a.cap)) continue;
+        }
         const float2 zr = a.z[i];
         const int zmin = __float_as_int(zr.x), zmax = __float_as_int(zr.y);   // positive floats order as ints
         const int bw = b.z - b.x + 1, npx = bw * (b.w - b.y + 1);
@@ -624,12 +680,11 @@ hipError_t tfk_expected_depths(tf_ctx* c)
 {
     EdArgs a;
     a.hash = c->hash; a.visibleIds = c->visibleIds; a.range = (float2*)c->range;
-    a.box = c->blockBox; a.z = c->blockZ; a.tiles = c->blockTiles; a.keep = c->blockKeep;
+    a.box = c->blockBox; a.z = c->blockZ; a.tiles = c->blockTiles; a.off = c->blockOff; a.chunk = c->edChunk;
     a.W = c->W; a.H = c->H;
     a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy; a.voxelSize = c->p.voxelSize;
     a.cap = (unsigned)c->p.max_render_blocks;
-    // st->tiles_total / ed_ticket are zero between launches (tf_create, re-armed by k_ed_project)
-    hipLaunchKernelGGL(k_ed_project, dim3(1024), dim3(256), 0, c->stream, a, c->st);
+    hipLaunchKernelGGL(k_ed_project, dim3(256), dim3(256), 0, c->stream, a, c->st);
     hipLaunchKernelGGL(k_ed_fill, dim3(512), dim3(256), 0, c->stream, a, c->st);
     return hipGetLastError();
 }
