@@ -141,12 +141,17 @@ def test_icp_stage(oracle_mod, icp_schedule):
     assert_bit_exact("icp affine", aff.reshape(12), affine)
 
 
-@pytest.fixture(params=["persistent", "persistent_allgather", "per_iteration"])
+ICP_SCHED = {"persistent_hier_allgather": "3", "persistent_hier": "2", "persistent_flat": "0", "persistent_allgather": "1", "per_iteration": "2"}
+
+
+@pytest.fixture(params=list(ICP_SCHED))
 def icp_schedule(request, monkeypatch):
     """Run a test under every ICP schedule (tf_create reads TFUSION_ICP_PERSISTENT and
-    TFUSION_ICP_ALLGATHER)."""
+    TFUSION_ICP_SCHED: 3 hierarchical gather + allgather of the partials (default),
+    2 hierarchical gather + broadcast, 0 flat gather, 1 allgather)."""
     monkeypatch.setenv("TFUSION_ICP_PERSISTENT", "0" if request.param == "per_iteration" else "1")
-    monkeypatch.setenv("TFUSION_ICP_ALLGATHER", "1" if request.param == "persistent_allgather" else "0")
+    monkeypatch.setenv("TFUSION_ICP_SCHED", ICP_SCHED[request.param])
+    monkeypatch.delenv("TFUSION_ICP_ALLGATHER", raising=False)
     return request.param
 
 

@@ -222,7 +222,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->frame_mode, sizeof(int) * TF_PROF_RING);
     ALLOC(c->icp_partial, sizeof(float) * 28 * 256);
     ALLOC(c->icp_ticket, 64);
-    ALLOC(c->icp_tagged, sizeof(unsigned long long) * (2 * 256 * 28 + 16));
+    ALLOC(c->icp_tagged, sizeof(unsigned long long) * TF_ICP_TAG_WORDS);
     ALLOC(c->st, sizeof(TfDevState));
 #undef ALLOC
     e = hipHostMalloc((void**)&c->st_host, sizeof(TfDevState), hipHostMallocDefault);
@@ -235,7 +235,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     e = hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_ticket, 0, 64, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->bgrid, 0xff, sizeof(int2) * (size_t)TF_GRID_DIM * TF_GRID_DIM * TF_GRID_DIM, c->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(c->icp_tagged, 0, sizeof(unsigned long long) * (2 * 256 * 28 + 16), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->icp_tagged, 0, sizeof(unsigned long long) * TF_ICP_TAG_WORDS, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->allocType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->winnerKey, 0xff, sizeof(int) * ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->visType, 0, ntot_pad, c->stream);
@@ -265,7 +265,10 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         const char* env = getenv("TFUSION_ICP_PERSISTENT");
         c->icp_persistent = (env && env[0] == '0') ? 0 : tfk_icp_persistent_ok(c);
         const char* ag = getenv("TFUSION_ICP_ALLGATHER");
-        c->icp_allgather = (ag && ag[0] == '1') ? 1 : 0;
+        const char* sc = getenv("TFUSION_ICP_SCHED");
+        c->icp_sched = 3;
+        if (ag && ag[0] == '1') c->icp_sched = 1;
+        if (sc && sc[0] >= '0' && sc[0] <= '3') c->icp_sched = sc[0] - '0';
         const char* rl = getenv("TFUSION_RENDER_LATE");
         c->render_late = (rl && rl[0] == '1') ? 1 : 0;
     }

@@ -127,14 +127,16 @@ __device__ __forceinline__ void tstep(float* v, int lane)
     }
 }
 
-__constant__ double c_inv_sin[14] = { 0.0, 1.0/6.0, 1.0/20.0, 1.0/42.0, 1.0/72.0, 1.0/110.0, 1.0/156.0,
-    1.0/210.0, 1.0/272.0, 1.0/342.0, 1.0/420.0, 1.0/506.0, 1.0/600.0, 1.0/702.0 };
-__constant__ double c_inv_cos[14] = { 0.0, 1.0/2.0, 1.0/12.0, 1.0/30.0, 1.0/56.0, 1.0/90.0, 1.0/132.0,
-    1.0/182.0, 1.0/240.0, 1.0/306.0, 1.0/380.0, 1.0/462.0, 1.0/552.0, 1.0/650.0 };
-
-// fixed-polynomial sin/cos (replaces std::sin/cos inside cv::Affine3's Rodrigues)
-__device__ void icp_sincos(double th, double* s, double* c)
+// fixed-polynomial sin/cos (replaces std::sin/cos inside cv::Affine3's Rodrigues).  The
+// coefficients are compile-time immediates and the Horner loop is fully unrolled: the serial
+// ICP tail waits on this chain, and a __constant__ table costs one dependent scalar load per
+// term.
+__device__ __forceinline__ void icp_sincos(double th, double* s, double* c)
 {
+    constexpr double inv_sin[14] = { 0.0, 1.0/6.0, 1.0/20.0, 1.0/42.0, 1.0/72.0, 1.0/110.0, 1.0/156.0,
+        1.0/210.0, 1.0/272.0, 1.0/342.0, 1.0/420.0, 1.0/506.0, 1.0/600.0, 1.0/702.0 };
+    constexpr double inv_cos[14] = { 0.0, 1.0/2.0, 1.0/12.0, 1.0/30.0, 1.0/56.0, 1.0/90.0, 1.0/132.0,
+        1.0/182.0, 1.0/240.0, 1.0/306.0, 1.0/380.0, 1.0/462.0, 1.0/552.0, 1.0/650.0 };
     const double PI = 3.14159265358979323846;
     const double TWO_PI = 6.28318530717958647692;
     double r = th;
@@ -144,16 +146,17 @@ __device__ void icp_sincos(double th, double* s, double* c)
     }
     double r2 = r * r;
     double ps = 1.0, pc = 1.0;
+#pragma unroll
     for (int n = 13; n >= 1; --n) {
-        ps = 1.0 - (r2 * c_inv_sin[n]) * ps;
-        pc = 1.0 - (r2 * c_inv_cos[n]) * pc;
+        ps = 1.0 - (r2 * inv_sin[n]) * ps;
+        pc = 1.0 - (r2 * inv_cos[n]) * pc;
     }
     *s = r * ps;
     *c = pc;
 }
 
 // Affine3f(rvec, t) rotation (Rodrigues in double)
-__device__ void icp_rodrigues(const float* rv, float* R)
+__device__ __forceinline__ void icp_rodrigues(const float* rv, float* R)
 {
     double rx = rv[0], ry = rv[1], rz = rv[2];
     double theta = sqrt((rx * rx + ry * ry) + rz * rz);
@@ -273,7 +276,7 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
            int nwg, int slots, int last_iter)
 {
     __shared__ float red[ICP_MAX_SLOTS][ICP_T_STRIDE];
-    __shared__ float tv[27][ICP_NWG];
+    __shared__ float tv[27][ICP_NWG + 1];   // +1: the gather's (col, q) stores hit distinct banks
     __shared__ int is_last;
     if (st->abort || st->mode == 0) return;
     ICP_TS0();
@@ -449,6 +452,8 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 #define IP_SREG 1                       // CTA slots kept in registers per wave (8 per WG; larger images use k_icp_iter)
 #define IP_SPIN_LIMIT (1u << 21)
 #define IP_BCAST (2 * ICP_NWG * ICP_T_STRIDE)   // column slots are double-buffered by generation parity
+#define IP_PART (IP_BCAST + 16)                  // SCHED 2: 8 residue-class partials, double-buffered
+#define IP_NPART 8                               // residue classes of the final tree's first five steps
 #define IP_LDS_PAD (56 * 1024)
 
 struct IcpFrameArgs {
@@ -541,7 +546,7 @@ __device__ __forceinline__ float ip_cta_reduce(const float (&r)[4][7], int lane)
 }
 
 // final 256-wide tree of the column sums in LDS -> the 27 sums in every lane (uniform)
-__device__ __forceinline__ void ip_final_tree(const float (*tv)[ICP_NWG], int lane, float (&sm)[27])
+__device__ __forceinline__ void ip_final_tree(const float (*tv)[ICP_NWG + 1], int lane, float (&sm)[27])
 {
     float v[32];
 #pragma unroll
@@ -576,15 +581,41 @@ __device__ __forceinline__ void ip_unpack(const float (&sm)[27], float (&Am)[6][
         }
 }
 
-// ALLGATHER = false: workgroup 0 gathers, solves and broadcasts the new affine (two hops per
-// iteration).  ALLGATHER = true: every workgroup gathers the 256 column sums and runs the
+// Partial tree of one residue class.  icp_final_reduce_kernel's 256-wide halving tree
+// (temp_utils.hpp:503-523) pairs column t with t+128, t+64, t+32, t+16, t+8 in its first five
+// steps, so after them slot x < 8 holds a sum over the 32 columns x + 8k only, in a fixed
+// pairing: c[k] + c[k+16], then +8, +4, +2, +1 (k = 0..31).  Bit-identical to the full tree.
+__device__ __forceinline__ float ip_residue_tree(const float* c)
+{
+    float b[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) b[k] = c[k] + c[k + 16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b[k] = b[k] + b[k + 8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) b[k] = b[k] + b[k + 4];
+    b[0] = b[0] + b[2];
+    b[1] = b[1] + b[3];
+    return b[0] + b[1];
+}
+
+// SCHED 0: workgroup 0 gathers the 256 column sums, solves and broadcasts the new affine (two
+// hops per iteration).  SCHED 1: every workgroup gathers the 256 column sums and runs the
 // (deterministic, bit-identical) tail itself -- one hop per iteration, no broadcast.
-template <bool ALLGATHER>
+// SCHED 2 (hierarchical): workgroup x < 8 gathers the 32 columns of residue class x (the
+// workgroups dispatched round-robin onto its own XCD), runs the first five tree steps on them
+// (ip_residue_tree) and publishes 27 partials; workgroup 0 gathers the 8 x 27 partials, runs
+// the last three steps and the tail, and broadcasts.  Two small gathers instead of one 55 KB
+// one, and the serial tree in the tail shrinks to 3 steps.  SCHED 3: as 2, but every
+// workgroup gathers the partials and runs the tail itself (no broadcast hop).
+template <int SCHED>
 __global__ void __launch_bounds__(64 * IP_WAVES)
 k_icp_frame(IcpFrameArgs a)
 {
+    constexpr bool ALLGATHER = SCHED == 1;
     __shared__ float red[ICP_MAX_SLOTS][ICP_T_STRIDE];
-    __shared__ float tv[27][ICP_NWG];
+    __shared__ float tl[27][33];                // SCHED 2: a residue class's 32 columns (+1 pad)
+    __shared__ float tv[27][ICP_NWG + 1];   // +1: the gather's (col, q) stores hit distinct banks
     __shared__ float aff_s[12];
     __shared__ int status_s, det_ok_s;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, wg = blockIdx.x;
@@ -674,7 +705,110 @@ k_icp_frame(IcpFrameArgs a)
                 ip_store(&tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE + wg * ICP_T_STRIDE + tid], ip_pack(gen, sum));
             }
             IPT_REC(done, ICP_NWG + wg);
-            if (ALLGATHER || wg == 0) {
+            if (SCHED >= 2 && wg < IP_NPART) {
+                // ---- residue-class leader: gather columns wg + 8k, partial tree, publish
+                constexpr int PER = (32 * 27 + 64 * IP_WAVES - 1) / (64 * IP_WAVES);
+                const unsigned long long* cols = &tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE];
+                unsigned long long v[PER];
+#pragma unroll
+                for (int k = 0; k < PER; ++k) {
+                    const int e = tid + 64 * IP_WAVES * k;
+                    const int kk = e / 27, q = e - kk * 27;
+                    v[k] = e < 32 * 27 ? ip_load(&cols[(wg + IP_NPART * kk) * ICP_T_STRIDE + q]) : ((unsigned long long)gen << 32);
+                }
+                bool timeout = false;
+                for (unsigned spins = 0;; ++spins) {
+                    bool ready = true;
+#pragma unroll
+                    for (int k = 0; k < PER; ++k) {
+                        if ((unsigned)(v[k] >> 32) != gen) {
+                            ready = false;
+                            const int e = tid + 64 * IP_WAVES * k;
+                            const int kk = e / 27, q = e - kk * 27;
+                            v[k] = ip_load(&cols[(wg + IP_NPART * kk) * ICP_T_STRIDE + q]);
+                        }
+                    }
+                    if (ready) break;
+                    if (spins > IP_SPIN_LIMIT) { timeout = true; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+#pragma unroll
+                for (int k = 0; k < PER; ++k) {
+                    const int e = tid + 64 * IP_WAVES * k;
+                    const int kk = e / 27, q = e - kk * 27;
+                    if (e < 32 * 27) tl[q][kk] = __uint_as_float((unsigned)v[k]);
+                }
+                const int lead_timeout = __syncthreads_or(timeout);
+                if (!lead_timeout && tid < 27)          // a missing column: publish nothing, WG0 times out
+                    ip_store(&tag[IP_PART + (gen & 1) * IP_NPART * ICP_T_STRIDE + wg * ICP_T_STRIDE + tid],
+                             ip_pack(gen, ip_residue_tree(tl[tid])));
+            }
+            if ((SCHED == 2 && wg == 0) || SCHED == 3) {
+                // ---- gather the 8 x 27 partials, last three tree steps, det / solve / compose
+                // (SCHED 3: every workgroup, redundantly and bit-identically -- no broadcast hop)
+                const unsigned long long* parts = &tag[IP_PART + (gen & 1) * IP_NPART * ICP_T_STRIDE];
+                bool timeout = false;
+                if (tid < IP_NPART * 27) {
+                    const int x = tid / 27, q = tid - x * 27;
+                    unsigned long long v = ip_load(&parts[x * ICP_T_STRIDE + q]);
+                    for (unsigned spins = 0; (unsigned)(v >> 32) != gen; ++spins) {
+                        if (spins > IP_SPIN_LIMIT) { timeout = true; break; }
+                        __builtin_amdgcn_s_sleep(1);
+                        v = ip_load(&parts[x * ICP_T_STRIDE + q]);
+                    }
+                    tv[q][x] = __uint_as_float((unsigned)v);
+                }
+                if (tid == 0) det_ok_s = 1;
+                const int any_timeout = __syncthreads_or(timeout);
+                IPT_REC(done, 2 * ICP_NWG + 0);
+                if (!any_timeout && wave < 2) {
+                    // steps 4, 2, 1: ((P0+P4) + (P2+P6)) + ((P1+P5) + (P3+P7)); lane q holds sum q
+                    float tot = 0.f;
+                    if (lane < 27) {
+                        const float* P = tv[lane];
+                        tot = ((P[0] + P[4]) + (P[2] + P[6])) + ((P[1] + P[5]) + (P[3] + P[7]));
+                    }
+                    float sm[27], Am[6][6], bv[6];
+#pragma unroll
+                    for (int q = 0; q < 27; ++q)
+                        sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), q));
+                    ip_unpack(sm, Am, bv);
+                    IPT_REC(done, 2 * ICP_NWG + 2);
+                    if (wave == 1) {                                   // det on its own wave
+                        const double det = icp_det6_reg(Am);           // projective_icp.cpp:197-203
+                        if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
+                        IPT_REC_T(done, 2 * ICP_NWG + 5, 64);
+                    } else {                                           // solve -> Rodrigues -> compose
+                        float rv[6], R[9], tinc[12];
+                        icp_solve6_reg(Am, bv, rv);                     // projective_icp.cpp:206-209
+                        IPT_REC(done, 2 * ICP_NWG + 3);
+                        icp_rodrigues(rv, R);
+#pragma unroll
+                        for (int j = 0; j < 3; ++j) {
+                            tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1];
+                            tinc[j * 4 + 2] = R[j * 3 + 2]; tinc[j * 4 + 3] = rv[3 + j];
+                        }
+                        float A[12];
+#pragma unroll
+                        for (int i = 0; i < 12; ++i) A[i] = aff[i];
+                        tf_rigid_mul(tinc, A, A);
+                        if (lane < 12) aff_s[lane] = A[lane];
+                        IPT_REC(done, 2 * ICP_NWG + 4);
+                        last_sums = tot;
+                    }
+                }
+                __syncthreads();
+                IPT_REC(done, 2 * ICP_NWG + 1);
+                status = any_timeout ? 2 : (det_ok_s ? 1 : 0);
+                if (SCHED == 2 && wave == 0 && lane <= 12) {           // broadcast affine + status
+                    const float v = lane < 12 ? aff_s[lane] : (float)status;
+                    ip_store(&tag[IP_BCAST + lane], ip_pack(gen, v));
+                }
+                if (status == 1) {
+#pragma unroll
+                    for (int i = 0; i < 12; ++i) aff[i] = aff_s[i];
+                }
+            } else if (SCHED < 2 && (ALLGATHER || wg == 0)) {
                 // ---- gather the 256 column sums (tagged polling; all loads in flight at once)
                 constexpr int PER = (ICP_NWG * 27 + 64 * IP_WAVES - 1) / (64 * IP_WAVES);
                 unsigned long long v[PER];
@@ -871,7 +1005,7 @@ static int icp_used_levels(const tf_params& p)
 int tfk_icp_persistent_ok(tf_ctx* c)
 {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame<false>, 64 * IP_WAVES, IP_LDS_PAD) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame<2>, 64 * IP_WAVES, IP_LDS_PAD) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) return 0;
     if (per_cu * cus < ICP_NWG) return 0;
     for (int l = 0; l < TF_LEVELS; ++l) {
@@ -903,10 +1037,14 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update)
         a.tag = c->icp_tagged;
         // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
         // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up
-        if (c->icp_allgather)
-            hipLaunchKernelGGL(k_icp_frame<true>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
+        if (c->icp_sched == 3)
+            hipLaunchKernelGGL(k_icp_frame<3>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
+        else if (c->icp_sched == 1)
+            hipLaunchKernelGGL(k_icp_frame<1>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
+        else if (c->icp_sched == 0)
+            hipLaunchKernelGGL(k_icp_frame<0>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
         else
-            hipLaunchKernelGGL(k_icp_frame<false>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
+            hipLaunchKernelGGL(k_icp_frame<2>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, c->stream, c->st);

@@ -19,7 +19,8 @@
 #define TF_RB_SIZE 16           // renderingBlockSizeX/Y (VisualisationEngine_Shared.hpp:25-26)
 #define TF_LEVELS 3
 #define TF_NUM_STAGES 9     // tf_stage_id in include/tfusion_hip.h
-#define TF_PROF_RING 32     // frames enqueued between host syncs (and timing-event ring slots)
+#define TF_PROF_RING 32
+#define TF_ICP_TAG_WORDS (2 * 256 * 28 + 16 + 2 * 8 * 28)   // persistent ICP tagged granules (tf_icp.hip)     // frames enqueued between host syncs (and timing-event ring slots)
 
 // HashEntry, VoxelBlockHash.hpp:32-44 (16 B; one dwordx4 probe)
 struct __attribute__((aligned(16))) TfHashEntry {
@@ -221,7 +222,7 @@ struct tf_ctx {
     unsigned* icp_ticket;    // last-workgroup ticket (zero between launches)
     unsigned long long* icp_tagged;   // persistent ICP: [256][28] tagged column sums + [16] broadcast
     int icp_persistent;      // 1: one launch per frame (k_icp_frame), 0: one launch per iteration
-    int icp_allgather;       // persistent ICP: every workgroup gathers + solves (no broadcast hop)
+    int icp_sched;           // persistent ICP: 0 WG0 gathers 256 columns, 1 allgather, 2 hierarchical, 3 hierarchical allgather (default)
     int icp_max_cta;
     float min_cosine, dist2_thres;
     // device state
