@@ -251,15 +251,15 @@ def test_capacity_exhaustion(oracle_mod):
     compare_scene(g, o, "exhausted")
 
 
-@pytest.mark.parametrize("render_late", ["0", "1"])
-def test_batched_frames_overlap(oracle_mod, monkeypatch, render_late):
+@pytest.mark.parametrize("render_mode", ["0", "1", "2"])
+def test_batched_frames_overlap(oracle_mod, monkeypatch, render_mode):
     """The device-driven batch path (tf_process_frames): frames enqueued back to back with no
     host sync, renderImage on the render stream overlapping the frame's tail and the next
-    frame's ICP (TFUSION_RENDER_LATE selects which).  Per-frame results, the last frame's grey
+    frame's ICP, or inline (TFUSION_RENDER_MODE 0 / 1 / 2).  Per-frame results, the last frame's grey
     image, the final pose and the whole scene match the oracle run frame by frame."""
     from parity_util import DeviceFrames
     from topfusion_amd import TopFu, default_params
-    monkeypatch.setenv("TFUSION_RENDER_LATE", render_late)
+    monkeypatch.setenv("TFUSION_RENDER_MODE", render_mode)
     cols, rows, n = 320, 240, 40          # 40 frames > one 32-frame enqueue group
     fx, fy, cx, cy = synth.intrinsics(cols, rows)
     args = dict(cols=cols, rows=rows, fx=fx, fy=fy, cx=cx, cy=cy)

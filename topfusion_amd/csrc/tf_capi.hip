@@ -180,6 +180,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_integrated, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_rendered, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventRecord(c->ev_rendered, c->rstream);
+    if (e == hipSuccess) e = hipEventRecord(c->ev_integrated, c->stream);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     ALLOC(c->hash, sizeof(TfHashEntry) * (size_t)c->n_total);
     ALLOC(c->excessList, sizeof(int) * (size_t)pin->n_excess);
@@ -269,8 +270,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         c->icp_sched = 3;
         if (ag && ag[0] == '1') c->icp_sched = 1;
         if (sc && sc[0] >= '0' && sc[0] <= '3') c->icp_sched = sc[0] - '0';
-        const char* rl = getenv("TFUSION_RENDER_LATE");
-        c->render_late = (rl && rl[0] == '1') ? 1 : 0;
+        const char* rm = getenv("TFUSION_RENDER_MODE");
+        c->render_mode = (rm && rm[0] >= '0' && rm[0] <= '2') ? rm[0] - '0' : 2;
     }
     *out = c;
     return TF_OK;
@@ -362,8 +363,10 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
 // it (frame counters, per-slot ok flag).  A batch is therefore enqueued back to back.
 static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, int slot)
 {
-    STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, 1));  // topfu.cpp:166-197 (+ frame begin)
-    STAGE(TF_STAGE_ICP, tfk_icp(c, 1));                              // topfu.cpp:242-243 (tracking only)
+    // preprocessing (topfu.cpp:166-197).  (Measured: on a stream of its own, overlapping the
+    // previous frame's tail, the cross-stream waits cost more than the overlap saves.)
+    STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, c->stream));
+    STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1));                           // frame begin + topfu.cpp:242-243 (tracking only)
     // the previous frame's renderImage (render stream) must be done before the scene changes
     TF_CHECK(join_render(c));
     TF_CHECK(tfk_render_prologue(c));
@@ -372,19 +375,21 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     // renderImage (raycast + grey, topfu.cpp:284-285) on the render stream, behind integration;
     // it overlaps CreateExpectedDepths / CreateICPMaps and the next frame's preprocessing + ICP,
     // none of which writes what it reads (the scene, the range snapshot, M_render)
-    if (!c->render_late) {
+    if (c->render_mode == 2) {   // inline on the main stream (A/B reference)
+        STAGE(TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c, c->stream));
+    } else if (c->render_mode == 0) {
         TF_CHECK(hipEventRecord(c->ev_integrated, c->stream));
         TF_CHECK(hipStreamWaitEvent(c->rstream, c->ev_integrated, 0));
-        STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c));
+        STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c, c->rstream));
         TF_CHECK(hipEventRecord(c->ev_rendered, c->rstream));
     }
     STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c));         // topfu.cpp:306
     STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));                  // CreateICPMaps, topfu.cpp:307
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps(c));                       // + resizePointsNormals :308-309
-    if (c->render_late) {   // render behind the frame's tail: it overlaps the next frame's ICP
+    if (c->render_mode == 1) {   // render behind the frame's tail: it overlaps the next frame's ICP
         TF_CHECK(hipEventRecord(c->ev_integrated, c->stream));
         TF_CHECK(hipStreamWaitEvent(c->rstream, c->ev_integrated, 0));
-        STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c));
+        STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c, c->rstream));
         TF_CHECK(hipEventRecord(c->ev_rendered, c->rstream));
     }
     TF_CHECK(tfk_reset_scene_on_failure(c, slot));                   // frame end; topfu.cpp:263-264
@@ -569,7 +574,7 @@ extern "C" tf_status tf_stage_preprocess(tf_ctx* c, const uint16_t* dev_depth, s
     if (!c || !dev_depth) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
     TF_CHECK(clear_abort(c));
-    TF_CHECK(tfk_preprocess(c, dev_depth, pitch));
+    TF_CHECK(tfk_preprocess(c, dev_depth, pitch, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }

@@ -463,6 +463,7 @@ struct IcpFrameArgs {
     int nlev;
     int total_iters;
     int pose_update;
+    int frame_begin;                    // frame path: the launch starts the frame (tf_frame_begin)
     TfDevState* st;
     unsigned long long* tag;            // [256][28] column sums, then [16] broadcast
 };
@@ -621,7 +622,17 @@ k_icp_frame(IcpFrameArgs a)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, wg = blockIdx.x;
     TfDevState* st = a.st;
     unsigned long long* tag = a.tag;
-    if (st->mode == 0) return;                 // frame 0 runs no ICP (uniform over the grid)
+    if (a.frame_begin) {
+        // the device-driven frame starts here (TopFu::operator(), topfu.cpp:200): frame 0 of a
+        // run (frame_counter == 0) takes the integrate-only path.  Workgroup 0 records the
+        // frame's mode; every workgroup derives it from frame_counter, which only the previous
+        // frame's end wrote (so the preprocessing stream never touches the state)
+        const bool frame0 = st->frame_counter == 0;
+        if (wg == 0 && tid == 0) tf_frame_begin(st);
+        if (frame0) return;
+    } else if (st->mode == 0) {
+        return;                                // frame 0 runs no ICP (uniform over the grid)
+    }
     const unsigned base = st->icp_gen;
     unsigned gen = base;
     float aff[12];
@@ -940,8 +951,9 @@ k_icp_frame(IcpFrameArgs a)
     }
 }
 
-__global__ void k_icp_begin(TfDevState* st)
+__global__ void k_icp_begin(TfDevState* st, int frame_begin)
 {
+    if (frame_begin) tf_frame_begin(st);       // frame path: the frame starts here
     if (st->mode == 0) return;                 // frame 0 runs no ICP
     for (int i = 0; i < 12; ++i) st->affine[i] = (i % 5 == 0) ? 1.0f : 0.0f;   // affine = Identity
     st->icp_ok = 1;
@@ -1016,7 +1028,7 @@ int tfk_icp_persistent_ok(tf_ctx* c)
     return 1;
 }
 
-hipError_t tfk_icp(tf_ctx* c, int pose_update)
+hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin)
 {
     const tf_params& p = c->p;
     const int levels = icp_used_levels(p);
@@ -1033,6 +1045,7 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update)
             a.nlev++;
         }
         a.pose_update = pose_update;
+        a.frame_begin = frame_begin;
         a.st = c->st;
         a.tag = c->icp_tagged;
         // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
@@ -1047,7 +1060,7 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update)
             hipLaunchKernelGGL(k_icp_frame<2>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, c->stream, c->st);
+    hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, c->stream, c->st, frame_begin);
     int last_l = -1;
     for (int l = 0; l < levels; ++l) if (p.icp_iter_num[l] > 0) { last_l = l; break; }
     for (int l = levels - 1; l >= 0; --l) {

@@ -180,7 +180,8 @@ struct tf_ctx {
     hipStream_t stream;
     hipStream_t rstream;     // renderImage stream (tf_capi.hip: enqueue_frame)
     hipEvent_t ev_integrated, ev_rendered;
-    int render_late;         // 1: renderImage enqueued behind the frame's tail (overlaps the next ICP)
+    int render_mode;         // renderImage: 0 render stream behind integration, 1 render stream
+                             // behind the frame's tail (overlaps the next ICP), 2 inline on the main stream (default: measured fastest)
     int n_total;
     int W, H;
     int lw[TF_LEVELS], lh[TF_LEVELS];
@@ -245,8 +246,8 @@ struct tf_ctx {
 // ---------------------------------------------------------------------------------------
 // launchers (one per kernel family); all enqueue on ctx->stream
 // ---------------------------------------------------------------------------------------
-hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, int frame_begin = 0);
-hipError_t tfk_icp(tf_ctx* c, int pose_update);
+hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStream_t strm);   // no st access
+hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin = 0);   // frame_begin: frame path (tf_frame_begin)
 int tfk_icp_persistent_ok(tf_ctx* c);      // k_icp_frame fits (co-residency, slot count)
 hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / raycast matrices
 hipError_t tfk_reset_scene(tf_ctx* c);
@@ -256,7 +257,7 @@ hipError_t tfk_alloc(tf_ctx* c);
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_grey(tf_ctx* c);
-hipError_t tfk_raycast_grey(tf_ctx* c);    // renderImage raycast + grey, fused (frame path, render stream)
+hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);    // renderImage raycast + grey, fused (frame path, render stream)
 hipError_t tfk_render_prologue(tf_ctx* c); // snapshot for the frame's renderImage (main stream)
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_expected_depths(tf_ctx* c);

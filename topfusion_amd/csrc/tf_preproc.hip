@@ -19,11 +19,9 @@
 __global__ void __launch_bounds__(256)
 k_dists_bilateral(const uint16_t* __restrict__ src, size_t pitch, int W, int H, int ksz,
                   float ss, float sd, int do_trunc, unsigned trunc_mm,
-                  float* __restrict__ dists, uint16_t* __restrict__ dst, TfDevState* st, int frame_begin)
+                  float* __restrict__ dists, uint16_t* __restrict__ dst)
 {
     __shared__ uint16_t tile[PRE_TY + 2 * HALO][PRE_TX + 2 * HALO + 2];
-    // the device-driven frame starts here (no separate launch): nothing in this kernel reads st
-    if (frame_begin && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) tf_frame_begin(st);
     const int tx = threadIdx.x & (PRE_TX - 1), ty = threadIdx.x / PRE_TX;
     const int x0 = blockIdx.x * PRE_TX, y0 = blockIdx.y * PRE_TY;
     for (int i = threadIdx.x; i < (PRE_TY + 2 * HALO) * (PRE_TX + 2 * HALO); i += 256) {
@@ -122,7 +120,7 @@ k_points_normals(PtsLevels L)
 
 static inline int div_up(int a, int b) { return (a + b - 1) / b; }
 
-hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, int frame_begin)
+hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStream_t strm)
 {
     const tf_params& p = c->p;
     const int W = c->W, H = c->H;
@@ -132,12 +130,11 @@ hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, int fr
     int do_trunc = p.icp_truncate_depth_dist > 0;
     unsigned trunc_mm = (unsigned)(uint16_t)(p.icp_truncate_depth_dist * 1000.f);   // imgproc.cu:87
     if (p.bilateral_kernel_size > 2 * HALO + 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_dists_bilateral, dim3(div_up(W, PRE_TX), div_up(H, PRE_TY)), dim3(256), 0, c->stream,
-                       depth, pitch, W, H, p.bilateral_kernel_size, ss, sd, do_trunc, trunc_mm, c->dists, c->depth_pyr[0],
-                       c->st, frame_begin);
+    hipLaunchKernelGGL(k_dists_bilateral, dim3(div_up(W, PRE_TX), div_up(H, PRE_TY)), dim3(256), 0, strm,
+                       depth, pitch, W, H, p.bilateral_kernel_size, ss, sd, do_trunc, trunc_mm, c->dists, c->depth_pyr[0]);
     float sigma3 = sigma_depth * 3.0f;                                               // imgproc.cu:138
     for (int l = 1; l < TF_LEVELS; ++l)
-        hipLaunchKernelGGL(k_pyr_down, dim3(div_up(c->lw[l], 32), div_up(c->lh[l], 8)), dim3(256), 0, c->stream,
+        hipLaunchKernelGGL(k_pyr_down, dim3(div_up(c->lw[l], 32), div_up(c->lh[l], 8)), dim3(256), 0, strm,
                            c->depth_pyr[l - 1], c->lw[l - 1], c->lh[l - 1], c->depth_pyr[l], c->lw[l], c->lh[l], sigma3);
     PtsLevels L;
     for (int l = 0; l < TF_LEVELS; ++l) {
@@ -146,6 +143,6 @@ hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, int fr
         L.w[l] = c->lw[l]; L.h[l] = c->lh[l];
         L.fx[l] = p.fx / (float)div; L.fy[l] = p.fy / (float)div; L.cx[l] = p.cx / (float)div; L.cy[l] = p.cy / (float)div;
     }
-    hipLaunchKernelGGL(k_points_normals, dim3(div_up(W, 32), div_up(H, 8), TF_LEVELS), dim3(256), 0, c->stream, L);
+    hipLaunchKernelGGL(k_points_normals, dim3(div_up(W, 32), div_up(H, 8), TF_LEVELS), dim3(256), 0, strm, L);
     return hipGetLastError();
 }

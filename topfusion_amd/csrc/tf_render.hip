@@ -342,13 +342,13 @@ static void ray_args(tf_ctx* c, RayArgs& a)
     a.oneOverVoxelSize = 1.0f / c->p.voxelSize; a.mu = c->p.mu;
 }
 
-static hipError_t launch_ray(tf_ctx* c, const RayArgs& a, int mode)
+static hipError_t launch_ray(tf_ctx* c, const RayArgs& a, int mode, hipStream_t strm = nullptr)
 {
     const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty;
     const dim3 grid((n + 7) / 8 * 8);
     if (mode == 0) hipLaunchKernelGGL(k_raycast<0>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
     else if (mode == 1) hipLaunchKernelGGL(k_raycast<1>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
-    else hipLaunchKernelGGL(k_raycast<2>, grid, dim3(256), 0, c->rstream, a, c->st, tx, n);
+    else hipLaunchKernelGGL(k_raycast<2>, grid, dim3(256), 0, strm, a, c->st, tx, n);
     return hipGetLastError();
 }
 
@@ -363,13 +363,13 @@ hipError_t tfk_raycast(tf_ctx* c, int update_visible)
 // renderImage in the frame path: castRay<false> + renderGrey fused (the intermediate point
 // image is overwritten by CreateICPMaps before anything can observe it).  It is enqueued on
 // the render stream behind the frame's integration and reads the range-image snapshot.
-hipError_t tfk_raycast_grey(tf_ctx* c)
+hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm)
 {
     RayArgs a;
     ray_args(c, a);
     a.range = (const float2*)c->range_render;
     a.grey = c->grey;
-    return launch_ray(c, a, 2);
+    return launch_ray(c, a, 2, strm);
 }
 
 // Main stream, after the previous frame's renderImage has finished and this frame's ICP has
@@ -486,40 +486,55 @@ __device__ __forceinline__ void resize4(const float4* v, const float4* n, float4
     }
 }
 
+// One workgroup per 32x32 tile of level 0: thread t owns the 2x2 level-0 quad under level-1
+// pixel (t & 15, t >> 4) of the tile's 16x16 level-1 tile, so it computes four processPixelICP
+// results and their resizePointsNormals average directly; level 2 (8x8 per tile) is averaged
+// from the level-1 values staged in LDS.  Every level-0 pixel is evaluated once (levels 1/2
+// are computed from the level-0 results, exactly as the reference's resize of the level-0
+// maps).
 __global__ void __launch_bounds__(256)
 k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
 {
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
-    const int l = blockIdx.z;
-    const int lw = a.W >> l, lh = a.H >> l;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= lw || y >= lh) return;
+    __shared__ float4 v1s[16][17], n1s[16][17];
+    const int lx1 = threadIdx.x & 15, ly1 = threadIdx.x >> 4;
+    const int x1 = blockIdx.x * 16 + lx1, y1 = blockIdx.y * 16 + ly1;
+    const int W = a.W, H = a.H, w1 = W >> 1, h1 = H >> 1, w2 = W >> 2, h2 = H >> 2;
     const float lx = -st->M_ray[8], ly = -st->M_ray[9], lz = -st->M_ray[10];
-    float4 po, no;
-    if (l == 0) {
-        icp_pixel(a, lx, ly, lz, x, y, &po, &no);
-    } else if (l == 1) {
-        float4 v[4], n[4];
-        icp_pixel(a, lx, ly, lz, 2 * x, 2 * y, &v[0], &n[0]);
-        icp_pixel(a, lx, ly, lz, 2 * x + 1, 2 * y, &v[1], &n[1]);
-        icp_pixel(a, lx, ly, lz, 2 * x, 2 * y + 1, &v[2], &n[2]);
-        icp_pixel(a, lx, ly, lz, 2 * x + 1, 2 * y + 1, &v[3], &n[3]);
-        resize4(v, n, &po, &no);
-    } else {
-        float4 v1[4], n1[4];
-        for (int q = 0; q < 4; ++q) {
-            int x1 = 2 * x + (q & 1), y1 = 2 * y + (q >> 1);
-            float4 v[4], n[4];
-            icp_pixel(a, lx, ly, lz, 2 * x1, 2 * y1, &v[0], &n[0]);
-            icp_pixel(a, lx, ly, lz, 2 * x1 + 1, 2 * y1, &v[1], &n[1]);
-            icp_pixel(a, lx, ly, lz, 2 * x1, 2 * y1 + 1, &v[2], &n[2]);
-            icp_pixel(a, lx, ly, lz, 2 * x1 + 1, 2 * y1 + 1, &v[3], &n[3]);
-            resize4(v, n, &v1[q], &n1[q]);
+    float4 v[4], n[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int x = 2 * x1 + (q & 1), y = 2 * y1 + (q >> 1);
+        if (x < W && y < H) {
+            icp_pixel(a, lx, ly, lz, x, y, &v[q], &n[q]);
+            a.pts[0][y * W + x] = v[q];
+            a.nrm[0][y * W + x] = n[q];
         }
-        resize4(v1, n1, &po, &no);
     }
-    a.pts[l][y * lw + x] = po;
-    a.nrm[l][y * lw + x] = no;
+    if (x1 < w1 && y1 < h1) {
+        float4 po, no;
+        resize4(v, n, &po, &no);
+        a.pts[1][y1 * w1 + x1] = po;
+        a.nrm[1][y1 * w1 + x1] = no;
+        v1s[ly1][lx1] = po;
+        n1s[ly1][lx1] = no;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int lx2 = threadIdx.x & 7, ly2 = threadIdx.x >> 3;
+        const int x2 = blockIdx.x * 8 + lx2, y2 = blockIdx.y * 8 + ly2;
+        if (x2 < w2 && y2 < h2) {
+            float4 vv[4], nn[4], po, no;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                vv[q] = v1s[2 * ly2 + (q >> 1)][2 * lx2 + (q & 1)];
+                nn[q] = n1s[2 * ly2 + (q >> 1)][2 * lx2 + (q & 1)];
+            }
+            resize4(vv, nn, &po, &no);
+            a.pts[2][y2 * w2 + x2] = po;
+            a.nrm[2][y2 * w2 + x2] = no;
+        }
+    }
 }
 
 hipError_t tfk_icp_maps(tf_ctx* c)
@@ -528,7 +543,7 @@ hipError_t tfk_icp_maps(tf_ctx* c)
     a.ray = (const float4*)c->raycast;
     for (int l = 0; l < TF_LEVELS; ++l) { a.pts[l] = c->prev_pts[l]; a.nrm[l] = c->prev_nrm[l]; }
     a.W = c->W; a.H = c->H; a.voxelSize = c->p.voxelSize;
-    hipLaunchKernelGGL(k_icp_maps, dim3((c->W + 15) / 16, (c->H + 15) / 16, TF_LEVELS), dim3(256), 0, c->stream, a, c->st);
+    hipLaunchKernelGGL(k_icp_maps, dim3((c->W + 31) / 32, (c->H + 31) / 32), dim3(256), 0, c->stream, a, c->st);
     return hipGetLastError();
 }
 
