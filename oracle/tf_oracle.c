@@ -939,6 +939,12 @@ static inline float sdf_interp_conf(const tfo_ctx* c, float* confidence, const f
     return ((1.0f - cz) * res1 + cz * res2) / 32767.0f;
 }
 
+/* debug instrumentation (analysis only; off unless buffers are set): per-pixel ray-march
+   sample counts of the last raycast, total and in unallocated blocks */
+static int* g_dbg_steps = 0;
+static int* g_dbg_empty = 0;
+void tfo_debug_ray_buffers(int* steps, int* empty) { g_dbg_steps = steps; g_dbg_empty = empty; }
+
 /* castRay, VisualisationEngine_Shared.hpp:99-172 */
 static void cast_ray(tfo_ctx* c, float out[4], int update_visible, int x, int y, const float invM[16],
                      const float invProj[4], float oneOverVoxelSize, float mu, const float* range2)
@@ -967,8 +973,11 @@ static void cast_ray(tfo_ctx* c, float out[4], int update_visible, int x, int y,
     dir[0] *= direction_norm; dir[1] *= direction_norm; dir[2] *= direction_norm;
     pt[0] = ps[0]; pt[1] = ps[1]; pt[2] = ps[2];
     icache k; cache_init(&k);
+    int n_steps = 0, n_empty = 0;
     while (totalLength < totalLengthMax) {
         sdfValue = sdf_uninterp(c, pt, &vmIndex, &k);
+        n_steps++;
+        if (!vmIndex) n_empty++;
         if (update_visible) {
             if (vmIndex) c->visType[vmIndex - 1] = 1;
         }
@@ -994,6 +1003,7 @@ static void cast_ray(tfo_ctx* c, float out[4], int update_visible, int x, int y,
     } else found = 0;
     out[0] = pt[0]; out[1] = pt[1]; out[2] = pt[2];
     out[3] = found ? confidence + 1.0f : 0.0f;
+    if (g_dbg_steps) { g_dbg_steps[x + y * c->p.cols] = n_steps; g_dbg_empty[x + y * c->p.cols] = n_empty; }
 }
 
 /* GenericRaycast, VisualisationEngine_CUDA.cu:175-218; genericRaycast_device VisualisationHelper.hpp:33-46 */

@@ -251,11 +251,11 @@ def test_capacity_exhaustion(oracle_mod):
     compare_scene(g, o, "exhausted")
 
 
-@pytest.mark.parametrize("render_mode", ["0", "1", "2"])
+@pytest.mark.parametrize("render_mode", ["0", "1", "2", "3"])
 def test_batched_frames_overlap(oracle_mod, monkeypatch, render_mode):
     """The device-driven batch path (tf_process_frames): frames enqueued back to back with no
     host sync, renderImage on the render stream overlapping the frame's tail and the next
-    frame's ICP, or inline (TFUSION_RENDER_MODE 0 / 1 / 2).  Per-frame results, the last frame's grey
+    frame's ICP, inline, or fused with CreateICPMaps' raycast (TFUSION_RENDER_MODE 0-3).  Per-frame results, the last frame's grey
     image, the final pose and the whole scene match the oracle run frame by frame."""
     from parity_util import DeviceFrames
     from topfusion_amd import TopFu, default_params

@@ -271,7 +271,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         if (ag && ag[0] == '1') c->icp_sched = 1;
         if (sc && sc[0] >= '0' && sc[0] <= '3') c->icp_sched = sc[0] - '0';
         const char* rm = getenv("TFUSION_RENDER_MODE");
-        c->render_mode = (rm && rm[0] >= '0' && rm[0] <= '2') ? rm[0] - '0' : 2;
+        c->render_mode = (rm && rm[0] >= '0' && rm[0] <= '3') ? rm[0] - '0' : 3;
     }
     *out = c;
     return TF_OK;
@@ -347,6 +347,7 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
     for (int f = 0; f < n; ++f)
         for (int i = 0; i < TF_NUM_STAGES; ++i) {
             if (!((c->prof_mask >> i) & 1u) || !stage_ran(i, mode[f], ok[f])) continue;
+            if (i == TF_STAGE_RAYCAST_RENDER && c->render_mode == 3) continue;   // fused into RAYCAST_ICP
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, prof_event(c, first + f, 2 * i), prof_event(c, first + f, 2 * i + 1)) == hipSuccess) {
                 c->prof_ms[i] += ms;
@@ -384,7 +385,10 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
         TF_CHECK(hipEventRecord(c->ev_rendered, c->rstream));
     }
     STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c));         // topfu.cpp:306
-    STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));                  // CreateICPMaps, topfu.cpp:307
+    if (c->render_mode == 3)    // CreateICPMaps raycast + renderImage in one launch (snapshot range)
+        STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c));            // topfu.cpp:284-285 + 307
+    else
+        STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));              // CreateICPMaps, topfu.cpp:307
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps(c));                       // + resizePointsNormals :308-309
     if (c->render_mode == 1) {   // render behind the frame's tail: it overlaps the next frame's ICP
         TF_CHECK(hipEventRecord(c->ev_integrated, c->stream));

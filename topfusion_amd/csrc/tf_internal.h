@@ -181,7 +181,8 @@ struct tf_ctx {
     hipStream_t rstream;     // renderImage stream (tf_capi.hip: enqueue_frame)
     hipEvent_t ev_integrated, ev_rendered;
     int render_mode;         // renderImage: 0 render stream behind integration, 1 render stream
-                             // behind the frame's tail (overlaps the next ICP), 2 inline on the main stream (default: measured fastest)
+                             // behind the frame's tail (overlaps the next ICP), 2 inline on the main
+                             // stream, 3 fused with CreateICPMaps' raycast in one launch (default)
     int n_total;
     int W, H;
     int lw[TF_LEVELS], lh[TF_LEVELS];
@@ -257,7 +258,8 @@ hipError_t tfk_alloc(tf_ctx* c);
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_grey(tf_ctx* c);
-hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);    // renderImage raycast + grey, fused (frame path, render stream)
+hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);
+hipError_t tfk_raycast_pair(tf_ctx* c);   // CreateICPMaps raycast + renderImage, one launch (frame path)    // renderImage raycast + grey, fused (frame path, render stream)
 hipError_t tfk_render_prologue(tf_ctx* c); // snapshot for the frame's renderImage (main stream)
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_expected_depths(tf_ctx* c);

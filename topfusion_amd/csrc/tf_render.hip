@@ -307,14 +307,13 @@ __device__ __forceinline__ int xcd_tile(int bid, int n)
 
 // MODE 0: castRay<false> -> point image; 1: castRay<true> (visibility marks) -> point image
 // (CreateICPMaps); 2: castRay<false> + renderGrey fused (renderImage in the frame path).
-// Distinct instantiations also give each use its own kernel name in rocprof.
 template <int MODE>
-__global__ void __launch_bounds__(256)
-k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles)
+__device__ __forceinline__ void raycast_tile(const RayArgs& a, const TfDevState* __restrict__ st, int bid,
+                                             int tiles_x, int n_tiles)
 {
-    // the frame's renderImage (MODE 2, render stream) reads the snapshot k_render_prologue took
+    // the frame's renderImage (MODE 2) reads the snapshot k_render_prologue took
     if (MODE == 2 ? !st->render_go : (st->abort || st->mode == 0)) return;   // ICP failed, or frame 0
-    const int tile = xcd_tile(blockIdx.x, n_tiles);     // grid padded to a multiple of 8
+    const int tile = xcd_tile(bid, n_tiles);            // grid padded to a multiple of 8
     if (tile < 0) return;
     const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15), y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.H) return;
@@ -329,6 +328,26 @@ k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles
     } else {
         a.out[x + y * a.W] = make_float4(pt[0], pt[1], pt[2], w);
     }
+}
+
+// Distinct instantiations also give each use its own kernel name in rocprof.
+template <int MODE>
+__global__ void __launch_bounds__(256)
+k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles)
+{
+    raycast_tile<MODE>(a, st, blockIdx.x, tiles_x, n_tiles);
+}
+
+// The frame's two raycasts in one launch: the first half of the grid casts CreateICPMaps'
+// rays (castRay<true>, new range image), the second half renderImage's (castRay<false> +
+// grey, range snapshot).  Neither writes what the other reads, and a launch's run time is its
+// slowest waves' ray length: the halves fill each other's tails instead of each kernel
+// draining alone.
+__global__ void __launch_bounds__(256)
+k_raycast_pair(RayArgs ai, RayArgs ar, const TfDevState* __restrict__ st, int tiles_x, int n_tiles, int nb)
+{
+    if ((int)blockIdx.x < nb) raycast_tile<1>(ai, st, blockIdx.x, tiles_x, n_tiles);
+    else raycast_tile<2>(ar, st, blockIdx.x - nb, tiles_x, n_tiles);
 }
 
 static void ray_args(tf_ctx* c, RayArgs& a)
@@ -363,6 +382,22 @@ hipError_t tfk_raycast(tf_ctx* c, int update_visible)
 // renderImage in the frame path: castRay<false> + renderGrey fused (the intermediate point
 // image is overwritten by CreateICPMaps before anything can observe it).  It is enqueued on
 // the render stream behind the frame's integration and reads the range-image snapshot.
+// CreateICPMaps' raycast + the frame's renderImage in one launch (main stream, after
+// CreateExpectedDepths)
+hipError_t tfk_raycast_pair(tf_ctx* c)
+{
+    RayArgs ai, ar;
+    ray_args(c, ai);
+    ai.visType = c->visType;
+    ray_args(c, ar);
+    ar.range = (const float2*)c->range_render;
+    ar.grey = c->grey;
+    const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty;
+    const int nb = (n + 7) / 8 * 8;
+    hipLaunchKernelGGL(k_raycast_pair, dim3(2 * nb), dim3(256), 0, c->stream, ai, ar, c->st, tx, n, nb);
+    return hipGetLastError();
+}
+
 hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm)
 {
     RayArgs a;
