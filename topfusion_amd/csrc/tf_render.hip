@@ -32,14 +32,20 @@ struct RCache { int bx, by, bz, voff; };   // VoxelBlockHash::IndexCache (VoxelB
 // reference's serial corner order.  Values, the IndexCache state and vmIndex are exactly
 // those of the reference's serial reads (RepresentationAccess.hpp:73-199).
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int vblk(int p) { return ((p < 0) ? p - TF_BLK + 1 : p) / TF_BLK; }   // :9-17
+__device__ __forceinline__ int vblk(int p) { return p >> 3; }   // floor(p / 8) (:9-17), arithmetic shift
 __device__ __forceinline__ int vlin(int x, int y, int z) { return (x & 7) + ((y & 7) << 3) + ((z & 7) << 6); }
 
-// (hash entry index, VBA voxel offset) of block (bx,by,bz), or (-1,-1) when findVoxel fails
-__device__ __forceinline__ int2 blk_find(const SceneView& s, int bx, int by, int bz)
+// 32-bit byte offset from a uniform (kernel-argument) base: one global_load with an SGPR base
+// and a VGPR offset, no 64-bit address arithmetic per lane
+template <typename T>
+__device__ __forceinline__ T ld_off(const void* base, unsigned byte_off)
 {
-    const unsigned gx = (unsigned)(bx + TF_GRID_HALF), gy = (unsigned)(by + TF_GRID_HALF), gz = (unsigned)(bz + TF_GRID_HALF);
-    if ((gx | gy | gz) < (unsigned)TF_GRID_DIM) return s.grid[tf_grid_cell(bx, by, bz)];
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
+// the hash walk for a block outside the block grid (rare: the grid spans +-128 blocks)
+__device__ __forceinline__ int2 blk_walk(const SceneView& s, int bx, int by, int bz)
+{
     int hi = tf_hash_index(bx, by, bz, s.mask);
     while (true) {
         const TfHashEntry e = s.hash[hi];
@@ -49,10 +55,47 @@ __device__ __forceinline__ int2 blk_find(const SceneView& s, int bx, int by, int
     }
 }
 
-// raw Voxel_s word (sdf = low 16 bits, w = bits 16-23); unallocated -> Voxel_s() = (32767, 0)
+// Lookups of the 2x2x2 block set {X[i]} x {Y[j]} x {Z[k]} (corner c = i + 2j + 4k), returning
+// (hash entry index, VBA voxel offset) per corner, or (-1,-1) when findVoxel fails.  Every grid
+// load is issued unconditionally (a cell outside the grid loads cell 0 and is replaced by the
+// hash walk afterwards), so the eight loads are in flight together: one memory round trip.
+__device__ __forceinline__ void blk_find8(const SceneView& s, const int (&X)[2], const int (&Y)[2], const int (&Z)[2],
+                                          int (&hidx)[8], int (&voff)[8])
+{
+    unsigned gx[2], gy[2], gz[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        gx[i] = (unsigned)(X[i] + TF_GRID_HALF); gy[i] = (unsigned)(Y[i] + TF_GRID_HALF); gz[i] = (unsigned)(Z[i] + TF_GRID_HALF);
+    }
+    bool in[8];
+    int2 g[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const unsigned x = gx[c & 1], y = gy[(c >> 1) & 1], z = gz[c >> 2];
+        in[c] = (x | y | z) < (unsigned)TF_GRID_DIM;
+        const unsigned cell = (z << (2 * TF_GRID_LOG)) | (y << TF_GRID_LOG) | x;
+        g[c] = ld_off<int2>(s.grid, (in[c] ? cell : 0u) * 8u);
+    }
+    bool all_in = true;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) all_in = all_in && in[c];
+    if (!all_in) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            if (!in[c]) g[c] = blk_walk(s, X[c & 1], Y[(c >> 1) & 1], Z[c >> 2]);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { hidx[c] = g[c].x; voff[c] = g[c].y; }
+}
+
+// raw Voxel_s word (sdf = low 16 bits, w = bits 16-23); unallocated -> Voxel_s() = (32767, 0).
+// The load is unconditional (voxel 0 when the block is missing) so neighbouring reads batch;
+// VBA byte offsets fit 32 bits (<= 2^21 blocks x 2 KiB).
 __device__ __forceinline__ unsigned vox_raw(const SceneView& s, int voff, int x, int y, int z)
 {
-    return voff >= 0 ? reinterpret_cast<const unsigned*>(s.vba)[voff + vlin(x, y, z)] : 0x7fffu;
+    const unsigned off = (unsigned)((voff + vlin(x, y, z)) & ~(voff >> 31));   // voxel 0 when voff < 0 (no branch)
+    const unsigned r = ld_off<unsigned>(s.vba, off * 4u);
+    return voff >= 0 ? r : 0x7fffu;
 }
 __device__ __forceinline__ float raw_sdf(unsigned r) { return (float)(short)(r & 0xffffu); }
 __device__ __forceinline__ float raw_w(unsigned r) { return (float)((r >> 16) & 0xffu); }
@@ -90,11 +133,8 @@ __device__ __forceinline__ void corners_fetch(const SceneView& s, const float* p
     q.cx = pt[0] - ffx; q.cy = pt[1] - ffy; q.cz = pt[2] - ffz;
     q.bx = vblk(q.fx); q.by = vblk(q.fy); q.bz = vblk(q.fz);
     q.sx = vblk(q.fx + 1) - q.bx; q.sy = vblk(q.fy + 1) - q.by; q.sz = vblk(q.fz + 1) - q.bz;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const int2 g = blk_find(s, q.bx + ((c & 1) & q.sx), q.by + (((c >> 1) & 1) & q.sy), q.bz + ((c >> 2) & q.sz));
-        q.hidx[c] = g.x; q.voff[c] = g.y;
-    }
+    const int X[2] = { q.bx, q.bx + q.sx }, Y[2] = { q.by, q.by + q.sy }, Z[2] = { q.bz, q.bz + q.sz };
+    blk_find8(s, X, Y, Z, q.hidx, q.voff);
 #pragma unroll
     for (int c = 0; c < 8; ++c)
         q.raw[c] = vox_raw(s, q.voff[c], q.fx + (c & 1), q.fy + ((c >> 1) & 1), q.fz + (c >> 2));
@@ -246,10 +286,9 @@ __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
     float nx = 1.0f - cx, ny = 1.0f - cy, nz = 1.0f - cz;
     const int bx = vblk(px - 1), by = vblk(py - 1), bz = vblk(pz - 1);
     const int sx = vblk(px + 2) - bx, sy = vblk(py + 2) - by, sz = vblk(pz + 2) - bz;
-    int voff[8];
-#pragma unroll
-    for (int o = 0; o < 8; ++o)
-        voff[o] = blk_find(s, bx + ((o & 1) & sx), by + (((o >> 1) & 1) & sy), bz + ((o >> 2) & sz)).y;
+    int voff[8], hidx[8];
+    const int X[2] = { bx, bx + sx }, Y[2] = { by, by + sy }, Z[2] = { bz, bz + sz };
+    blk_find8(s, X, Y, Z, hidx, voff);
     int ox[4], oy[4], oz[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
