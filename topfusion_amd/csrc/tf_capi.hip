@@ -370,8 +370,7 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1));                           // frame begin + topfu.cpp:242-243 (tracking only)
     // the previous frame's renderImage (render stream) must be done before the scene changes
     TF_CHECK(join_render(c));
-    TF_CHECK(tfk_render_prologue(c));
-    STAGE(TF_STAGE_ALLOC, tfk_alloc(c));                             // topfu.cpp:202 / 281
+    STAGE(TF_STAGE_ALLOC, tfk_alloc(c, 1));                          // topfu.cpp:202 / 281 (+ renderImage snapshot)
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1));                  // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
     // renderImage (raycast + grey, topfu.cpp:284-285) on the render stream, behind integration;
     // it overlaps CreateExpectedDepths / CreateICPMaps and the next frame's preprocessing + ICP,

@@ -64,7 +64,7 @@ struct TfDevState {
     int pad2_[5];
     // renderImage of the frame runs on the context's render stream, overlapping the rest of
     // the frame and the next frame's preprocessing/ICP; it reads only this snapshot (taken on
-    // the main stream once the previous render has finished: k_render_prologue)
+    // the main stream once the previous render has finished: render_snapshot)
     float M_render[16];      // M_ray of the frame being rendered
     int render_go;           // the frame took the tracking path (mode 1, ICP ok)
     int pad3_[3];
@@ -171,6 +171,24 @@ __device__ __forceinline__ float tf_wave_tree64(float b)
     return b;
 }
 
+// Main stream, after the previous frame's renderImage has finished and this frame's ICP has
+// set the pose (folded into the allocation pass's first kernel): snapshot what the frame's
+// renderImage reads and later stages of this frame or the next overwrite -- the raycast
+// matrix, the go flag, and the /8 region castRay reads of the range image
+// (range[x/8 + (y/8)*W], VisualisationEngine_Shared.hpp:104-106) that CreateExpectedDepths
+// rewrites before the render runs.
+static __device__ __forceinline__ void render_snapshot(TfDevState* st, const float2* range, float2* snap, int W, int H)
+{
+    if (blockIdx.x == 0 && threadIdx.x < 16) st->M_render[threadIdx.x] = st->M_ray[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->render_go = (st->mode != 0 && !st->abort) ? 1 : 0;
+    if (st->mode == 0 || st->abort) return;
+    const int rc = (W - 1) / TF_SUBSAMPLE + 1, rr = (H - 1) / TF_SUBSAMPLE + 1;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < rc * rr; i += gridDim.x * blockDim.x) {
+        const int y = i / rc, x = i - y * rc;
+        snap[x + y * W] = range[x + y * W];
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // host-side context
 // ---------------------------------------------------------------------------------------
@@ -254,13 +272,12 @@ hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / ray
 hipError_t tfk_reset_scene(tf_ctx* c);
 hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot);   // frame end + ResetScene if ICP failed
 hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a hash upload)
-hipError_t tfk_alloc(tf_ctx* c);
+hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0);   // snapshot: + the frame's renderImage snapshot
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_grey(tf_ctx* c);
 hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);
 hipError_t tfk_raycast_pair(tf_ctx* c);   // CreateICPMaps raycast + renderImage, one launch (frame path)    // renderImage raycast + grey, fused (frame path, render stream)
-hipError_t tfk_render_prologue(tf_ctx* c); // snapshot for the frame's renderImage (main stream)
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_expected_depths(tf_ctx* c);
 hipError_t tfk_frame0_matrices(tf_ctx* c);

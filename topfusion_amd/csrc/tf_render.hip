@@ -350,7 +350,7 @@ template <int MODE>
 __device__ __forceinline__ void raycast_tile(const RayArgs& a, const TfDevState* __restrict__ st, int bid,
                                              int tiles_x, int n_tiles)
 {
-    // the frame's renderImage (MODE 2) reads the snapshot k_render_prologue took
+    // the frame's renderImage (MODE 2) reads the snapshot render_snapshot took (tf_internal.h)
     if (MODE == 2 ? !st->render_go : (st->abort || st->mode == 0)) return;   // ICP failed, or frame 0
     const int tile = xcd_tile(bid, n_tiles);            // grid padded to a multiple of 8
     if (tile < 0) return;
@@ -446,30 +446,6 @@ hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm)
     return launch_ray(c, a, 2, strm);
 }
 
-// Main stream, after the previous frame's renderImage has finished and this frame's ICP has
-// set the pose: snapshot what renderImage reads and later stages of this frame or the next
-// overwrite -- the raycast matrix, the go flag, and the ÷8 region castRay reads of the range
-// image (range[x/8 + (y/8)*W], VisualisationEngine_Shared.hpp:104-106) that
-// CreateExpectedDepths rewrites before the render may have run.
-__global__ void __launch_bounds__(256)
-k_render_prologue(TfDevState* __restrict__ st, const float2* __restrict__ range, float2* __restrict__ snap, int W, int H)
-{
-    if (threadIdx.x < 16) st->M_render[threadIdx.x] = st->M_ray[threadIdx.x];
-    if (threadIdx.x == 0) st->render_go = (st->mode != 0 && !st->abort) ? 1 : 0;
-    if (st->mode == 0 || st->abort) return;
-    const int rc = (W - 1) / TF_SUBSAMPLE + 1, rr = (H - 1) / TF_SUBSAMPLE + 1;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < rc * rr; i += gridDim.x * 256) {
-        const int y = i / rc, x = i - y * rc;
-        snap[x + y * W] = range[x + y * W];
-    }
-}
-
-hipError_t tfk_render_prologue(tf_ctx* c)
-{
-    hipLaunchKernelGGL(k_render_prologue, dim3(8), dim3(256), 0, c->stream, c->st, (const float2*)c->range,
-                       (float2*)c->range_render, c->W, c->H);
-    return hipGetLastError();
-}
 
 
 __global__ void __launch_bounds__(256)

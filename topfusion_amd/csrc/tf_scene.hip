@@ -104,6 +104,41 @@ hipError_t tfk_grid_rebuild(tf_ctx* c)
 }
 
 // ---------------------------------------------------------------------------------------
+// checkBlockVisibility<false> (SceneReconstructionEngine.hpp:300-375)
+// ---------------------------------------------------------------------------------------
+struct VisArgs {
+    float fx, fy, cx, cy;
+    float factor;                 // (float)SDF_BLOCK_SIZE * voxelSize
+    int W, H;
+    int n_total, cap;
+};
+
+__device__ __forceinline__ bool vis_point(const float* M, const float* pt, const VisArgs& v)
+{
+    float b[4];
+    tf_m4v(M, pt[0], pt[1], pt[2], pt[3], b);
+    if (b[2] < 1e-10f) return false;
+    float bx = v.fx * b[0] / b[2] + v.cx;
+    float by = v.fy * b[1] / b[2] + v.cy;
+    return bx >= 0 && bx < (float)v.W && by >= 0 && by < (float)v.H;
+}
+
+__device__ bool vis_block(const TfHashEntry& e, const float* M, const VisArgs& v)
+{
+    const float f = v.factor;
+    float pt[4] = { (float)e.x * f, (float)e.y * f, (float)e.z * f, 1.0f };
+    if (vis_point(M, pt, v)) return true;
+    pt[2] += f; if (vis_point(M, pt, v)) return true;                     // 0 0 1
+    pt[1] += f; if (vis_point(M, pt, v)) return true;                     // 0 1 1
+    pt[0] += f; if (vis_point(M, pt, v)) return true;                     // 1 1 1
+    pt[2] -= f; if (vis_point(M, pt, v)) return true;                     // 1 1 0
+    pt[1] -= f; if (vis_point(M, pt, v)) return true;                     // 1 0 0
+    pt[0] -= f; pt[1] += f; if (vis_point(M, pt, v)) return true;         // 0 1 0
+    pt[0] += f; pt[1] -= f; pt[2] += f; if (vis_point(M, pt, v)) return true;  // 1 0 1
+    return false;
+}
+
+// ---------------------------------------------------------------------------------------
 // buildHashAllocAndVisibleTypePP (SceneReconstructionEngine.hpp:206-298)
 // ---------------------------------------------------------------------------------------
 struct AllocArgs {
@@ -144,18 +179,13 @@ __device__ __forceinline__ bool alloc_segment(const AllocArgs& a, const float* i
     return true;
 }
 
-__global__ void __launch_bounds__(256)
-k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
-                 unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType, int* __restrict__ winnerKey)
+// the hash probe of one step whose block the grid does not hold: found (outside the grid) ->
+// visible type; otherwise an allocation request in the bucket (1) or at the chain end (2)
+__device__ __forceinline__ void alloc_probe(const AllocArgs& a, const TfHashEntry* __restrict__ hash,
+                                            unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType,
+                                            int* __restrict__ winnerKey, int bx, int by, int bz, int key)
 {
-    if (st->abort) return;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.H) return;
-    float point[3], dir[3]; int noSteps;
-    if (!alloc_segment(a, st->invM_alloc, x, y, point, dir, &noSteps)) return;
-    const int key0 = (y * a.W + x) * 64;
-    for (int i = 0; i < noSteps; i++) {
-        int bx = (short)floorf(point[0]), by = (short)floorf(point[1]), bz = (short)floorf(point[2]);
+    {
         int hashIdx = tf_hash_index(bx, by, bz, a.mask);
         TfHashEntry e = hash[hashIdx];
         bool found = false;
@@ -180,10 +210,44 @@ k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEnt
             if (!found) {
                 allocType[hashIdx] = isExcess ? 2 : 1;
                 if (!isExcess) visType[hashIdx] = 1;
-                atomicMax(&winnerKey[hashIdx], key0 + i);   // raster-order last writer
+                atomicMax(&winnerKey[hashIdx], key);   // raster-order last writer
             }
         }
-        point[0] += dir[0]; point[1] += dir[1]; point[2] += dir[2];
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+                 unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType, int* __restrict__ winnerKey)
+{
+    if (st->abort) return;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.W || y >= a.H) return;
+    float point[3], dir[3]; int noSteps;
+    if (!alloc_segment(a, st->invM_alloc, x, y, point, dir, &noSteps)) return;
+    const int key0 = (y * a.W + x) * 64;
+    // Steps in batches of 8: the block grid answers "already allocated" for every step with one
+    // batch of independent loads (the grid mirrors the hash exactly, tf_internal.h); only the
+    // steps whose block is not in the grid walk the hash (bucket / excess chain) to place their
+    // allocation request.  Same outcomes, same raster-order keys as the serial loop.
+    for (int i0 = 0; i0 < noSteps; i0 += 8) {
+        int sbx[8], sby[8], sbz[8];
+        int2 g[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            sbx[j] = (short)floorf(point[0]); sby[j] = (short)floorf(point[1]); sbz[j] = (short)floorf(point[2]);
+            const bool in = i0 + j < noSteps && tf_grid_in(sbx[j], sby[j], sbz[j]);
+            g[j] = a.grid[in ? tf_grid_cell(sbx[j], sby[j], sbz[j]) : 0];
+            if (!in) g[j] = make_int2(-1, -1);
+            if (i0 + j < noSteps) { point[0] += dir[0]; point[1] += dir[1]; point[2] += dir[2]; }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = i0 + j;
+            if (i >= noSteps) break;
+            if (g[j].x >= 0) { visType[g[j].x] = 1; continue; }     // found (ptr >= 0; ptr == -1 never exists)
+            alloc_probe(a, hash, allocType, visType, winnerKey, sbx[j], sby[j], sbz[j], key0 + i);
+        }
     }
 }
 
@@ -198,14 +262,27 @@ __device__ __forceinline__ void alloc_block_from_key(const AllocArgs& a, const f
     pos[0] = (short)floorf(point[0]); pos[1] = (short)floorf(point[1]); pos[2] = (short)floorf(point[2]);
 }
 
-// setToType3 (SceneReconstructionEngine_host.cu:343-348) over the previous visible list
-__global__ void k_set_type3(const TfDevState* __restrict__ st, const int* __restrict__ visibleIds,
-                            unsigned char* __restrict__ visType)
+// setToType3 (SceneReconstructionEngine_host.cu:343-348) over the previous visible list, with
+// the checkBlockVisibility<false> test buildVisibleList applies to entries still of type 3
+// (:449-476) evaluated here already: it depends only on the entry's block position (which
+// the allocation pass does not change for existing entries) and on this frame's pose.  Type 4
+// = "type 3, not visible"; the allocation pass overwrites 3/4 exactly as it overwrites 3, and
+// k_vis_count turns the 4s that survive into 0.  One entry per thread instead of a dependent
+// hash load inside the N_tot scan.
+// It also takes the frame's renderImage snapshot (render_snapshot, tf_internal.h) first.
+__global__ void __launch_bounds__(256)
+k_set_type3(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+            const int* __restrict__ visibleIds, unsigned char* __restrict__ visType,
+            const float2* __restrict__ range, float2* __restrict__ snap)
 {
+    if (snap) render_snapshot(st, range, snap, v.W, v.H);
     if (st->abort) return;
     const int n = st->noVisibleEntries;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        visType[visibleIds[i]] = 3;
+    const float* M = st->M_alloc;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int id = visibleIds[i];
+        visType[id] = vis_block(hash[id], M, v) ? 3 : 4;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -382,38 +459,6 @@ __global__ void k_alloc_finish(AllocArgs a, TfDevState* __restrict__ st, unsigne
 // buildVisibleList_device<false> (SceneReconstructionEngine_host.cu:434-479) with
 // checkBlockVisibility<false> (SceneReconstructionEngine.hpp:300-375), ordered compaction
 // ---------------------------------------------------------------------------------------
-struct VisArgs {
-    float fx, fy, cx, cy;
-    float factor;                 // (float)SDF_BLOCK_SIZE * voxelSize
-    int W, H;
-    int n_total, cap;
-};
-
-__device__ __forceinline__ bool vis_point(const float* M, const float* pt, const VisArgs& v)
-{
-    float b[4];
-    tf_m4v(M, pt[0], pt[1], pt[2], pt[3], b);
-    if (b[2] < 1e-10f) return false;
-    float bx = v.fx * b[0] / b[2] + v.cx;
-    float by = v.fy * b[1] / b[2] + v.cy;
-    return bx >= 0 && bx < (float)v.W && by >= 0 && by < (float)v.H;
-}
-
-__device__ bool vis_block(const TfHashEntry& e, const float* M, const VisArgs& v)
-{
-    const float f = v.factor;
-    float pt[4] = { (float)e.x * f, (float)e.y * f, (float)e.z * f, 1.0f };
-    if (vis_point(M, pt, v)) return true;
-    pt[2] += f; if (vis_point(M, pt, v)) return true;                     // 0 0 1
-    pt[1] += f; if (vis_point(M, pt, v)) return true;                     // 0 1 1
-    pt[0] += f; if (vis_point(M, pt, v)) return true;                     // 1 1 1
-    pt[2] -= f; if (vis_point(M, pt, v)) return true;                     // 1 1 0
-    pt[1] -= f; if (vis_point(M, pt, v)) return true;                     // 1 0 0
-    pt[0] -= f; pt[1] += f; if (vis_point(M, pt, v)) return true;         // 0 1 0
-    pt[0] += f; pt[1] -= f; pt[2] += f; if (vis_point(M, pt, v)) return true;  // 1 0 1
-    return false;
-}
-
 __global__ void __launch_bounds__(256)
 k_vis_count(VisArgs v, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
             unsigned char* __restrict__ visType, int* __restrict__ counts)
@@ -427,12 +472,10 @@ k_vis_count(VisArgs v, const TfDevState* __restrict__ st, const TfHashEntry* __r
         bool dirty = false;
         for (int i = 0; i < 16; ++i) {
             unsigned t = byte16(lo, hi, i);
-            if (t == 3) {
-                if (!vis_block(hash[base + i], st->M_alloc, v)) {
-                    if (i < 8) lo &= ~(0xffull << (8 * i)); else hi &= ~(0xffull << (8 * (i - 8)));
-                    t = 0;
-                    dirty = true;
-                }
+            if (t == 4) {              // type 3 that failed checkBlockVisibility (k_set_type3)
+                if (i < 8) lo &= ~(0xffull << (8 * i)); else hi &= ~(0xffull << (8 * (i - 8)));
+                t = 0;
+                dirty = true;
             }
             cnt += t > 0;
         }
@@ -489,10 +532,15 @@ static AllocArgs make_alloc_args(tf_ctx* c)
 
 // AllocateSceneFromDepth (SceneReconstructionEngine_host.cu:75-195) with the matrices
 // already in st->M_alloc / st->invM_alloc
-hipError_t tfk_alloc(tf_ctx* c)
+hipError_t tfk_alloc(tf_ctx* c, int snapshot)
 {
     AllocArgs a = make_alloc_args(c);
-    hipLaunchKernelGGL(k_set_type3, dim3(256), dim3(256), 0, c->stream, c->st, c->visibleIds, c->visType);
+    VisArgs v;
+    v.fx = c->p.fx; v.fy = c->p.fy; v.cx = c->p.cx; v.cy = c->p.cy;
+    v.factor = (float)TF_BLK * c->p.voxelSize;
+    v.W = c->W; v.H = c->H; v.n_total = c->n_total; v.cap = c->p.vis_capacity;
+    hipLaunchKernelGGL(k_set_type3, dim3(256), dim3(256), 0, c->stream, v, c->st, c->hash, c->visibleIds, c->visType,
+                       (const float2*)c->range, snapshot ? (float2*)c->range_render : nullptr);
     hipLaunchKernelGGL(k_alloc_requests, dim3((c->W + 15) / 16, (c->H + 15) / 16), dim3(256), 0, c->stream,
                        a, c->st, c->hash, c->allocType, c->visType, c->winnerKey);
     hipLaunchKernelGGL(k_alloc_count, dim3(c->alloc_chunks), dim3(256), 0, c->stream, c->st, c->allocType, c->n_total,
@@ -502,10 +550,6 @@ hipError_t tfk_alloc(tf_ctx* c)
                        c->requestList, c->n_total);
     hipLaunchKernelGGL(k_alloc_finish, dim3(1), dim3(1), 0, c->stream, a, c->st, c->allocType, c->winnerKey, c->hash,
                        c->visType, c->allocList, c->excessList, c->requestList);
-    VisArgs v;
-    v.fx = c->p.fx; v.fy = c->p.fy; v.cx = c->p.cx; v.cy = c->p.cy;
-    v.factor = (float)TF_BLK * c->p.voxelSize;
-    v.W = c->W; v.H = c->H; v.n_total = c->n_total; v.cap = c->p.vis_capacity;
     hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
                        c->visCounts);
     hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
