@@ -28,8 +28,13 @@ PEAK_HBM_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-leve
 
 # stages that are one kernel launch per frame (persistent ICP), and that kernel's name
 KERNEL_OF_STAGE = {"icp": "k_icp_frame", "raycast_render": "k_raycast<2> (raycast + grey)",
-                   "raycast_icp": "k_raycast<1>", "integrate": "k_integrate"}
+                   "raycast_icp": "k_raycast_pair (CreateICPMaps castRay<true> + renderImage castRay + grey)",
+                   "integrate": "k_integrate"}
 SINGLE_KERNEL_STAGES = tuple(KERNEL_OF_STAGE)
+# renderImage schedule (tf_capi.hip, TFUSION_RENDER_MODE): 3 (default) = fused with CreateICPMaps' raycast
+RENDER_FUSED = os.environ.get("TFUSION_RENDER_MODE", "3") == "3"
+if not RENDER_FUSED:
+    KERNEL_OF_STAGE["raycast_icp"] = "k_raycast<1>"
 
 # SURVEY.md §8d configs.  C3 raises the capacities past the reference's (2^21 blocks = 4 GiB of
 # voxels, 2^22 buckets, 2^20 excess) -- sized for 288 GB of HBM, not for the reference's GPU.
@@ -62,6 +67,10 @@ def parse():
 def stage_bytes(stage, p, nvis, W, H):
     """Algorithmic HBM bytes of ONE launch of a stage."""
     if stage == "raycast_icp":
+        if RENDER_FUSED:
+            # default schedule (render mode 3): both raycasts in one launch -- float4 ray image +
+            # uchar4 grey image out, every visible block read once per raycast
+            return W * H * (16 + 4) + 2 * nvis * (2048 + 16)
         return W * H * 16 + nvis * (2048 + 16)          # ray output float4 + every visible block once
     if stage == "raycast_render":
         return W * H * 4 + nvis * (2048 + 16)           # fused raycast + grey: uchar4 out + blocks once

@@ -9,7 +9,7 @@ The output holds one entry per bench config (C2, C3); an existing file is update
 import csv, glob, json, os, sys
 from collections import defaultdict
 
-STAGE_OF = [("k_icp_frame", "icp"), ("k_raycast<2>", "raycast_render"), ("k_raycast<1>", "raycast_icp"),
+STAGE_OF = [("k_icp_frame", "icp"), ("k_raycast<2>", "raycast_render"), ("k_raycast_pair", "raycast_icp"),
             ("k_integrate", "integrate")]
 
 

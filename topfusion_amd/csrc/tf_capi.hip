@@ -77,6 +77,7 @@ static bool params_valid(const tf_params* p)
     if (p->cols <= 0 || p->rows <= 0 || (p->cols % 4) || (p->rows % 4)) return false;
     if (p->n_buckets <= 0 || (p->n_buckets & (p->n_buckets - 1))) return false;
     if (p->n_excess <= 0 || p->n_blocks <= 0 || p->vis_capacity <= 0 || p->max_render_blocks <= 0) return false;
+    if (p->n_blocks > (1 << 21)) return false;        // VBA byte offsets are 32-bit (tf_render.hip vox_raw)
     if ((p->n_buckets + p->n_excess) % 16) return false;
     if (p->bilateral_kernel_size < 1 || p->bilateral_kernel_size > 7) return false;
     if (p->voxelSize <= 0 || p->mu <= 0) return false;
