@@ -39,21 +39,25 @@ if not RENDER_FUSED:
 # SURVEY.md §8d configs.  C3 raises the capacities past the reference's (2^21 blocks = 4 GiB of
 # voxels, 2^22 buckets, 2^20 excess) -- sized for 288 GB of HBM, not for the reference's GPU.
 CONFIGS = {
-    "C2": dict(cols=640, rows=480, voxel=0.005, capacity={}),
+    "C2": dict(cols=640, rows=480, voxel=0.005, capacity={}, walk=False, steps=200),
     "C3": dict(cols=1280, rows=960, voxel=0.002,
                capacity=dict(n_buckets=1 << 22, n_excess=1 << 20, n_blocks=1 << 21, vis_capacity=1 << 21,
-                             max_render_blocks=1 << 20)),
+                             max_render_blocks=1 << 20), walk=False, steps=200),
+    # C5 hash stress: 10 mm voxels, 50 k-frame random walk (seed 13 + rank, <= 1 cm / 0.5 deg per
+    # frame), reference capacities; frames rendered on the GPU (synth.render_depth_torch)
+    "C5": dict(cols=640, rows=480, voxel=0.01, capacity={}, walk=True, steps=50000),
 }
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=None, help="timed frames (default: 200; C5: 50000)")
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=["C2", "C3"], default="C2",
+    ap.add_argument("--config", choices=["C2", "C3", "C5"], default="C2",
                     help="C2: 640x480 orbit, 5 mm (BASELINE configs[1], the headline); "
-                         "C3: 1280x960, 2 mm, capacities beyond the reference's (configs[2])")
+                         "C3: 1280x960, 2 mm, capacities beyond the reference's (configs[2]); "
+                         "C5: 10 mm hash stress, 50 k-frame random walk (configs[4])")
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--voxel", type=float, default=None)
@@ -130,6 +134,8 @@ def main():
     from topfusion_amd import TopFu, default_params, synth
 
     cfg = CONFIGS[args.config]
+    if args.steps is None:
+        args.steps = cfg["steps"]
     W = args.cols or cfg["cols"]
     H = args.rows or cfg["rows"]
     if args.voxel is None:
@@ -138,8 +144,21 @@ def main():
     pkw = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=args.voxel, **cfg["capacity"])
     n_breakdown = 0 if args.no_profile else min(args.breakdown_frames, args.steps)
     n_frames = args.warmup + args.steps
-    frames = synth.orbit_sequence(n_frames, W, H, seed=7 + rank)
-    dev = torch.from_numpy(frames.view(np.int16)).to(f"cuda:{local_rank}")
+    if cfg["walk"]:
+        # C5: poses on the host, depth rendered on the GPU in batches; the CPU baseline's bounded
+        # sample is the same frames, downloaded
+        R, t = synth.random_walk_poses(n_frames, seed=13 + rank)
+        dev = torch.empty((n_frames, H, W), dtype=torch.int16, device=f"cuda:{local_rank}")
+        gen = torch.Generator(device=f"cuda:{local_rank}")
+        gen.manual_seed(13 + rank)
+        for b0 in range(0, n_frames, 128):
+            b1 = min(n_frames, b0 + 128)
+            dev[b0:b1] = synth.render_depth_torch(R[b0:b1], t[b0:b1], W, H, noise_mm=1.0, generator=gen,
+                                                  device=f"cuda:{local_rank}")
+        frames = dev[:min(n_frames, 64)].cpu().numpy().view(np.uint16)
+    else:
+        frames = synth.orbit_sequence(n_frames, W, H, seed=7 + rank)
+        dev = torch.from_numpy(frames.view(np.int16)).to(f"cuda:{local_rank}")
     frame_bytes = W * H * 2
     base = dev.data_ptr()
 
@@ -226,7 +245,7 @@ def main():
         if not args.no_cpu_baseline:
             v, n, dt = cpu_baseline(frames, pkw, args.cpu_seconds)
             cpu = {"value": round(v, 4), "unit": "frames/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle (serial C restatement) on frames 0..{n - 1} of the same C2 stream, "
+                   "sample": f"oracle (serial C restatement) on frames 0..{n - 1} of the same {args.config} stream, "
                              f"{W}x{H}, {dt:.1f} s, 1 thread, host CPU of the GPU box"}
         out = {
             "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame",
@@ -241,7 +260,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"{args.config} orbit, {W}x{H}, {args.voxel * 1000:g} mm voxels, 8^3 blocks, "
+            "config": {"workload": f"{args.config} {'random walk' if cfg['walk'] else 'orbit'}, {W}x{H}, "
+                                   f"{args.voxel * 1000:g} mm voxels, 8^3 blocks, "
                                    "3-level ICP (10/5/4) + alloc + integrate + renderImage + expected depths + "
                                    "ICP-map raycast; one independent stream per GPU",
                        "cols": W, "rows": H, "voxel_m": args.voxel, "parallelism": f"replicas{world}",
@@ -253,6 +273,7 @@ def main():
             "frames_ok": int(ok.sum()), "resets": int(st["n_resets"] - resets_before),
             "ok_frames_per_sec": round(int(ok.sum()) * (total_frames / args.steps) / elapsed_max, 2),
             "visible_blocks_last": st["noVisibleEntries"],
+            "allocated_blocks_last": int(tf.params().n_blocks - 1 - st["lastFreeBlockId"]),
             "roofline": roof,
             "roofline_stages": roof_all,
             "icp_schedule": "persistent" if tf.icp_persistent() else "per_iteration",

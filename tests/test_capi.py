@@ -97,3 +97,22 @@ def test_product_does_not_import_oracle():
                 src = open(os.path.join(dp, f), errors="ignore").read()
                 bad = ("import oracle", "from oracle", "tf_oracle.h", "liboracle", "tfo_")
                 assert not any(b in src for b in bad), f
+
+
+def test_random_walk_synth():
+    """C5 trajectory: deterministic, steps bounded by 1 cm / 0.5 deg, camera inside the room box;
+    the GPU-batch renderer agrees with the host renderer bit for bit without noise."""
+    import numpy as np
+    from topfusion_amd import synth
+    R, t = synth.random_walk_poses(400, seed=13)
+    R2, t2 = synth.random_walk_poses(400, seed=13)
+    assert np.array_equal(R, R2) and np.array_equal(t, t2)
+    assert np.all(t >= synth.ROOM_LO - 1e-12) and np.all(t <= synth.ROOM_HI + 1e-12)
+    step = np.linalg.norm(np.diff(t, axis=0), axis=1)
+    assert step.max() <= 0.01 + 1e-12
+    rel = np.einsum("nij,nkj->nik", R[1:], R[:-1])                  # R_{k+1} R_k^T
+    ang = np.degrees(np.arccos(np.clip((np.trace(rel, axis1=1, axis2=2) - 1) / 2, -1, 1)))
+    assert ang.max() <= 0.5 + 1e-6
+    host = synth.random_walk_sequence(2, 96, 72, seed=13, noise_mm=0.0)
+    dev = synth.render_depth_torch(R[:2], t[:2], 96, 72, noise_mm=0.0, device="cpu").numpy().view(np.uint16)
+    assert np.array_equal(host, dev)

@@ -281,3 +281,22 @@ def test_batched_frames_overlap(oracle_mod, monkeypatch, render_mode):
     assert_bit_exact("batched final raycast", g.raycast_result(), o.raycast_result())
     g.close()
     dev.free()
+
+
+def test_c5_random_walk_10mm(oracle_mod):
+    """C5 geometry: 10 mm voxels (noSteps flips 1 <-> 2 at this size), the seed-13
+    random walk (<= 1 cm / 0.5 deg per frame); every frame identical to the oracle, including
+    the ICP-failure resets the reference's frame-mixing quirk produces away from the identity."""
+    cols, rows, n = 320, 240, 14
+    g, o = make_pair(oracle_mod, cols, rows, voxelSize=0.01)
+    seq = synth.random_walk_sequence(n, cols, rows, seed=13)
+    for k in range(n):
+        okg, oko = g(seq[k]), o(seq[k])
+        assert okg == oko, f"frame {k}: ok gpu {okg} oracle {oko}"
+        sg, so = g.last_stats, o.counters()
+        for key in ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries", "icp_iterations", "frame_counter",
+                    "n_resets"):
+            assert sg[key] == so[key], f"frame {k} {key}: gpu {sg[key]} oracle {so[key]}"
+        assert_bit_exact(f"frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
+    compare_scene(g, o, "C5 final")
+    assert_bit_exact("C5 final raycast", g.raycast_result(), o.raycast_result())

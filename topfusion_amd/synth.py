@@ -93,3 +93,79 @@ def orbit_sequence(n, cols=640, rows=480, seed=7, noise_mm=1.0, holes=0.0, deg_p
         R, t = orbit_pose(k, deg_per_frame)
         out[k] = render_depth(R, t, cols, rows, sphere=True, noise_mm=noise_mm, holes=holes, seed=seed * 100003 + k)
     return out
+
+
+# ----------------------------------------------------------------------------------------
+# C5: hash stress -- 10 mm voxels, random-walk trajectory (seed 13, steps
+# <= 1 cm / 0.5 deg).  The walk stays inside the room box (reflected at its faces) so every
+# ray hits a surface within the view frustum.
+# ----------------------------------------------------------------------------------------
+ROOM_LO = np.array([-0.55, -0.65, -0.35])     # camera-centre box inside the room (walls at
+ROOM_HI = np.array([0.85, 0.35, 0.8])         # x -0.8/1.1, y -0.9/0.6, z -0.6/1.8; sphere kept clear)
+
+
+def _axis_angle(axis, ang):
+    axis = axis / np.linalg.norm(axis)
+    K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * (K @ K)
+
+
+def random_walk_poses(n, seed=13, step_m=0.01, step_deg=0.5):
+    """Camera->world poses (R[n,3,3], t[n,3]) of the C5 random walk: frame 0 at the identity,
+    then per frame a translation of length <= step_m in a uniformly random direction and a
+    rotation of angle <= step_deg about a uniformly random axis (float64)."""
+    rng = np.random.default_rng(seed)
+    R = np.empty((n, 3, 3))
+    t = np.empty((n, 3))
+    Rc, tc = np.eye(3), np.zeros(3)
+    for k in range(n):
+        R[k], t[k] = Rc, tc
+        d = rng.normal(size=3)
+        tc = tc + d / np.linalg.norm(d) * step_m * rng.random()
+        tc = np.where(tc < ROOM_LO, 2 * ROOM_LO - tc, tc)          # reflect at the box faces
+        tc = np.where(tc > ROOM_HI, 2 * ROOM_HI - tc, tc)
+        Rc = _axis_angle(rng.normal(size=3), np.deg2rad(step_deg) * rng.random()) @ Rc
+    return R, t
+
+
+def random_walk_sequence(n, cols=640, rows=480, seed=13, noise_mm=1.0, step_m=0.01, step_deg=0.5):
+    """C5 frames on the host (numpy renderer, for the parity tests), uint16 (n, rows, cols)."""
+    R, t = random_walk_poses(n, seed, step_m, step_deg)
+    out = np.empty((n, rows, cols), np.uint16)
+    for k in range(n):
+        out[k] = render_depth(R[k], t[k], cols, rows, sphere=True, noise_mm=noise_mm, seed=seed * 100003 + k)
+    return out
+
+
+def render_depth_torch(R, t, cols=640, rows=480, noise_mm=1.0, generator=None, device="cuda"):
+    """The same analytic room + sphere as render_depth, for a batch of poses on a torch device
+    (float64; noise from torch's generator): the bench's way to make long sequences (C5's
+    50 k frames) without a host renderer in the loop.  Returns int16 (B, rows, cols) holding
+    the uint16 millimetre bits."""
+    import torch
+    fx, fy, cx, cy = intrinsics(cols, rows)
+    R = torch.as_tensor(R, dtype=torch.float64, device=device)
+    t = torch.as_tensor(t, dtype=torch.float64, device=device)
+    u = torch.arange(cols, dtype=torch.float64, device=device)
+    v = torch.arange(rows, dtype=torch.float64, device=device)
+    vv, uu = torch.meshgrid(v, u, indexing="ij")
+    dc = torch.stack([(uu - cx) / fx, (vv - cy) / fy, torch.ones_like(uu)], dim=-1)      # (H, W, 3)
+    dw = torch.einsum("hwk,bjk->bhwj", dc, R)                                           # (B, H, W, 3)
+    o = t[:, None, None, :]
+    best = torch.full(dw.shape[:3], float("inf"), dtype=torch.float64, device=device)
+    for ax, off in [(2, 1.8), (1, 0.6), (0, -0.8), (0, 1.1), (1, -0.9), (2, -0.6)]:
+        tt = (off - o[..., ax]) / dw[..., ax]
+        best = torch.minimum(best, torch.where(tt > 1e-6, tt, torch.full_like(tt, float("inf"))))
+    c = torch.tensor([0.15, 0.25, 1.3], dtype=torch.float64, device=device)
+    oc = o - c
+    b = (dw * oc).sum(-1)
+    a = (dw * dw).sum(-1)
+    cc = (oc * oc).sum(-1) - 0.09
+    disc = b * b - a * cc
+    t0 = (-b - torch.sqrt(torch.clamp(disc, min=0))) / a
+    best = torch.minimum(best, torch.where((disc >= 0) & (t0 > 1e-6), t0, torch.full_like(t0, float("inf"))))
+    mm = best * 1000.0
+    if noise_mm > 0:
+        mm = mm + noise_mm * torch.randn(mm.shape, dtype=torch.float64, device=device, generator=generator)
+    mm = torch.where(torch.isfinite(mm), torch.round(mm), torch.zeros_like(mm))
+    return torch.clamp(mm, 0, 65535).to(torch.int32).to(torch.int16)
