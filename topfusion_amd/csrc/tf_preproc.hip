@@ -2,8 +2,8 @@
 //
 //   k_dists_bilateral : compute_dists_kernel + bilateral_kernel + truncate_depth_kernel
 //                       (imgproc.cu:10-89,263-290) fused; 32x8 tiles staged in LDS
-//   k_pyr_down        : pyramid_kernel (imgproc.cu:98-140)
-//   k_points_normals  : points_normals_kernel (imgproc.cu:214-254), all levels in one launch
+//   k_pyr_normals     : pyramid_kernel x2 (imgproc.cu:98-140) + points_normals_kernel x3
+//                       (imgproc.cu:214-254), all levels in one launch from LDS-staged tiles
 //
 // All three are HBM/L2-light elementwise-with-halo kernels; the bilateral filter is
 // VALU-bound (49 canonical exp per pixel).
@@ -62,49 +62,47 @@ k_dists_bilateral(const uint16_t* __restrict__ src, size_t pitch, int W, int H, 
     dst[y * W + x] = out;
 }
 
-// pyramid_kernel (imgproc.cu:98-127)
-__global__ void __launch_bounds__(256)
-k_pyr_down(const uint16_t* __restrict__ src, int W, int H, uint16_t* __restrict__ dst, int DW, int DH, float sigma3)
+// pyramid_kernel (imgproc.cu:98-127) on a source staged in LDS: destination pixel (x, y) of a
+// level whose source is sw x sh; the source sample (gx, gy) lives at lds[(gy - oy) * ld + gx - ox]
+template <typename T>
+__device__ __forceinline__ int pyr_pixel(const T* lds, int ld, int ox, int oy, int sw, int sh, int x, int y, float sigma3)
 {
-    const int x = blockIdx.x * 32 + (threadIdx.x & 31), y = blockIdx.y * 8 + (threadIdx.x >> 5);
-    if (x >= DW || y >= DH) return;
     const int D = 5;
-    int center = src[(2 * y) * W + 2 * x];
-    int txe = 2 * x - D / 2 + D; if (txe > W - 1) txe = W - 1;
-    int tye = 2 * y - D / 2 + D; if (tye > H - 1) tye = H - 1;
+    const int center = lds[(2 * y - oy) * ld + 2 * x - ox];
+    int txe = 2 * x - D / 2 + D; if (txe > sw - 1) txe = sw - 1;
+    int tye = 2 * y - D / 2 + D; if (tye > sh - 1) tye = sh - 1;
     int sum = 0, count = 0;
     for (int cy = (2 * y - D / 2 > 0 ? 2 * y - D / 2 : 0); cy < tye; ++cy)
         for (int cx = (2 * x - D / 2 > 0 ? 2 * x - D / 2 : 0); cx < txe; ++cx) {
-            int val = src[cy * W + cx];
+            const int val = lds[(cy - oy) * ld + cx - ox];
             if ((float)abs(val - center) < sigma3) { sum += val; ++count; }
         }
-    dst[y * DW + x] = (uint16_t)((count == 0) ? 0 : sum / count);
+    return (count == 0) ? 0 : sum / count;
 }
 
-struct PtsLevels {
-    const uint16_t* depth[TF_LEVELS];
+struct PyrArgs {
+    const uint16_t* d0;                 // level-0 depth (bilateral + truncation output)
+    uint16_t* d1; uint16_t* d2;         // levels 1, 2
     float4* pts[TF_LEVELS];
     float4* nrm[TF_LEVELS];
     int w[TF_LEVELS], h[TF_LEVELS];
     float fx[TF_LEVELS], fy[TF_LEVELS], cx[TF_LEVELS], cy[TF_LEVELS];
+    float sigma3;
 };
 
-// points_normals_kernel (imgproc.cu:214-243); blockIdx.z = pyramid level
-__global__ void __launch_bounds__(256)
-k_points_normals(PtsLevels L)
+// points_normals_kernel (imgproc.cu:214-243) for level pixel (x, y), depths from LDS
+template <typename T>
+__device__ __forceinline__ void pn_pixel(const T* lds, int ld, int ox, int oy, const PyrArgs& a, int l, int x, int y)
 {
-    const int l = blockIdx.z;
-    const int W = L.w[l], H = L.h[l];
-    const int x = blockIdx.x * 32 + (threadIdx.x & 31), y = blockIdx.y * 8 + (threadIdx.x >> 5);
-    if (x >= W || y >= H) return;
+    const int W = a.w[l], H = a.h[l];
     const float qnan = tf_qnan();
     float4 p = make_float4(qnan, qnan, qnan, qnan), n = p;
     if (x < W - 1 && y < H - 1) {
-        const uint16_t* d = L.depth[l];
-        const float fxi = 1.f / L.fx[l], fyi = 1.f / L.fy[l], cx = L.cx[l], cy = L.cy[l];
-        float z00 = (float)d[y * W + x] * 0.001f;
-        float z01 = (float)d[y * W + x + 1] * 0.001f;
-        float z10 = (float)d[(y + 1) * W + x] * 0.001f;
+        const float fxi = 1.f / a.fx[l], fyi = 1.f / a.fy[l], cx = a.cx[l], cy = a.cy[l];
+        const int i = (y - oy) * ld + x - ox;
+        float z00 = (float)lds[i] * 0.001f;
+        float z01 = (float)lds[i + 1] * 0.001f;
+        float z10 = (float)lds[i + ld] * 0.001f;
         if (z00 * z01 * z10 != 0) {
             tf3 v00 = mk3(z00 * ((float)x - cx) * fxi, z00 * ((float)y - cy) * fyi, z00);
             tf3 v01 = mk3(z01 * ((float)(x + 1) - cx) * fxi, z01 * ((float)y - cy) * fyi, z01);
@@ -114,8 +112,68 @@ k_points_normals(PtsLevels L)
             p = make_float4(v00.x, v00.y, v00.z, 1.0f);
         }
     }
-    L.pts[l][y * W + x] = p;
-    L.nrm[l][y * W + x] = n;
+    a.pts[l][y * W + x] = p;
+    a.nrm[l][y * W + x] = n;
+}
+
+// depthBuildPyramid x2 + computePointNormals x3 (imgproc.cpp:12-41) in one launch.  A workgroup
+// owns a 32x32 level-0 tile (16x16 at level 1, 8x8 at level 2) and stages what its outputs
+// read: level 0 over the tile +6/+7 pixels (the level-1 windows of the level-2 windows and the
+// normals' +1 neighbours), level 1 over its tile -2..+18, level 2 over its tile +1.  The few
+// level-1 values next to a tile are computed by both neighbours (identical arithmetic).
+#define PN_T0 32
+#define PN_R0 45                       // level-0 staging: [X0-6, X0+39)
+#define PN_R1 21                       // level-1 staging: [X1-2, X1+19)
+#define PN_R2 9                        // level-2 staging: [X2, X2+9)
+__global__ void __launch_bounds__(256)
+k_pyr_normals(PyrArgs a)
+{
+    __shared__ uint16_t s0[PN_R0 * PN_R0];
+    __shared__ int s1[PN_R1 * PN_R1];
+    __shared__ int s2[PN_R2 * PN_R2];
+    const int W0 = a.w[0], H0 = a.h[0], W1 = a.w[1], H1 = a.h[1], W2 = a.w[2], H2 = a.h[2];
+    const int X0 = blockIdx.x * PN_T0, Y0 = blockIdx.y * PN_T0;
+    const int X1 = X0 / 2, Y1 = Y0 / 2, X2 = X0 / 4, Y2 = Y0 / 4;
+    const int o0x = X0 - 6, o0y = Y0 - 6, o1x = X1 - 2, o1y = Y1 - 2;
+    for (int i = threadIdx.x; i < PN_R0 * PN_R0; i += 256) {
+        const int gy = o0y + i / PN_R0, gx = o0x + i % PN_R0;
+        s0[i] = (gx >= 0 && gx < W0 && gy >= 0 && gy < H0) ? a.d0[gy * W0 + gx] : 0;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < PN_R1 * PN_R1; i += 256) {
+        const int y = o1y + i / PN_R1, x = o1x + i % PN_R1;
+        int v = 0;
+        if (x >= 0 && x < W1 && y >= 0 && y < H1) {
+            v = pyr_pixel(s0, PN_R0, o0x, o0y, W0, H0, x, y, a.sigma3);
+            if (x >= X1 && x < X1 + 16 && y >= Y1 && y < Y1 + 16) a.d1[y * W1 + x] = (uint16_t)v;
+        }
+        s1[i] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < PN_R2 * PN_R2) {
+        const int y = Y2 + threadIdx.x / PN_R2, x = X2 + threadIdx.x % PN_R2;
+        int v = 0;
+        if (x < W2 && y < H2) {
+            v = pyr_pixel(s1, PN_R1, o1x, o1y, W1, H1, x, y, a.sigma3);
+            if (x < X2 + 8 && y < Y2 + 8) a.d2[y * W2 + x] = (uint16_t)v;
+        }
+        s2[threadIdx.x] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {                       // level 0: 32x32, four rows of 8 per thread
+        const int t = threadIdx.x + 256 * q;
+        const int x = X0 + (t & 31), y = Y0 + (t >> 5);
+        if (x < W0 && y < H0) pn_pixel(s0, PN_R0, o0x, o0y, a, 0, x, y);
+    }
+    {
+        const int x = X1 + (threadIdx.x & 15), y = Y1 + (threadIdx.x >> 4);
+        if (x < W1 && y < H1) pn_pixel(s1, PN_R1, o1x, o1y, a, 1, x, y);
+    }
+    if (threadIdx.x < 64) {
+        const int x = X2 + (threadIdx.x & 7), y = Y2 + (threadIdx.x >> 3);
+        if (x < W2 && y < H2) pn_pixel(s2, PN_R2, X2, Y2, a, 2, x, y);
+    }
 }
 
 static inline int div_up(int a, int b) { return (a + b - 1) / b; }
@@ -132,17 +190,15 @@ hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStr
     if (p.bilateral_kernel_size > 2 * HALO + 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_dists_bilateral, dim3(div_up(W, PRE_TX), div_up(H, PRE_TY)), dim3(256), 0, strm,
                        depth, pitch, W, H, p.bilateral_kernel_size, ss, sd, do_trunc, trunc_mm, c->dists, c->depth_pyr[0]);
-    float sigma3 = sigma_depth * 3.0f;                                               // imgproc.cu:138
-    for (int l = 1; l < TF_LEVELS; ++l)
-        hipLaunchKernelGGL(k_pyr_down, dim3(div_up(c->lw[l], 32), div_up(c->lh[l], 8)), dim3(256), 0, strm,
-                           c->depth_pyr[l - 1], c->lw[l - 1], c->lh[l - 1], c->depth_pyr[l], c->lw[l], c->lh[l], sigma3);
-    PtsLevels L;
+    PyrArgs a;
+    a.sigma3 = sigma_depth * 3.0f;                                                    // imgproc.cu:138
+    a.d0 = c->depth_pyr[0]; a.d1 = c->depth_pyr[1]; a.d2 = c->depth_pyr[2];
     for (int l = 0; l < TF_LEVELS; ++l) {
         int div = 1 << l;                                 // Intr::operator()(level), precomp.cpp:10-14
-        L.depth[l] = c->depth_pyr[l]; L.pts[l] = c->curr_pts[l]; L.nrm[l] = c->curr_nrm[l];
-        L.w[l] = c->lw[l]; L.h[l] = c->lh[l];
-        L.fx[l] = p.fx / (float)div; L.fy[l] = p.fy / (float)div; L.cx[l] = p.cx / (float)div; L.cy[l] = p.cy / (float)div;
+        a.pts[l] = c->curr_pts[l]; a.nrm[l] = c->curr_nrm[l];
+        a.w[l] = c->lw[l]; a.h[l] = c->lh[l];
+        a.fx[l] = p.fx / (float)div; a.fy[l] = p.fy / (float)div; a.cx[l] = p.cx / (float)div; a.cy[l] = p.cy / (float)div;
     }
-    hipLaunchKernelGGL(k_points_normals, dim3(div_up(W, 32), div_up(H, 8), TF_LEVELS), dim3(256), 0, strm, L);
+    hipLaunchKernelGGL(k_pyr_normals, dim3(div_up(W, PN_T0), div_up(H, PN_T0)), dim3(256), 0, strm, a);
     return hipGetLastError();
 }
