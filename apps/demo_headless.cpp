@@ -1,10 +1,17 @@
 // demo_headless.cpp -- apps/demo.cpp's loop (tfusion/apps/demo.cpp:27-168) without OpenCV /
-// OpenNI: synthetic depth frames (the C2 orbit of SURVEY.md §8d, rendered analytically on the
-// host) are uploaded with cuda::Depth::upload, fused by TopFu::operator(), and the grey
-// rendering is fetched with renderImage + download, exactly as the reference demo does.
+// OpenNI: depth frames are uploaded with cuda::Depth::upload, fused by TopFu::operator(), and
+// the grey rendering is fetched with renderImage + download, exactly as the reference demo
+// does.  Frames are either synthetic (the C2 orbit of SURVEY.md §8d, rendered analytically on
+// the host) or read from a numbered 16-bit PGM sequence like the reference demo's
+// "%04d.pgm" / "%04d.ppm" pairs (demo.cpp:91-97) through tfusion::io::FrameSequenceSource.
 //
 //   ./demo_headless [frames=100] [cols=640] [rows=480]
+//   ./demo_headless --pgm 'dir/%04d.pgm' [--ppm 'dir/%04d.ppm'] [max_frames]
+#include <tfusion/io.hpp>
 #include <tfusion/topfu.hpp>
+
+#include <cstring>
+#include <string>
 
 #include <cmath>
 #include <cstdio>
@@ -50,9 +57,25 @@ static void render_depth(const double R[9], const double t[3], int cols, int row
 
 int main(int argc, char** argv)
 {
-    const int frames = argc > 1 ? std::atoi(argv[1]) : 100;
-    const int cols = argc > 2 ? std::atoi(argv[2]) : 640;
-    const int rows = argc > 3 ? std::atoi(argv[3]) : 480;
+    std::string pgm, ppm;
+    std::vector<const char*> pos;
+    for (int i = 1; i < argc; ++i) {
+        if (!std::strcmp(argv[i], "--pgm") && i + 1 < argc) pgm = argv[++i];
+        else if (!std::strcmp(argv[i], "--ppm") && i + 1 < argc) ppm = argv[++i];
+        else pos.push_back(argv[i]);
+    }
+    int frames = pos.size() > 0 ? std::atoi(pos[0]) : (pgm.empty() ? 100 : 1 << 30);
+    int cols = pos.size() > 1 ? std::atoi(pos[1]) : 640;
+    int rows = pos.size() > 2 ? std::atoi(pos[2]) : 480;
+    io::FrameSequenceSource source(pgm, ppm);
+    std::vector<unsigned short> depth;
+    std::vector<unsigned char> image;
+    bool have_first = false;
+    if (!pgm.empty()) {                        // frame size from the first file
+        if (!source.grab(depth, image)) { std::fprintf(stderr, "no frame %s\n", pgm.c_str()); return 1; }
+        cols = source.cols(); rows = source.rows();
+        have_first = true;
+    }
 
     int device = 0;
     cuda::setDevice(device);
@@ -68,15 +91,21 @@ int main(int argc, char** argv)
 
     cuda::Depth depth_device;
     cuda::image4u view_device;
-    std::vector<unsigned short> depth;
     std::vector<unsigned char> view_host((size_t)cols * rows * 4);
     double time_ms = 0;
-    int n_ok = 0;
+    int n_ok = 0, n = 0;
     for (int i = 0; i < frames; ++i) {
-        const double ang = 0.25 * i * M_PI / 180.0, ca = std::cos(ang), sa = std::sin(ang);
-        const double R[9] = { ca, 0, sa, 0, 1, 0, -sa, 0, ca };
-        const double t[3] = { -sa * 1.2, 0.0, 1.2 - ca * 1.2 };     // orbit about a pivot 1.2 m ahead
-        render_depth(R, t, cols, rows, params.intr, depth);
+        if (!pgm.empty()) {
+            if (!have_first && !source.grab(depth, image)) break;         // end of the sequence
+            have_first = false;
+            if (source.cols() != cols || source.rows() != rows) { std::fprintf(stderr, "frame size changed\n"); return 1; }
+        } else {
+            const double ang = 0.25 * i * M_PI / 180.0, ca = std::cos(ang), sa = std::sin(ang);
+            const double R[9] = { ca, 0, sa, 0, 1, 0, -sa, 0, ca };
+            const double t[3] = { -sa * 1.2, 0.0, 1.2 - ca * 1.2 };     // orbit about a pivot 1.2 m ahead
+            render_depth(R, t, cols, rows, params.intr, depth);
+        }
+        ++n;
         depth_device.upload(depth.data(), (size_t)cols * 2, rows, cols);
         bool has_image;
         {
@@ -91,7 +120,7 @@ int main(int argc, char** argv)
     }
     const Affine3f pose = topfu->getCameraPose();
     const tf_stats st = topfu->stats();
-    std::printf("frames %d ok %d resets %d visible %d  pose t = (%.4f %.4f %.4f)\n", frames, n_ok, st.n_resets,
+    std::printf("frames %d ok %d resets %d visible %d  pose t = (%.4f %.4f %.4f)\n", n, n_ok, st.n_resets,
                 st.noVisibleEntries, pose.translation()[0], pose.translation()[1], pose.translation()[2]);
     long lit = 0;
     for (size_t k = 0; k < view_host.size(); k += 4) lit += view_host[k] > 0;

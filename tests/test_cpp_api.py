@@ -31,3 +31,21 @@ def test_demo_headless_runs():
     m = re.search(r"frames (\d+) ok (\d+) resets (\d+)", r.stdout)
     assert m and int(m.group(1)) == 40 and int(m.group(2)) >= 30, r.stdout
     assert "rendered pixels lit" in r.stdout
+
+
+@pytest.mark.gpu
+def test_demo_headless_pgm_sequence(tmp_path):
+    """The demo over a %04d.pgm / %04d.ppm sequence (the reference demo's input format,
+    apps/demo.cpp:91-97), read through tfusion::io::FrameSequenceSource."""
+    import numpy as np
+    from topfusion_amd import io, synth
+    seq = synth.orbit_sequence(12, 320, 240, seed=7)
+    for i, f in enumerate(seq):
+        io.write_pgm16(tmp_path / f"{i:04d}.pgm", f)
+        io.write_ppm(tmp_path / f"{i:04d}.ppm", np.zeros((240, 320, 3), np.uint8))
+    exe = _build()
+    r = subprocess.run([exe, "--pgm", str(tmp_path / "%04d.pgm"), "--ppm", str(tmp_path / "%04d.ppm")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = re.search(r"frames (\d+) ok (\d+) resets (\d+)", r.stdout)
+    assert m and int(m.group(1)) == 12 and int(m.group(2)) >= 8, r.stdout
