@@ -54,10 +54,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed frames (default: 200; C5: 50000)")
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=["C2", "C3", "C5"], default="C2",
+    ap.add_argument("--config", choices=["C2", "C3", "C3I", "C5"], default="C2",
                     help="C2: 640x480 orbit, 5 mm (BASELINE configs[1], the headline); "
                          "C3: 1280x960, 2 mm, capacities beyond the reference's (configs[2]); "
-                         "C5: 10 mm hash stress, 50 k-frame random walk (configs[4])")
+                         "C5: 10 mm hash stress, 50 k-frame random walk (configs[4]); "
+                         "C3I: IntegrateIntoScene alone over 2^21 active blocks at C3 geometry (HBM-bound)")
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--voxel", type=float, default=None)
@@ -119,8 +120,73 @@ def combine_ranks(elapsed, frames, device, world):
     return float(mx[0]), float(sm[0])
 
 
+def c3_integrate(args):
+    """C3I ("integrate over the active list is truly HBM-bound"): 2^21 active
+    voxel blocks (4 GiB of voxels) fill the 1280x960 frustum from 0.3 m on, every one in the
+    visible list; one IntegrateIntoScene pass per step against a wall at 1.5 m, all passes
+    back to back on the context stream, timed by HIP events.  Algorithmic bytes per pass:
+    Nvis x (4096 voxel R+W + 20 entry/id) + W x H x 4 (dists)."""
+    import torch
+    from topfusion_amd import TopFu, default_params, synth
+    from topfusion_amd import _lib as L
+    from topfusion_amd.topfu import HASH_DTYPE
+    torch.cuda.set_device(0)
+    cfg = CONFIGS["C3"]
+    W, H, vox = cfg["cols"], cfg["rows"], cfg["voxel"]
+    fx, fy, cx, cy = synth.intrinsics(W, H)
+    p = default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=vox, **cfg["capacity"])
+    nb = p.n_blocks
+    bs = 8 * vox
+    blocks, z = [], 0.3
+    while sum(len(b) for b in blocks) < nb:                # frustum layers of blocks, near to far
+        bz = int(np.floor(z / bs))
+        zc = (bz + 0.5) * bs
+        x0, x1 = int(np.floor((0 - cx) / fx * zc / bs)), int(np.ceil((W - cx) / fx * zc / bs))
+        y0, y1 = int(np.floor((0 - cy) / fy * zc / bs)), int(np.ceil((H - cy) / fy * zc / bs))
+        yy, xx = np.meshgrid(np.arange(y0, y1), np.arange(x0, x1), indexing="ij")
+        blocks.append(np.stack([xx.ravel(), yy.ravel(), np.full(xx.size, bz)], 1))
+        z = (bz + 1) * bs + 1e-6
+    pos = np.concatenate(blocks)[:nb]
+    tf = TopFu(p, device=0)
+    h = np.zeros(tf.nbytes(L.TF_BUF_HASH) // HASH_DTYPE.itemsize, HASH_DTYPE)
+    h["ptr"] = -2
+    h["x"][:nb], h["y"][:nb], h["z"][:nb] = pos[:, 0], pos[:, 1], pos[:, 2]
+    h["ptr"][:nb] = np.arange(nb)
+    tf.upload(L.TF_BUF_HASH, h)
+    ids = np.zeros(tf.nbytes(L.TF_BUF_VISIBLE_IDS) // 4, np.int32)
+    ids[:nb] = np.arange(nb)
+    tf.upload(L.TF_BUF_VISIBLE_IDS, ids)
+    tf.set_counters(-1, p.n_excess - 1, nb)
+    tf.stage_preprocess(np.full((H, W), 1500, np.uint16))   # dists of a wall at 1.5 m
+    I = np.eye(4, dtype=np.float32)[:3]
+    tf.time_stage("integrate", I, 2)                        # warm-up
+    ms = tf.time_stage("integrate", I, args.steps)
+    b = nb * (4096 + 20) + W * H * 4
+    ach = b / (ms * 1e-3) / 1e9
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        pmc = (json.load(open(pmc_path)).get("C3I", {}) or {}).get("integrate", {})
+    out = {"metric": f"IntegrateIntoScene passes/sec over {nb} active voxel blocks @{W}x{H}, {vox * 1000:g} mm",
+           "value": round(1000.0 / ms, 2), "unit": "passes/s", "n_gpus": 1, "steps": args.steps, "warmup": 2,
+           "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32", "data": "synthetic",
+           "config": {"workload": "C3I: k_integrate over 2^21 blocks filling the frustum from 0.3 m, wall at 1.5 m",
+                      "cols": W, "rows": H, "voxel_m": vox, "active_blocks": int(nb), "parallelism": "replicas1"},
+           "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": pmc.get("bytes_per_launch"),
+                        "kernel": "k_integrate", "algorithmic_bytes_per_launch": b, "avg_launch_ms": round(ms, 5),
+                        "timing": "HIP events around back-to-back launches on the context stream"}}
+    print(json.dumps(out))
+    tf.close()
+
+
 def main():
     args = parse()
+    if args.config == "C3I":
+        if args.steps is None:
+            args.steps = 20
+        return c3_integrate(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -192,6 +192,11 @@ tf_status tf_profile_reset(tf_ctx* ctx);
 /* ms[i] = accumulated milliseconds, counts[i] = frames measured, for i < n (n <= 9) */
 tf_status tf_profile_read(tf_ctx* ctx, double* ms, long long* counts, int n);
 tf_status tf_set_counters(tf_ctx* ctx, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries);
+/* Measurement: `iters` back-to-back launches of one stage's kernels on the context stream
+ * with the pose/matrices of tf_stage_* (stage = TF_STAGE_INTEGRATE or TF_STAGE_RAYCAST_ICP),
+ * timed by HIP events on that stream; *ms_per_iter = elapsed / iters.  The scene is updated
+ * by every launch exactly as by tf_stage_integrate / tf_stage_raycast. */
+tf_status tf_time_stage(tf_ctx* ctx, int stage, const float pose_rt[12], int iters, float* ms_per_iter);
 
 #ifdef __cplusplus
 }

@@ -673,6 +673,30 @@ extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
     return TF_OK;
 }
 
+extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12], int iters, float* ms_per_iter)
+{
+    if (!c || !pose_rt || iters <= 0 || !ms_per_iter) return TF_INVALID_ARG;
+    if (stage != TF_STAGE_INTEGRATE && stage != TF_STAGE_RAYCAST_ICP) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
+    tf_status s = set_pose_in(c, pose_rt, stage == TF_STAGE_INTEGRATE ? TF_POSE_ALLOC_NOINV : 0);
+    if (s != TF_OK) return s;
+    hipEvent_t e0, e1;
+    TF_CHECK(hipEventCreate(&e0));
+    TF_CHECK(hipEventCreate(&e1));
+    hipError_t e = hipEventRecord(e0, c->stream);
+    for (int i = 0; i < iters && e == hipSuccess; ++i)
+        e = stage == TF_STAGE_INTEGRATE ? tfk_integrate(c) : tfk_raycast(c, 1);
+    if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (e != hipSuccess) return tf_from_hip(e);
+    *ms_per_iter = ms / (float)iters;
+    return TF_OK;
+}
+
 extern "C" tf_status tf_stage_reset_scene(tf_ctx* c)
 {
     if (!c) return TF_INVALID_ARG;

@@ -243,7 +243,7 @@ __device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, 
             vmIndex = hit ? 1 : sel8(q.hidx, cu) + 1;
             k.bx = Ubx; k.by = Uby; k.bz = Ubz; k.voff = vu;
         }
-        sdfValue = raw_sdf((unsigned)sel8(reinterpret_cast<const int(&)[8]>(q.raw), cu)) / 32767.0f;
+        sdfValue = tf_short_to_float((short)((unsigned)sel8(reinterpret_cast<const int(&)[8]>(q.raw), cu) & 0xffffu));
         if (MARK && vmIndex) a.visType[vmIndex - 1] = 1;
         if (!vmIndex) {
             stepLength = (float)TF_BLK;

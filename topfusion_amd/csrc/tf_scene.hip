@@ -589,7 +589,7 @@ __device__ __forceinline__ unsigned integ_voxel(unsigned vox, float px, float py
     if (eta < -a.mu) return vox;
     short sdf = (short)(vox & 0xffff);
     int oldW = (vox >> 16) & 0xff;
-    float oldF = (float)sdf / 32767.0f;
+    float oldF = tf_short_to_float(sdf);          // == (float)sdf / 32767.0f, exactly
     float newF = eta / a.mu;
     newF = (1.0f < newF) ? 1.0f : newF;
     newF = (float)oldW * oldF + 1.0f * newF;
@@ -598,6 +598,31 @@ __device__ __forceinline__ unsigned integ_voxel(unsigned vox, float px, float py
     newW = (newW < a.maxW) ? newW : a.maxW;
     short nsdf = (short)(newF * 32767.0f);
     return ((unsigned)(unsigned short)nsdf) | ((unsigned)(newW & 0xff) << 16) | (vox & 0xff000000u);
+}
+
+typedef unsigned int tf_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load16(const uint4* p)
+{
+    const tf_u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const tf_u32x4*>(p));
+    return make_uint4(r.x, r.y, r.z, r.w);
+}
+__device__ __forceinline__ void nt_store16(uint4* p, uint4 v)
+{
+    tf_u32x4 r = { v.x, v.y, v.z, v.w };
+    __builtin_nontemporal_store(r, reinterpret_cast<tf_u32x4*>(p));
+}
+
+// one lane's 4 consecutive voxels (16 B) of a block: update and store
+__device__ __forceinline__ void integ_chunk(uint4 v, const TfHashEntry& e, int vx, int vy, int vz, const float* M,
+                                            const IntegArgs& a, uint4* p)
+{
+    const int gx = e.x * TF_BLK, gy = e.y * TF_BLK, gz = e.z * TF_BLK;
+    const float py = (float)(gy + vy) * a.voxelSize, pz = (float)(gz + vz) * a.voxelSize;
+    v.x = integ_voxel(v.x, (float)(gx + vx + 0) * a.voxelSize, py, pz, M, a);
+    v.y = integ_voxel(v.y, (float)(gx + vx + 1) * a.voxelSize, py, pz, M, a);
+    v.z = integ_voxel(v.z, (float)(gx + vx + 2) * a.voxelSize, py, pz, M, a);
+    v.w = integ_voxel(v.w, (float)(gx + vx + 3) * a.voxelSize, py, pz, M, a);
+    nt_store16(p, v);
 }
 
 __global__ void __launch_bounds__(256)
@@ -619,18 +644,23 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
     const int half = threadIdx.x >> 7, t = threadIdx.x & 127;
     const int lin = t * 4;                       // first voxel of this lane: x in {0,4}
     const int vx = lin & 7, vy = (lin >> 3) & 7, vz = lin >> 6;
-    for (int i = blockIdx.x * 2 + half; i < n; i += gridDim.x * 2) {
-        TfHashEntry e = hash[visibleIds[i]];
-        if (e.ptr < 0) continue;
-        const int gx = e.x * TF_BLK, gy = e.y * TF_BLK, gz = e.z * TF_BLK;
-        uint4* p = (uint4*)(vba + (size_t)e.ptr * TF_BLK3 + lin);
-        uint4 v = *p;
-        const float py = (float)(gy + vy) * a.voxelSize, pz = (float)(gz + vz) * a.voxelSize;
-        v.x = integ_voxel(v.x, (float)(gx + vx + 0) * a.voxelSize, py, pz, M, a);
-        v.y = integ_voxel(v.y, (float)(gx + vx + 1) * a.voxelSize, py, pz, M, a);
-        v.z = integ_voxel(v.z, (float)(gx + vx + 2) * a.voxelSize, py, pz, M, a);
-        v.w = integ_voxel(v.w, (float)(gx + vx + 3) * a.voxelSize, py, pz, M, a);
-        *p = v;
+    // two blocks per half-workgroup per pass, their id / entry / voxel loads issued before
+    // either is computed: twice the bytes in flight per wave (at C3 scale, 2^21 blocks, the
+    // pass is a stream over 8.6 GB)
+    const int stride = gridDim.x * 2;
+    for (int i = blockIdx.x * 2 + half; i < n; i += 2 * stride) {
+        const int i2 = i + stride;
+        const TfHashEntry e = hash[visibleIds[i]];
+        TfHashEntry e2;
+        e2.ptr = -1;
+        if (i2 < n) e2 = hash[visibleIds[i2]];
+        uint4* p = (uint4*)(vba + (size_t)(e.ptr < 0 ? 0 : e.ptr) * TF_BLK3 + lin);
+        uint4* p2 = (uint4*)(vba + (size_t)(e2.ptr < 0 ? 0 : e2.ptr) * TF_BLK3 + lin);
+        // the voxel stream is read and written once per pass: non-temporal, so it does not
+        // evict the depth image every voxel samples from L2
+        uint4 v = nt_load16(p), v2 = nt_load16(p2);
+        if (e.ptr >= 0) integ_chunk(v, e, vx, vy, vz, M, a, p);
+        if (e2.ptr >= 0) integ_chunk(v2, e2, vx, vy, vz, M, a, p2);
     }
 }
 

@@ -204,6 +204,14 @@ class TopFu:
     def set_pose(self, rt):
         L.check(L.load().tf_set_pose(self._h, _ptr(_rt(rt))), "tf_set_pose")
 
+    def time_stage(self, stage, pose_rt, iters):
+        """ms per launch of `iters` back-to-back launches of a stage's kernels (HIP events on
+        the context stream); stage: "integrate" or "raycast_icp"."""
+        ms = ctypes.c_float()
+        L.check(L.load().tf_time_stage(self._h, L.STAGE_NAMES.index(stage), _ptr(_rt(pose_rt)), int(iters),
+                                       ctypes.byref(ms)), "tf_time_stage")
+        return float(ms.value)
+
     def set_counters(self, lastFreeBlockId, lastFreeExcessListId, noVisibleEntries):
         L.check(L.load().tf_set_counters(self._h, lastFreeBlockId, lastFreeExcessListId, noVisibleEntries),
                 "tf_set_counters")
