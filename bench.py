@@ -91,10 +91,21 @@ def stage_bytes(stage, p, nvis, W, H):
     return None
 
 
-def cpu_baseline(frames, params_kw, seconds):
-    """Oracle (serial C restatement of the reference, 1 thread) on a bounded prefix of the same stream."""
+def omp_threads():
+    """Threads the OpenMP build uses: OMP_NUM_THREADS (16 on the GPU box), else the CPUs this
+    process may run on."""
+    v = os.environ.get("OMP_NUM_THREADS")
+    if v and v.isdigit() and int(v) > 0:
+        return int(v)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(frames, params_kw, seconds, omp=False):
+    """Oracle (C restatement of the reference) on a bounded prefix of the same stream: the serial
+    build (1 thread) or its OpenMP build (omp=True: independent pixels / CTAs / blocks over
+    OMP_NUM_THREADS threads, the allocation pass serial; results identical)."""
     from oracle import oracle as O
-    o = O.Oracle(O.default_params(**params_kw))
+    o = O.Oracle(O.default_params(**params_kw), omp=omp)
     t0 = time.perf_counter()
     n = 0
     while n < len(frames):
@@ -309,10 +320,16 @@ def main():
                 roof = roof_all[dominant]
         cpu = None
         if not args.no_cpu_baseline:
-            v, n, dt = cpu_baseline(frames, pkw, args.cpu_seconds)
-            cpu = {"value": round(v, 4), "unit": "frames/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle (serial C restatement) on frames 0..{n - 1} of the same {args.config} stream, "
-                             f"{W}x{H}, {dt:.1f} s, 1 thread, host CPU of the GPU box"}
+            # all cores: the OpenMP build of the oracle; 1 thread: the serial build (reported beside)
+            nt = omp_threads()
+            v, n, dt = cpu_baseline(frames, pkw, args.cpu_seconds, omp=True)
+            v1, n1, dt1 = cpu_baseline(frames, pkw, args.cpu_seconds, omp=False)
+            cpu = {"value": round(v, 4), "unit": "frames/s", "cores": nt, "kind": "port",
+                   "sample": f"oracle (C restatement, OpenMP build: per-pixel / per-CTA / per-block loops on {nt} "
+                             f"threads, allocation serial) on frames 0..{n - 1} of the same {args.config} stream, "
+                             f"{W}x{H}, {dt:.1f} s, host CPU of the GPU box",
+                   "single_thread": {"value": round(v1, 4), "cores": 1,
+                                     "sample": f"serial oracle on frames 0..{n1 - 1}, {dt1:.1f} s"}}
         out = {
             "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame",
             "value": round(value, 2),

@@ -12,6 +12,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_HERE, "liboracle.so")
+_LIB_OMP = os.path.join(_HERE, "liboracle_omp.so")      # same source, OpenMP loops enabled
 
 
 class Params(ctypes.Structure):
@@ -39,20 +40,22 @@ class Counters(ctypes.Structure):
 HASH_DTYPE = np.dtype([("x", "<i2"), ("y", "<i2"), ("z", "<i2"), ("pad", "<i2"), ("offset", "<i4"), ("ptr", "<i4")])
 VOXEL_DTYPE = np.dtype([("sdf", "<i2"), ("w", "u1"), ("pad", "u1")])
 
-_lib = None
+_libs = {}
 
 
-def build():
+def build(omp=False):
     """Compile the oracle with its Makefile (gcc, -ffp-contract=off)."""
-    subprocess.run(["make", "-s", "-C", _HERE, "liboracle.so"], check=True)
+    subprocess.run(["make", "-s", "-C", _HERE, "liboracle_omp.so" if omp else "liboracle.so"], check=True)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB):
-            build()
-        L = ctypes.CDLL(_LIB)
+def lib(omp=False):
+    """The serial oracle (default) or its OpenMP build (omp=True: the all-cores CPU baseline;
+    every result identical, tests/test_oracle.py)."""
+    if omp not in _libs:
+        path = _LIB_OMP if omp else _LIB
+        if not os.path.exists(path):
+            build(omp)
+        L = ctypes.CDLL(path)
         P = ctypes.c_void_p
         L.tfo_default_params.argtypes = [ctypes.POINTER(Params)]
         L.tfo_exp.argtypes = [ctypes.c_float]; L.tfo_exp.restype = ctypes.c_float
@@ -91,8 +94,8 @@ def lib():
             getattr(L, name).argtypes = [P]; getattr(L, name).restype = P
         for name in ("tfo_prev_points", "tfo_prev_normals", "tfo_curr_points", "tfo_curr_normals", "tfo_curr_depth"):
             getattr(L, name).argtypes = [P, ctypes.c_int]; getattr(L, name).restype = P
-        _lib = L
-    return _lib
+        _libs[omp] = L
+    return _libs[omp]
 
 
 def ptr(a):
@@ -202,16 +205,17 @@ def tsdf_update(sdf, w, eta, mu=0.02, maxW=100):
 class Oracle:
     """The reference TopFu pipeline restated on the CPU (oracle/tf_oracle.c)."""
 
-    def __init__(self, params=None, **kw):
+    def __init__(self, params=None, omp=False, **kw):
+        self.L = lib(omp)
         self.params = params if params is not None else default_params(**kw)
-        self.ctx = lib().tfo_create(ctypes.byref(self.params))
+        self.ctx = self.L.tfo_create(ctypes.byref(self.params))
         self.W, self.H = self.params.cols, self.params.rows
         self.n_total = self.params.n_buckets + self.params.n_excess
 
     def __del__(self):
         try:
             if getattr(self, "ctx", None):
-                lib().tfo_destroy(self.ctx)
+                self.L.tfo_destroy(self.ctx)
                 self.ctx = None
         except Exception:
             pass
@@ -219,19 +223,19 @@ class Oracle:
     def __call__(self, depth):
         d = np.ascontiguousarray(depth, np.uint16)
         assert d.shape == (self.H, self.W)
-        return bool(lib().tfo_process_frame(self.ctx, ptr(d)))
+        return bool(self.L.tfo_process_frame(self.ctx, ptr(d)))
 
     def reset(self):
-        lib().tfo_reset(self.ctx)
+        self.L.tfo_reset(self.ctx)
 
     def counters(self):
         c = Counters()
-        lib().tfo_get_counters(self.ctx, ctypes.byref(c))
+        self.L.tfo_get_counters(self.ctx, ctypes.byref(c))
         return c.as_dict()
 
     def pose(self):
         rt = np.zeros(12, np.float32)
-        lib().tfo_get_pose(self.ctx, ptr(rt))
+        self.L.tfo_get_pose(self.ctx, ptr(rt))
         return rt.reshape(3, 4)
 
     def _view(self, addr, dtype, count, shape=None):
@@ -240,78 +244,78 @@ class Oracle:
         return a.reshape(shape) if shape else a
 
     def hash(self):
-        return self._view(lib().tfo_hash(self.ctx), HASH_DTYPE, self.n_total).copy()
+        return self._view(self.L.tfo_hash(self.ctx), HASH_DTYPE, self.n_total).copy()
 
     def vba(self):
-        return self._view(lib().tfo_vba(self.ctx), VOXEL_DTYPE, self.params.n_blocks * 512).copy()
+        return self._view(self.L.tfo_vba(self.ctx), VOXEL_DTYPE, self.params.n_blocks * 512).copy()
 
     def visible_ids(self):
         n = self.counters()["noVisibleEntries"]
-        return self._view(lib().tfo_visible_ids(self.ctx), np.int32, self.params.vis_capacity)[:n].copy()
+        return self._view(self.L.tfo_visible_ids(self.ctx), np.int32, self.params.vis_capacity)[:n].copy()
 
     def visible_type(self):
-        return self._view(lib().tfo_visible_type(self.ctx), np.uint8, self.n_total).copy()
+        return self._view(self.L.tfo_visible_type(self.ctx), np.uint8, self.n_total).copy()
 
     def range_image(self):
-        return self._view(lib().tfo_range_image(self.ctx), np.float32, self.W * self.H * 2, (self.H, self.W, 2)).copy()
+        return self._view(self.L.tfo_range_image(self.ctx), np.float32, self.W * self.H * 2, (self.H, self.W, 2)).copy()
 
     def raycast_result(self):
-        return self._view(lib().tfo_raycast_result(self.ctx), np.float32, self.W * self.H * 4, (self.H, self.W, 4)).copy()
+        return self._view(self.L.tfo_raycast_result(self.ctx), np.float32, self.W * self.H * 4, (self.H, self.W, 4)).copy()
 
     def frame_grey(self):
-        return self._view(lib().tfo_frame_grey(self.ctx), np.uint8, self.W * self.H * 4, (self.H, self.W, 4)).copy()
+        return self._view(self.L.tfo_frame_grey(self.ctx), np.uint8, self.W * self.H * 4, (self.H, self.W, 4)).copy()
 
     def dists(self):
-        return self._view(lib().tfo_dists(self.ctx), np.float32, self.W * self.H, (self.H, self.W)).copy()
+        return self._view(self.L.tfo_dists(self.ctx), np.float32, self.W * self.H, (self.H, self.W)).copy()
 
     def level_shape(self, l):
         return self.H >> l, self.W >> l
 
     def prev_maps(self, l):
         h, w = self.level_shape(l)
-        p = self._view(lib().tfo_prev_points(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
-        n = self._view(lib().tfo_prev_normals(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
+        p = self._view(self.L.tfo_prev_points(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
+        n = self._view(self.L.tfo_prev_normals(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
         return p, n
 
     def curr_maps(self, l):
         h, w = self.level_shape(l)
-        p = self._view(lib().tfo_curr_points(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
-        n = self._view(lib().tfo_curr_normals(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
+        p = self._view(self.L.tfo_curr_points(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
+        n = self._view(self.L.tfo_curr_normals(self.ctx, l), np.float32, h * w * 4, (h, w, 4)).copy()
         return p, n
 
     def curr_depth(self, l):
         h, w = self.level_shape(l)
-        return self._view(lib().tfo_curr_depth(self.ctx, l), np.uint16, h * w, (h, w)).copy()
+        return self._view(self.L.tfo_curr_depth(self.ctx, l), np.uint16, h * w, (h, w)).copy()
 
     # stage-level
     def alloc(self, pose_rt, dists):
-        lib().tfo_alloc(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
+        self.L.tfo_alloc(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
                         ptr(np.ascontiguousarray(dists, np.float32)))
 
     def integrate(self, pose_rt, dists):
-        lib().tfo_integrate(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
+        self.L.tfo_integrate(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
                             ptr(np.ascontiguousarray(dists, np.float32)))
 
     def expected_depths(self, pose_rt):
-        lib().tfo_expected_depths(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)))
+        self.L.tfo_expected_depths(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)))
 
     def raycast(self, invM_rt, update_visible):
-        lib().tfo_raycast(self.ctx, ptr(np.ascontiguousarray(invM_rt, np.float32).reshape(12)), int(update_visible))
+        self.L.tfo_raycast(self.ctx, ptr(np.ascontiguousarray(invM_rt, np.float32).reshape(12)), int(update_visible))
 
     def render_icp(self, invM_rt):
         pts = np.empty((self.H, self.W, 4), np.float32)
         nrm = np.empty((self.H, self.W, 4), np.float32)
-        lib().tfo_render_icp(self.ctx, ptr(np.ascontiguousarray(invM_rt, np.float32).reshape(12)), ptr(pts), ptr(nrm))
+        self.L.tfo_render_icp(self.ctx, ptr(np.ascontiguousarray(invM_rt, np.float32).reshape(12)), ptr(pts), ptr(nrm))
         return pts, nrm
 
     def render_grey(self, invM_rt):
         img = np.empty((self.H, self.W, 4), np.uint8)
-        lib().tfo_render_grey(self.ctx, ptr(np.ascontiguousarray(invM_rt, np.float32).reshape(12)), ptr(img))
+        self.L.tfo_render_grey(self.ctx, ptr(np.ascontiguousarray(invM_rt, np.float32).reshape(12)), ptr(img))
         return img
 
     def render_image(self):
         img = np.empty((self.H, self.W, 4), np.uint8)
-        lib().tfo_render_image(self.ctx, ptr(img))
+        self.L.tfo_render_image(self.ctx, ptr(img))
         return img
 
 

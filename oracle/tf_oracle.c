@@ -212,6 +212,7 @@ void tfo_rodrigues(const float r[3], float R[9])
 /* compute_dists_kernel, imgproc.cu:263-280 */
 void tfo_compute_dists(const uint16_t* depth, int W, int H, float* dists)
 {
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < W * H; ++i) {
         int d = depth[i];
         dists[i] = (d >= 2047 || d <= 0) ? -1.0f : (float)d * 0.001f;
@@ -224,6 +225,7 @@ void tfo_bilateral(const uint16_t* src, uint16_t* dst, int W, int H, int ksz, fl
     float sigma_depth = sigma_depth_m * 1000.0f;
     float ss = 0.5f / (sigma_spatial * sigma_spatial);
     float sd = 0.5f / (sigma_depth * sigma_depth);
+#pragma omp parallel for schedule(static)
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             int value = src[y * W + x];
@@ -259,6 +261,7 @@ void tfo_pyr_down(const uint16_t* src, int W, int H, uint16_t* dst, float sigma_
     float sigma3 = sigma_depth_m * 1000.0f * 3.0f;
     int DW = W / 2, DH = H / 2;
     const int D = 5;
+#pragma omp parallel for schedule(static)
     for (int y = 0; y < DH; ++y)
         for (int x = 0; x < DW; ++x) {
             int center = src[(2 * y) * W + 2 * x];
@@ -280,6 +283,7 @@ void tfo_points_normals(const uint16_t* depth, int W, int H, float fx, float fy,
 {
     const float qnan = qnanf_bits();
     float fxi = 1.f / fx, fyi = 1.f / fy;
+#pragma omp parallel for schedule(static)
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             float* p = points + 4 * (y * W + x);
@@ -306,6 +310,7 @@ void tfo_resize_points_normals(const float* vsrc, const float* nsrc, int W, int 
 {
     const float qnan = qnanf_bits();
     int DW = W / 2, DH = H / 2;
+#pragma omp parallel for schedule(static)
     for (int y = 0; y < DH; ++y)
         for (int x = 0; x < DW; ++x) {
             float* vo = vdst + 4 * (y * DW + x);
@@ -383,10 +388,16 @@ void tfo_icp_reduce(const float* vcurr, const float* ncurr, const float* vprev, 
     int gx = (W + 31) / 32, gy = (H + 7) / 8;     /* CTA 32x8, proj_icp.cu:17-19,439-440 */
     int nct = gx * gy;
     float* partial = (float*)malloc(sizeof(float) * 27 * (size_t)nct);
-    float (*rows)[7] = malloc(sizeof(float) * 7 * 256);
     float v[256];
-    for (int by = 0; by < gy; ++by)
-        for (int bx = 0; bx < gx; ++bx) {
+    /* the CTAs' partial sums are independent (OpenMP build: one CTA per iteration) */
+#pragma omp parallel
+    {
+    float (*rows)[7] = malloc(sizeof(float) * 7 * 256);
+    float vt[256];
+#pragma omp for schedule(static)
+    for (int cta_i = 0; cta_i < nct; ++cta_i) {
+        const int by = cta_i / gx, bx = cta_i % gx;
+        {
             for (int tid = 0; tid < 256; ++tid) {
                 int x = bx * 32 + (tid & 31), y = by * 8 + (tid >> 5);
                 int filtered = (x < W && y < H) ? icp_row(vcurr, ncurr, vprev, nprev, W, H, x, y, fx, fy, cx, cy,
@@ -396,10 +407,13 @@ void tfo_icp_reduce(const float* vcurr, const float* ncurr, const float* vprev, 
             int cta = bx + gx * by, k = 0;
             for (int i = 0; i < 6; ++i)
                 for (int j = i; j < 7; ++j, ++k) {   /* partial_reduce order, proj_icp.cu:137-356 */
-                    for (int tid = 0; tid < 256; ++tid) v[tid] = rows[tid][i] * rows[tid][j];
-                    partial[k * nct + cta] = tree256(v);
+                    for (int tid = 0; tid < 256; ++tid) vt[tid] = rows[tid][i] * rows[tid][j];
+                    partial[k * nct + cta] = tree256(vt);
                 }
         }
+    }
+    free(rows);
+    }
     for (int k = 0; k < 27; ++k) {              /* icp_final_reduce_kernel, proj_icp.cu:382-403 */
         for (int tid = 0; tid < 256; ++tid) {
             float sum = 0.f;
@@ -408,7 +422,6 @@ void tfo_icp_reduce(const float* vcurr, const float* ncurr, const float* vprev, 
         }
         out27[k] = tree256(v);
     }
-    free(rows);
     free(partial);
 }
 
@@ -817,6 +830,7 @@ void tfo_integrate(tfo_ctx* c, const float pose_rt[12], const float* dists)
     rt_to_m4(pose_rt, M);
     float proj[4] = { c->p.fx, c->p.fy, c->p.cx, c->p.cy };
     float vs = c->p.voxelSize;
+#pragma omp parallel for schedule(dynamic, 16)
     for (int i = 0; i < c->noVisibleEntries; ++i) {
         const tfo_hash_entry* e = &c->hash[c->visibleIds[i]];
         if (e->ptr < 0) continue;
@@ -1014,6 +1028,8 @@ void tfo_raycast(tfo_ctx* c, const float invM_rt[12], int update_visible)
     rt_to_m4(invM_rt, invM);
     float oneOverVoxelSize = 1.0f / c->p.voxelSize;
     float invProj[4] = { 1.0f / c->p.fx, 1.0f / c->p.fy, -c->p.cx, -c->p.cy };  /* InvertProjectionParams :28-31 */
+    /* rays are independent; castRay<true>'s visibility marks all write the value 1 */
+#pragma omp parallel for schedule(dynamic, 4)
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             int locId = x + y * W;
@@ -1031,6 +1047,7 @@ void tfo_render_icp(tfo_ctx* c, const float invM_rt[12], float* points, float* n
     float light[3] = { -invM_rt[2], -invM_rt[6], -invM_rt[10] };   /* -Vector3f(invM.getColumn(2)) */
     const float qnan = qnanf_bits();
     const float* ray = c->raycast;
+#pragma omp parallel for schedule(static)
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             int locId = x + y * W;
@@ -1117,6 +1134,7 @@ void tfo_render_grey(tfo_ctx* c, const float invM_rt[12], uint8_t* rgba)
 {
     int W = c->p.cols, H = c->p.rows;
     float light[3] = { -invM_rt[2], -invM_rt[6], -invM_rt[10] };
+#pragma omp parallel for schedule(dynamic, 256)
     for (int i = 0; i < W * H; ++i) {
         const float* p = c->raycast + 4 * i;
         int found = p[3] > 0;
