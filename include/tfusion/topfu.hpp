@@ -175,11 +175,21 @@ namespace tfusion
             return true;
         }
 
-        // TopFu::renderImage (topfu.cpp:332-377): grey shading of the current pose
-        void renderImage(cuda::image4u& image)
+        // TopFu::renderImage (topfu.cpp:332-377): grey shading of the current pose.  The type
+        // argument (default: the reference's RENDER_SHADED_GREYSCALE) selects one of the engine's
+        // RenderImageType modes (VisualisationEngine.hpp:15-22) -- an addition, source compatible.
+        enum RenderImageType {
+            RENDER_SHADED_GREYSCALE = TF_RENDER_SHADED_GREYSCALE,
+            RENDER_SHADED_GREYSCALE_IMAGENORMALS = TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS,
+            RENDER_COLOUR_FROM_VOLUME = TF_RENDER_COLOUR_FROM_VOLUME,
+            RENDER_COLOUR_FROM_NORMAL = TF_RENDER_COLOUR_FROM_NORMAL,
+            RENDER_COLOUR_FROM_CONFIDENCE = TF_RENDER_COLOUR_FROM_CONFIDENCE
+        };
+        void renderImage(cuda::image4u& image, RenderImageType type = RENDER_SHADED_GREYSCALE)
         {
             image.create(params_.rows, params_.cols);
-            check(tf_render_image(ctx_, reinterpret_cast<uint8_t*>(image.ptr()), image.step()), "tf_render_image");
+            check(tf_render_image_type(ctx_, (int)type, reinterpret_cast<uint8_t*>(image.ptr()), image.step()),
+                  "tf_render_image_type");
         }
 
         Affine3f getCameraPose(int time = -1) const   // topfu.cpp:154-159

@@ -122,6 +122,19 @@ tf_status tf_process_frames(tf_ctx* ctx, const uint16_t* dev_frames, size_t fram
 /* TopFu::renderImage (tfusion/src/topfu.cpp:332-377): raycast + grey shading of the
  * current pose into dev_rgba (uchar4, rows x cols, pitch bytes). */
 tf_status tf_render_image(tf_ctx* ctx, uint8_t* dev_rgba, size_t pitch_bytes);
+/* IVisualisationEngine::RenderImageType (tfusion/include/tfusion/VisualisationEngine.hpp:15-22) */
+typedef enum tf_render_type {
+    TF_RENDER_SHADED_GREYSCALE = 0,              /* renderGrey_device (SDF-gradient normals) */
+    TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS = 1, /* renderGrey_ImageNormals_device<false> (raycast-image normals) */
+    TF_RENDER_COLOUR_FROM_VOLUME = 2,            /* Voxel_s has no colour: greyscale (VisualisationEngine_CUDA.cu:251-252) */
+    TF_RENDER_COLOUR_FROM_NORMAL = 3,            /* renderColourFromNormal_device (alpha left as it was) */
+    TF_RENDER_COLOUR_FROM_CONFIDENCE = 4         /* renderColourFromConfidence_device */
+} tf_render_type;
+/* VisualisationEngine_CUDA::RenderImage(scene, pose, intr, renderState, image, type,
+ * RENDER_FROM_NEW_RAYCAST) (VisualisationEngine_CUDA.cu:220-291, 423-429) from poses_.back():
+ * raycast with the current range image, then the type's pixel stage into the context's
+ * image buffer (TF_BUF_GREY) and, when dev_rgba is non-null, a copy there. */
+tf_status tf_render_image_type(tf_ctx* ctx, int type, uint8_t* dev_rgba, size_t pitch_bytes);
 /* TopFu::getCameraPose (tfusion/src/topfu.cpp:154-159), time = -1 only */
 tf_status tf_get_pose(tf_ctx* ctx, float rt[12]);
 tf_status tf_get_stats(tf_ctx* ctx, tf_stats* stats);

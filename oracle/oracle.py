@@ -89,6 +89,8 @@ def lib(omp=False):
         L.tfo_render_icp.argtypes = [P, P, P, P]
         L.tfo_render_grey.argtypes = [P, P, P]
         L.tfo_render_image.argtypes = [P, P]
+        L.tfo_render_type.argtypes = [P, P, ctypes.c_int, P]
+        L.tfo_render_image_type.argtypes = [P, ctypes.c_int]
         for name in ("tfo_hash", "tfo_vba", "tfo_visible_ids", "tfo_visible_type", "tfo_range_image",
                      "tfo_raycast_result", "tfo_dists", "tfo_frame_grey"):
             getattr(L, name).argtypes = [P]; getattr(L, name).restype = P
@@ -317,6 +319,12 @@ class Oracle:
         img = np.empty((self.H, self.W, 4), np.uint8)
         self.L.tfo_render_image(self.ctx, ptr(img))
         return img
+
+    def render_image_type(self, type):
+        """RenderImage(type) from the current pose into the context image (the buffer the frame's
+        renderImage fills, so alpha-preserving types see its previous content); returns a copy."""
+        self.L.tfo_render_image_type(self.ctx, int(type))
+        return self.frame_grey()
 
 
 def point_conv(p):

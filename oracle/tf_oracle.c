@@ -1128,31 +1128,119 @@ static void normal_from_sdf(const tfo_ctx* c, const float pt[3], float ret[3])
 #undef RV
 }
 
-/* renderGrey_device / processPixelGrey / drawPixelGrey,
-   VisualisationHelper.hpp:105-118; VisualisationEngine_Shared.hpp:187-203,272-276,450-462 */
-void tfo_render_grey(tfo_ctx* c, const float invM_rt[12], uint8_t* rgba)
+/* baseCol / interpolateCol, VisualisationEngine_Shared.hpp:278-288 */
+static float interpolate_col(float val, float y0, float x0, float y1, float x1) { return (val - x0) * (y1 - y0) / (x1 - x0) + y0; }
+static float base_col(float val)
+{
+    if (val <= -0.75f) return 0.0f;
+    else if (val <= -0.25f) return interpolate_col(val, 0.0f, -0.75f, 1.0f, -0.25f);
+    else if (val <= 0.25f) return 1.0f;
+    else if (val <= 0.75f) return interpolate_col(val, 1.0f, 0.25f, 0.0f, 0.75f);
+    else return 0.0f;
+}
+
+/* Vector4f::toUChar: CLAMP((int)ROUND(v), 0, 255), Vector.hpp:398-404, MathUtils.hpp:16-20 */
+static uint8_t round_u8(float v)
+{
+    int i = (int)((v < 0) ? (v - 0.5f) : (v + 0.5f));
+    return (uint8_t)(i < 0 ? 0 : (i > 255 ? 255 : i));
+}
+
+/* computeNormalAndAngle<useSmoothing=true, flipNormals=false> on the raycast image,
+   VisualisationEngine_Shared.hpp:205-270 */
+static int image_normal_angle(const float* ray, int W, int H, int x, int y, float voxelSize, const float light[3], float* angle)
+{
+    if (y <= 2 || y >= H - 3 || x <= 2 || x >= W - 3) return 0;
+    const float *xp = ray + 4 * ((x + 2) + y * W), *yp = ray + 4 * (x + (y + 2) * W);
+    const float *xm = ray + 4 * ((x - 2) + y * W), *ym = ray + 4 * (x + (y - 2) * W);
+    float dx[3] = { 0, 0, 0 }, dy[3] = { 0, 0, 0 };
+    int plus1 = 0;
+    if (xp[3] <= 0 || yp[3] <= 0 || xm[3] <= 0 || ym[3] <= 0) plus1 = 1;
+    else {
+        for (int k = 0; k < 3; ++k) { dx[k] = xp[k] - xm[k]; dy[k] = yp[k] - ym[k]; }
+        float lx = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2], ly = dy[0] * dy[0] + dy[1] * dy[1] + dy[2] * dy[2];
+        float length_diff = (lx < ly) ? ly : lx;                  /* MAX */
+        if (length_diff * voxelSize * voxelSize > (0.15f * 0.15f)) plus1 = 1;
+    }
+    if (plus1) {
+        xp = ray + 4 * ((x + 1) + y * W); yp = ray + 4 * (x + (y + 1) * W);
+        xm = ray + 4 * ((x - 1) + y * W); ym = ray + 4 * (x + (y - 1) * W);
+        for (int k = 0; k < 3; ++k) { dx[k] = xp[k] - xm[k]; dy[k] = yp[k] - ym[k]; }
+        if (xp[3] <= 0 || yp[3] <= 0 || xm[3] <= 0 || ym[3] <= 0) return 0;
+    }
+    float n[3] = { -(dx[1] * dy[2] - dx[2] * dy[1]), -(dx[2] * dy[0] - dx[0] * dy[2]), -(dx[0] * dy[1] - dx[1] * dy[0]) };
+    float ns = 1.0f / sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    n[0] *= ns; n[1] *= ns; n[2] *= ns;
+    *angle = n[0] * light[0] + n[1] * light[1] + n[2] * light[2];
+    return *angle > 0.0f;
+}
+
+/* RenderImage_common's pixel stages, VisualisationEngine_CUDA.cu:254-290: renderGrey_device,
+   renderGrey_ImageNormals_device<false>, renderColourFromNormal_device,
+   renderColourFromConfidence_device (VisualisationHelper.hpp:76-148); processPixel* /
+   drawPixel* VisualisationEngine_Shared.hpp:187-310,399-498.  RENDER_COLOUR_FROM_VOLUME falls
+   back to greyscale for Voxel_s (:251-252).  drawPixelNormal leaves alpha as it was. */
+void tfo_render_type(tfo_ctx* c, const float invM_rt[12], int type, uint8_t* rgba)
 {
     int W = c->p.cols, H = c->p.rows;
     float light[3] = { -invM_rt[2], -invM_rt[6], -invM_rt[10] };
 #pragma omp parallel for schedule(dynamic, 256)
     for (int i = 0; i < W * H; ++i) {
         const float* p = c->raycast + 4 * i;
+        uint8_t* o = rgba + 4 * i;
         int found = p[3] > 0;
-        uint8_t v = 0;
+        float n[3] = { 0, 0, 0 }, angle = 0;
+        if (type == 1) {
+            if (found) found = image_normal_angle(c->raycast, W, H, i % W, i / W, c->p.voxelSize, light, &angle);
+            uint8_t v = found ? (uint8_t)((0.8f * angle + 0.2f) * 255.0f) : 0;
+            o[0] = o[1] = o[2] = o[3] = v;
+            continue;
+        }
         if (found) {
-            float n[3];
             normal_from_sdf(c, p, n);
             float ns = 1.0f / sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
             n[0] *= ns; n[1] *= ns; n[2] *= ns;
-            float angle = n[0] * light[0] + n[1] * light[1] + n[2] * light[2];
+            angle = n[0] * light[0] + n[1] * light[1] + n[2] * light[2];
             if (!(angle > 0.0)) found = 0;
-            else {
-                float outRes = (0.8f * angle + 0.2f) * 255.0f;
-                v = (uint8_t)outRes;
-            }
         }
-        rgba[4 * i + 0] = rgba[4 * i + 1] = rgba[4 * i + 2] = rgba[4 * i + 3] = found ? v : 0;
+        if (type == 3) {
+            if (found) {
+                for (int k = 0; k < 3; ++k) o[k] = (uint8_t)((0.3f + (-n[k] + 1.0f) * 0.35f) * 255.0f);
+            } else {
+                o[0] = o[1] = o[2] = o[3] = 0;
+            }
+        } else if (type == 4) {
+            if (found) {
+                float conf = p[3] - 1.0f;
+                float mn = (100.f < conf) ? 100.f : conf;          /* CLAMP(conf, 0, 100.f) */
+                float cn = ((0 < mn) ? mn : 0) / 100.0f;
+                float col[4] = { (float)(uint8_t)(base_col(cn) * 255.0f), (float)(uint8_t)(base_col(cn - 0.5f) * 255.0f),
+                                 (float)(uint8_t)(base_col(cn + 0.5f) * 255.0f), 255.0f };
+                float sc = 0.8f * angle + 0.2f;
+                for (int k = 0; k < 4; ++k) o[k] = round_u8(sc * col[k]);
+            } else {
+                o[0] = o[1] = o[2] = o[3] = 0;
+            }
+        } else {
+            uint8_t v = found ? (uint8_t)((0.8f * angle + 0.2f) * 255.0f) : 0;
+            o[0] = o[1] = o[2] = o[3] = v;
+        }
     }
+}
+
+/* renderGrey_device / processPixelGrey / drawPixelGrey,
+   VisualisationHelper.hpp:105-118; VisualisationEngine_Shared.hpp:187-203,272-276,450-462 */
+void tfo_render_grey(tfo_ctx* c, const float invM_rt[12], uint8_t* rgba)
+{
+    tfo_render_type(c, invM_rt, 0, rgba);
+}
+
+/* VisualisationEngine_CUDA::RenderImage(type, RENDER_FROM_NEW_RAYCAST) from the current pose into
+   the context's image (the buffer the frame's renderImage fills) */
+void tfo_render_image_type(tfo_ctx* c, int type)
+{
+    tfo_raycast(c, c->pose, 0);
+    tfo_render_type(c, c->pose, type, c->frame_grey);
 }
 
 /* TopFu::renderImage -> RenderImage_common(RENDER_SHADED_GREYSCALE), topfu.cpp:332-377,

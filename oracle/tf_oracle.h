@@ -130,6 +130,8 @@ void tfo_integrate(tfo_ctx* c, const float pose_rt[12], const float* dists);  /*
 void tfo_expected_depths(tfo_ctx* c, const float pose_rt[12]);                 /* CreateExpectedDepths */
 void tfo_raycast(tfo_ctx* c, const float invM_rt[12], int update_visible);    /* GenericRaycast */
 void tfo_render_icp(tfo_ctx* c, const float invM_rt[12], float* points, float* normals); /* renderICP */
+void tfo_render_type(tfo_ctx* c, const float invM_rt[12], int type, uint8_t* rgba);
+void tfo_render_image_type(tfo_ctx* c, int type);
 void tfo_render_grey(tfo_ctx* c, const float invM_rt[12], uint8_t* rgba);     /* renderGrey */
 void tfo_render_image(tfo_ctx* c, uint8_t* rgba);                              /* TopFu::renderImage */
 /* state access */

@@ -300,3 +300,19 @@ def test_c5_random_walk_10mm(oracle_mod):
         assert_bit_exact(f"frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
     compare_scene(g, o, "C5 final")
     assert_bit_exact("C5 final raycast", g.raycast_result(), o.raycast_result())
+
+
+def test_render_image_types(oracle_mod):
+    """The engine's five RenderImageType modes (VisualisationEngine.hpp:15-22; pixel stages
+    VisualisationEngine_CUDA.cu:254-290) from the current pose after a tracked sequence, in an
+    order where the alpha-preserving colour-from-normal mode follows each of the others."""
+    g, o = make_pair(oracle_mod, 320, 240)
+    seq = synth.orbit_sequence(6, 320, 240, seed=7)
+    for k in range(6):
+        assert g(seq[k]) == o(seq[k])
+    lit = {}
+    for t in (3, 0, 3, 1, 3, 4, 3, 2, 1, 4, 0):
+        img_g, img_o = g.renderImage(t), o.render_image_type(t)
+        assert_bit_exact(f"render type {t}", img_g, img_o)
+        lit[t] = int((img_g[..., :3] > 0).any(-1).sum())
+    assert all(v > 1000 for v in lit.values()), lit          # every mode renders the scene

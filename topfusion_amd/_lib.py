@@ -103,6 +103,7 @@ def load():
         "tf_upload": ([P, I, I, P, S], I),
         "tf_set_pose": ([P, P], I),
         "tf_set_counters": ([P, I, I, I], I),
+        "tf_render_image_type": ([P, I, P, S], I),
         "tf_time_stage": ([P, I, P, I, ctypes.POINTER(ctypes.c_float)], I),
         "tf_profile_enable": ([P, I], I),
         "tf_profile_stages": ([P, ctypes.c_uint], I),

@@ -515,12 +515,17 @@ extern "C" tf_status tf_process_frames(tf_ctx* c, const uint16_t* dev_frames, si
 
 extern "C" tf_status tf_render_image(tf_ctx* c, uint8_t* dev_rgba, size_t pitch)
 {   // TopFu::renderImage: raycast from poses_.back() with the current range image + grey
-    if (!c) return TF_INVALID_ARG;
+    return tf_render_image_type(c, TF_RENDER_SHADED_GREYSCALE, dev_rgba, pitch);
+}
+
+extern "C" tf_status tf_render_image_type(tf_ctx* c, int type, uint8_t* dev_rgba, size_t pitch)
+{   // VisualisationEngine_CUDA::RenderImage(..., type, RENDER_FROM_NEW_RAYCAST) from poses_.back()
+    if (!c || type < TF_RENDER_SHADED_GREYSCALE || type > TF_RENDER_COLOUR_FROM_CONFIDENCE) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));
     TF_CHECK(hipMemcpyAsync(c->st->pose_in, c->st->pose, sizeof(float) * 12, hipMemcpyDeviceToDevice, c->stream));
     TF_CHECK(tfk_pose_from_input(c, 0));
     TF_CHECK(tfk_raycast(c, 0));
-    TF_CHECK(tfk_render_grey(c));
+    TF_CHECK(tfk_render_type(c, type));
     if (dev_rgba) {
         if (pitch == 0) pitch = (size_t)c->W * 4;
         TF_CHECK(hipMemcpy2DAsync(dev_rgba, pitch, c->grey, (size_t)c->W * 4, (size_t)c->W * 4, c->H,
@@ -668,7 +673,7 @@ extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, invM_rt, 0);
     if (s != TF_OK) return s;
-    TF_CHECK(tfk_render_grey(c));
+    TF_CHECK(tfk_render_type(c, TF_RENDER_SHADED_GREYSCALE));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }

@@ -287,7 +287,7 @@ hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a h
 hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0);   // snapshot: + the frame's renderImage snapshot
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
-hipError_t tfk_render_grey(tf_ctx* c);
+hipError_t tfk_render_type(tf_ctx* c, int type);   // RenderImage pixel stage (tf_render_type) on raycast
 hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);
 hipError_t tfk_raycast_pair(tf_ctx* c);   // CreateICPMaps raycast + renderImage, one launch (frame path)    // renderImage raycast + grey, fused (frame path, render stream)
 hipError_t tfk_icp_maps(tf_ctx* c);

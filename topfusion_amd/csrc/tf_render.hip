@@ -3,7 +3,7 @@
 //   k_raycast     : genericRaycast_device / castRay (VisualisationHelper.hpp:33-46,
 //                   VisualisationEngine_Shared.hpp:99-172), incl. the IndexCache behaviour
 //                   that decides which entries castRay<true> marks visible
-//   k_grey        : renderGrey_device (VisualisationHelper.hpp:105-118)
+//   k_render_type : renderGrey_device and the other RenderImage types (VisualisationHelper.hpp:76-148)
 //   k_icp_maps    : renderICP_device + 2x resizePointsNormals fused: every pyramid level
 //                   is recomputed from the raycast result in one launch
 //   k_ed_*        : CreateExpectedDepths (VisualisationEngine_CUDA.cu:119-173) as
@@ -326,14 +326,25 @@ __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
 #undef RV
 }
 
-__device__ __forceinline__ unsigned char grey_pixel(const SceneView& s, const float* pt, float lx, float ly, float lz)
+// computeNormalAndAngle<TVoxel,TIndex> (VisualisationEngine_Shared.hpp:189-203): the SDF-gradient
+// normal at pt, normalised, and its angle to the light; false when the angle is not positive
+__device__ __forceinline__ bool sdf_normal_angle(const SceneView& s, const float* pt, float lx, float ly, float lz,
+                                                 float* nn, float* angle)
 {
-    float nn[3];
     sdf_normal(s, pt, nn);
     float ns = 1.0f / sqrtf(nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]);
     nn[0] *= ns; nn[1] *= ns; nn[2] *= ns;
-    float angle = nn[0] * lx + nn[1] * ly + nn[2] * lz;
-    return angle > 0.0f ? (unsigned char)((0.8f * angle + 0.2f) * 255.0f) : (unsigned char)0;
+    *angle = nn[0] * lx + nn[1] * ly + nn[2] * lz;
+    return *angle > 0.0f;
+}
+
+// drawPixelGrey (VisualisationEngine_Shared.hpp:272-276)
+__device__ __forceinline__ unsigned char grey_of(float angle) { return (unsigned char)((0.8f * angle + 0.2f) * 255.0f); }
+
+__device__ __forceinline__ unsigned char grey_pixel(const SceneView& s, const float* pt, float lx, float ly, float lz)
+{
+    float nn[3], angle;
+    return sdf_normal_angle(s, pt, lx, ly, lz, nn, &angle) ? grey_of(angle) : (unsigned char)0;
 }
 
 // XCD-aware tile order: consecutive image tiles land on the same XCD (and its L2)
@@ -448,28 +459,130 @@ hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm)
 
 
 
+// ---------------------------------------------------------------------------------------
+// RenderImage_common's pixel stages (VisualisationEngine_CUDA.cu:254-290) on the raycast image:
+// the five IVisualisationEngine::RenderImageType values (VisualisationEngine.hpp:15-22).
+// ---------------------------------------------------------------------------------------
+// baseCol / interpolateCol (VisualisationEngine_Shared.hpp:278-288)
+__device__ __forceinline__ float base_col(float val)
+{
+    if (val <= -0.75f) return 0.0f;
+    else if (val <= -0.25f) return (val - -0.75f) * (1.0f - 0.0f) / (-0.25f - -0.75f) + 0.0f;
+    else if (val <= 0.25f) return 1.0f;
+    else if (val <= 0.75f) return (val - 0.25f) * (0.0f - 1.0f) / (0.75f - 0.25f) + 1.0f;
+    else return 0.0f;
+}
+
+// Vector4f::toUChar: CLAMP((int)ROUND(v), 0, 255) (Vector.hpp:398-404, MathUtils.hpp:16-20)
+__device__ __forceinline__ unsigned char round_u8(float v)
+{
+    const int i = tf_round(v);
+    return (unsigned char)(i < 0 ? 0 : (i > 255 ? 255 : i));
+}
+
+// computeNormalAndAngle<useSmoothing = true, flipNormals = false> on the raycast image
+// (VisualisationEngine_Shared.hpp:205-270): +-2 neighbours, +-1 where those are missing or
+// the difference is longer than 15 cm
+__device__ __forceinline__ bool image_normal_angle(const float4* ray, int W, int H, int x, int y, float voxelSize,
+                                                   float lx, float ly, float lz, float* angle)
+{
+    if (y <= 2 || y >= H - 3 || x <= 2 || x >= W - 3) return false;
+    float4 xp = ray[(x + 2) + y * W], yp = ray[x + (y + 2) * W];
+    float4 xm = ray[(x - 2) + y * W], ym = ray[x + (y - 2) * W];
+    float dx0 = 0.f, dx1 = 0.f, dx2 = 0.f, dy0 = 0.f, dy1 = 0.f, dy2 = 0.f;
+    bool plus1 = false;
+    if (xp.w <= 0 || yp.w <= 0 || xm.w <= 0 || ym.w <= 0) plus1 = true;
+    else {
+        dx0 = xp.x - xm.x; dx1 = xp.y - xm.y; dx2 = xp.z - xm.z;
+        dy0 = yp.x - ym.x; dy1 = yp.y - ym.y; dy2 = yp.z - ym.z;
+        const float lx2 = dx0 * dx0 + dx1 * dx1 + dx2 * dx2, ly2 = dy0 * dy0 + dy1 * dy1 + dy2 * dy2;
+        const float length_diff = (lx2 < ly2) ? ly2 : lx2;                      // MAX
+        if (length_diff * voxelSize * voxelSize > (0.15f * 0.15f)) plus1 = true;
+    }
+    if (plus1) {
+        xp = ray[(x + 1) + y * W]; yp = ray[x + (y + 1) * W];
+        xm = ray[(x - 1) + y * W]; ym = ray[x + (y - 1) * W];
+        dx0 = xp.x - xm.x; dx1 = xp.y - xm.y; dx2 = xp.z - xm.z;
+        dy0 = yp.x - ym.x; dy1 = yp.y - ym.y; dy2 = yp.z - ym.z;
+        if (xp.w <= 0 || yp.w <= 0 || xm.w <= 0 || ym.w <= 0) return false;
+    }
+    float n0 = -(dx1 * dy2 - dx2 * dy1), n1 = -(dx2 * dy0 - dx0 * dy2), n2 = -(dx0 * dy1 - dx1 * dy0);
+    const float ns = 1.0f / sqrtf(n0 * n0 + n1 * n1 + n2 * n2);
+    n0 *= ns; n1 *= ns; n2 *= ns;
+    *angle = n0 * lx + n1 * ly + n2 * lz;
+    return *angle > 0.0f;
+}
+
+template <int TYPE>
 __global__ void __launch_bounds__(256)
-k_grey(SceneView s, const float4* __restrict__ ray, int n, const TfDevState* __restrict__ st, uchar4* __restrict__ out)
+k_render_type(SceneView s, const float4* __restrict__ ray, int W, int H, float voxelSize,
+              const TfDevState* __restrict__ st, uchar4* __restrict__ out)
 {
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
+    if (i >= W * H) return;
+    const int x = i % W, y = i / W;
     // lightSource = -Vector3f(pose.getColumn(2)) (VisualisationEngine_CUDA.cu:243)
     const float lx = -st->M_ray[8], ly = -st->M_ray[9], lz = -st->M_ray[10];
-    float4 p = ray[i];
-    unsigned char v = 0;
-    if (p.w > 0) {
-        float pt[3] = { p.x, p.y, p.z };
-        v = grey_pixel(s, pt, lx, ly, lz);
+    const float4 p = ray[i];
+    bool found = p.w > 0;
+    float nn[3], angle = 0.f;
+    if (TYPE == TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS) {           // processPixelGrey_ImageNormals<true,false>
+        if (found) found = image_normal_angle(ray, W, H, x, y, voxelSize, lx, ly, lz, &angle);
+        const unsigned char v = found ? grey_of(angle) : (unsigned char)0;
+        out[i] = make_uchar4(v, v, v, v);
+        return;
     }
-    out[i] = make_uchar4(v, v, v, v);
+    if (found) {
+        const float pt[3] = { p.x, p.y, p.z };
+        found = sdf_normal_angle(s, pt, lx, ly, lz, nn, &angle);
+    }
+    if (TYPE == TF_RENDER_COLOUR_FROM_NORMAL) {                      // processPixelNormal / drawPixelNormal
+        if (found) {                                                 // r, g, b; alpha is left as it was (:305-310)
+            uchar4 o = out[i];
+            o.x = (unsigned char)((0.3f + (-nn[0] + 1.0f) * 0.35f) * 255.0f);
+            o.y = (unsigned char)((0.3f + (-nn[1] + 1.0f) * 0.35f) * 255.0f);
+            o.z = (unsigned char)((0.3f + (-nn[2] + 1.0f) * 0.35f) * 255.0f);
+            out[i] = o;
+        } else {
+            out[i] = make_uchar4(0, 0, 0, 0);
+        }
+    } else if (TYPE == TF_RENDER_COLOUR_FROM_CONFIDENCE) {           // processPixelConfidence (:290-303)
+        if (found) {
+            const float conf = p.w - 1.0f;
+            const float mn = (100.f < conf) ? 100.f : conf;          // CLAMP(conf, 0, 100.f)
+            const float cn = ((0 < mn) ? mn : 0) / 100.0f;
+            const float r = (float)(unsigned char)(base_col(cn) * 255.0f);
+            const float g = (float)(unsigned char)(base_col(cn - 0.5f) * 255.0f);
+            const float b = (float)(unsigned char)(base_col(cn + 0.5f) * 255.0f);
+            const float sc = 0.8f * angle + 0.2f;
+            out[i] = make_uchar4(round_u8(sc * r), round_u8(sc * g), round_u8(sc * b), round_u8(sc * 255.0f));
+        } else {
+            out[i] = make_uchar4(0, 0, 0, 0);
+        }
+    } else {       // RENDER_SHADED_GREYSCALE; RENDER_COLOUR_FROM_VOLUME falls back to it for Voxel_s (:251-252)
+        const unsigned char v = found ? grey_of(angle) : (unsigned char)0;
+        out[i] = make_uchar4(v, v, v, v);
+    }
 }
 
-hipError_t tfk_render_grey(tf_ctx* c)
+hipError_t tfk_render_type(tf_ctx* c, int type)
 {
     SceneView s; s.hash = c->hash; s.vba = c->vba; s.grid = c->bgrid; s.mask = (unsigned)(c->p.n_buckets - 1); s.n_buckets = c->p.n_buckets;
-    int n = c->W * c->H;
-    hipLaunchKernelGGL(k_grey, dim3((n + 255) / 256), dim3(256), 0, c->stream, s, (const float4*)c->raycast, n, c->st, c->grey);
+    const int n = c->W * c->H;
+    const dim3 g((n + 255) / 256), b(256);
+    const float4* ray = (const float4*)c->raycast;
+    const float vs = c->p.voxelSize;
+    switch (type) {
+    case TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS:
+        hipLaunchKernelGGL(k_render_type<TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey); break;
+    case TF_RENDER_COLOUR_FROM_NORMAL:
+        hipLaunchKernelGGL(k_render_type<TF_RENDER_COLOUR_FROM_NORMAL>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey); break;
+    case TF_RENDER_COLOUR_FROM_CONFIDENCE:
+        hipLaunchKernelGGL(k_render_type<TF_RENDER_COLOUR_FROM_CONFIDENCE>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey); break;
+    default:
+        hipLaunchKernelGGL(k_render_type<TF_RENDER_SHADED_GREYSCALE>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey); break;
+    }
     return hipGetLastError();
 }
 

@@ -91,9 +91,12 @@ class TopFu:
                 "tf_process_frames")
         return ok.astype(bool)
 
-    def renderImage(self):
-        """TopFu::renderImage -> uint8 (rows, cols, 4) grey image (host copy)."""
-        L.check(L.load().tf_render_image(self._h, None, 0), "tf_render_image")
+    def renderImage(self, type=0):
+        """TopFu::renderImage -> uint8 (rows, cols, 4) image (host copy).  type: the reference's
+        IVisualisationEngine::RenderImageType (0 shaded greyscale = TopFu::renderImage, 1 greyscale
+        from image normals, 2 colour from volume (greyscale for Voxel_s), 3 colour from normal,
+        4 colour from confidence)."""
+        L.check(L.load().tf_render_image_type(self._h, int(type), None, 0), "tf_render_image_type")
         return self.download(L.TF_BUF_GREY).view(np.uint8).reshape(self.H, self.W, 4)
 
     def frame_grey(self):
