@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample length")
     ap.add_argument("--no-profile", action="store_true", help="disable the per-stage HIP-event timing")
+    ap.add_argument("--profile-every", type=int, default=16,
+                    help="timed region: HIP events around the dominant kernel on every N-th frame only "
+                         "(an event pair is a few us of dispatch gap; 1 = every frame)")
     ap.add_argument("--breakdown-frames", type=int, default=60, help="frames of the per-stage timing pass")
     return ap.parse_args()
 
@@ -252,9 +255,10 @@ def main():
             avg = {k: pw[k][0] / pw[k][1] for k in single if pw[k][1]}
             if avg:
                 dominant = max(avg, key=avg.get)
-    # timed region: HIP events only around the dominant kernel's stage (each timed stage costs
-    # GPU time; the full per-stage breakdown comes from a separate pass below)
-    tf.profile(not args.no_profile, stages=[dominant])
+    # timed region: HIP events only around the dominant kernel's stage, on every
+    # --profile-every-th frame (an event pair costs a few us of dispatch gap; the full per-stage
+    # breakdown comes from a separate pass below)
+    tf.profile(not args.no_profile, stages=[dominant], every=args.profile_every)
     resets_before = tf.stats()["n_resets"]
     torch.cuda.synchronize()
     if world > 1:
@@ -314,7 +318,8 @@ def main():
                                "traffic": (pmc.get(k) or {}).get("bytes_per_launch"),
                                "kernel": KERNEL_OF_STAGE[k], "algorithmic_bytes_per_launch": b,
                                "avg_launch_ms": round(ms, 5),
-                               "timing": "HIP events in the timed region" if (k == dominant and timed_ms)
+                               "timing": (f"HIP events around every {args.profile_every}-th launch of the timed region "
+                                          f"({prof_timed[k][1]} launches)") if (k == dominant and timed_ms)
                                          else "HIP events in the breakdown pass"}
             if dominant in roof_all:
                 roof = roof_all[dominant]

@@ -201,6 +201,10 @@ tf_status tf_profile_enable(tf_ctx* ctx, int enable);
  * adds two event records per frame to the stream, which cost GPU time of their own, so a
  * throughput measurement times only the stage it needs. */
 tf_status tf_profile_stages(tf_ctx* ctx, unsigned mask);
+/* time only every `period`-th frame enqueued from now on (1 = every frame, the default after
+ * tf_profile_enable / tf_profile_stages): a throughput run keeps its stage timing live while
+ * all but 1/period of its frames carry no events */
+tf_status tf_profile_sample(tf_ctx* ctx, int period);
 tf_status tf_profile_reset(tf_ctx* ctx);
 /* ms[i] = accumulated milliseconds, counts[i] = frames measured, for i < n (n <= 9) */
 tf_status tf_profile_read(tf_ctx* ctx, double* ms, long long* counts, int n);

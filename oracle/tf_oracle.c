@@ -60,7 +60,9 @@ float tfo_exp(float x)
     return ldexpf(p, (int)k);
 }
 
-/* fixed-polynomial double sin/cos (replaces std::sin/cos in cv::Affine3 Rodrigues) */
+/* fixed-polynomial double sin/cos (replaces std::sin/cos in cv::Affine3 Rodrigues).  Horner
+   over 13 terms; for |r| < 1/8 (every ICP increment in practice) 6 terms, whose first omitted
+   term is below 2^-80 relative */
 static const double k_inv_sin[14] = { 0.0, 1.0/6.0, 1.0/20.0, 1.0/42.0, 1.0/72.0, 1.0/110.0, 1.0/156.0,
     1.0/210.0, 1.0/272.0, 1.0/342.0, 1.0/420.0, 1.0/506.0, 1.0/600.0, 1.0/702.0 };
 static const double k_inv_cos[14] = { 0.0, 1.0/2.0, 1.0/12.0, 1.0/30.0, 1.0/56.0, 1.0/90.0, 1.0/132.0,
@@ -76,7 +78,8 @@ void tfo_sincos(double th, double* s, double* c)
     }
     double r2 = r * r;
     double ps = 1.0, pc = 1.0;
-    for (int n = 13; n >= 1; --n) {
+    const int nt = r2 < 0.015625 ? 6 : 13;
+    for (int n = nt; n >= 1; --n) {
         ps = 1.0 - (r2 * k_inv_sin[n]) * ps;
         pc = 1.0 - (r2 * k_inv_cos[n]) * pc;
     }
@@ -452,31 +455,35 @@ static double cv_det6(const float Ain[36])
     return det;
 }
 
-/* cv::solve(A, b, DECOMP_SVD) -> Gaussian elimination with partial pivoting in double */
+/* cv::solve(A, b, DECOMP_SVD) replacement.  A is the symmetric normal matrix J^T J, already
+   past the determinant check: LDL^T in double (lower triangle of A, one reciprocal per pivot),
+   then forward, diagonal and backward substitution.  Few dependent operations -- the GPU runs
+   this on one wave between two iterations (tf_icp.hip: icp_solve6_ldl, same operation order) */
 static void solve6(const float Af[36], const float bf[6], float x[6])
 {
-    double A[36], b[6];
-    for (int i = 0; i < 36; ++i) A[i] = Af[i];
-    for (int i = 0; i < 6; ++i) b[i] = bf[i];
-    for (int i = 0; i < 6; ++i) {
-        int k = i;
-        for (int j = i + 1; j < 6; ++j) if (fabs(A[j * 6 + i]) > fabs(A[k * 6 + i])) k = j;
-        if (k != i) {
-            for (int j = 0; j < 6; ++j) { double t = A[i * 6 + j]; A[i * 6 + j] = A[k * 6 + j]; A[k * 6 + j] = t; }
-            double t = b[i]; b[i] = b[k]; b[k] = t;
-        }
-        double piv = A[i * 6 + i];
-        for (int j = i + 1; j < 6; ++j) {
-            double l = A[j * 6 + i] / piv;
-            for (int c = i; c < 6; ++c) A[j * 6 + c] = A[j * 6 + c] - l * A[i * 6 + c];
-            b[j] = b[j] - l * b[i];
+    double L[36], d[6], r[6], y[6], xs[6];
+    for (int j = 0; j < 6; ++j) {
+        double w[6];
+        for (int k = 0; k < j; ++k) w[k] = L[j * 6 + k] * d[k];
+        double dj = Af[j * 6 + j];
+        for (int k = 0; k < j; ++k) dj = dj - L[j * 6 + k] * w[k];
+        d[j] = dj;
+        r[j] = 1.0 / dj;
+        for (int i = j + 1; i < 6; ++i) {
+            double s = Af[i * 6 + j];
+            for (int k = 0; k < j; ++k) s = s - L[i * 6 + k] * w[k];
+            L[i * 6 + j] = s * r[j];
         }
     }
-    double xs[6];
+    for (int i = 0; i < 6; ++i) {
+        double s = bf[i];
+        for (int k = 0; k < i; ++k) s = s - L[i * 6 + k] * y[k];
+        y[i] = s;
+    }
     for (int i = 5; i >= 0; --i) {
-        double s = b[i];
-        for (int c = i + 1; c < 6; ++c) s = s - A[i * 6 + c] * xs[c];
-        xs[i] = s / A[i * 6 + i];
+        double s = y[i] * r[i];
+        for (int k = i + 1; k < 6; ++k) s = s - L[k * 6 + i] * xs[k];
+        xs[i] = s;
     }
     for (int i = 0; i < 6; ++i) x[i] = (float)xs[i];
 }

@@ -107,6 +107,7 @@ def load():
         "tf_time_stage": ([P, I, P, I, ctypes.POINTER(ctypes.c_float)], I),
         "tf_profile_enable": ([P, I], I),
         "tf_profile_stages": ([P, ctypes.c_uint], I),
+        "tf_profile_sample": ([P, I], I),
         "tf_profile_reset": ([P], I),
         "tf_profile_read": ([P, P, P, I], I),
     }

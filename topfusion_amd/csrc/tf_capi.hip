@@ -162,6 +162,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (!c) return TF_OOM;
     memset((void*)c, 0, sizeof(*c));
     c->p = *pin;
+    c->prof_period = 1;
     hipError_t e = hipGetDevice(&c->device);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     c->W = pin->cols; c->H = pin->rows;
@@ -320,7 +321,7 @@ static void swap_pyramids(tf_ctx* c)
 // sync, once their mode / ok flags are known, and only for the stages that did work.
 #define STAGE_ON(strm, id, expr)                                                              \
     do {                                                                                      \
-        const bool timed_ = c->prof_enabled && ((c->prof_mask >> (id)) & 1u);                 \
+        const bool timed_ = c->prof_slot_on[slot] && ((c->prof_mask >> (id)) & 1u);          \
         if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id)), (strm)));          \
         TF_CHECK(expr);                                                                       \
         if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id) + 1), (strm)));      \
@@ -347,7 +348,7 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
     if (!c->prof_enabled) return TF_OK;
     for (int f = 0; f < n; ++f)
         for (int i = 0; i < TF_NUM_STAGES; ++i) {
-            if (!((c->prof_mask >> i) & 1u) || !stage_ran(i, mode[f], ok[f])) continue;
+            if (!c->prof_slot_on[first + f] || !((c->prof_mask >> i) & 1u) || !stage_ran(i, mode[f], ok[f])) continue;
             if (i == TF_STAGE_RAYCAST_RENDER && c->render_mode == 3) continue;   // fused into RAYCAST_ICP
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, prof_event(c, first + f, 2 * i), prof_event(c, first + f, 2 * i + 1)) == hipSuccess) {
@@ -365,12 +366,15 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
 // it (frame counters, per-slot ok flag).  A batch is therefore enqueued back to back.
 static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, int slot)
 {
+    c->prof_slot_on[slot] = c->prof_enabled && (c->prof_seq++ % c->prof_period) == 0;
     // preprocessing (topfu.cpp:166-197).  (Measured: on a stream of its own, overlapping the
     // previous frame's tail, the cross-stream waits cost more than the overlap saves.)
     STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, c->stream));
     STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1));                           // frame begin + topfu.cpp:242-243 (tracking only)
     // the previous frame's renderImage (render stream) must be done before the scene changes
-    TF_CHECK(join_render(c));
+    // (modes 2 and 3 render on the main stream: no wait -- an event wait is a barrier packet,
+    // a few microseconds of dispatch gap even when the event has long completed)
+    if (c->render_mode <= 1) TF_CHECK(join_render(c));
     STAGE(TF_STAGE_ALLOC, tfk_alloc(c, 1));                          // topfu.cpp:202 / 281 (+ renderImage snapshot)
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1));                  // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
     // renderImage (raycast + grey, topfu.cpp:284-285) on the render stream, behind integration;
@@ -428,6 +432,8 @@ extern "C" tf_status tf_profile_enable(tf_ctx* c, int enable)
     }
     c->prof_enabled = enable ? 1 : 0;
     c->prof_mask = (1u << TF_NUM_STAGES) - 1;
+    c->prof_period = 1;
+    c->prof_seq = 0;
     return TF_OK;
 }
 
@@ -437,6 +443,14 @@ extern "C" tf_status tf_profile_stages(tf_ctx* c, unsigned mask)
     tf_status s = tf_profile_enable(c, mask != 0);
     if (s != TF_OK) return s;
     c->prof_mask = mask;
+    return TF_OK;
+}
+
+extern "C" tf_status tf_profile_sample(tf_ctx* c, int period)
+{
+    if (!c || period < 1) return TF_INVALID_ARG;
+    c->prof_period = period;
+    c->prof_seq = 0;
     return TF_OK;
 }
 

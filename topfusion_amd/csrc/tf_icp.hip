@@ -146,10 +146,18 @@ __device__ __forceinline__ void icp_sincos(double th, double* s, double* c)
     }
     double r2 = r * r;
     double ps = 1.0, pc = 1.0;
+    if (r2 < 0.015625) {                // |r| < 1/8: 6 terms, first omitted term < 2^-80 relative
 #pragma unroll
-    for (int n = 13; n >= 1; --n) {
-        ps = 1.0 - (r2 * inv_sin[n]) * ps;
-        pc = 1.0 - (r2 * inv_cos[n]) * pc;
+        for (int n = 6; n >= 1; --n) {
+            ps = 1.0 - (r2 * inv_sin[n]) * ps;
+            pc = 1.0 - (r2 * inv_cos[n]) * pc;
+        }
+    } else {
+#pragma unroll
+        for (int n = 13; n >= 1; --n) {
+            ps = 1.0 - (r2 * inv_sin[n]) * ps;
+            pc = 1.0 - (r2 * inv_cos[n]) * pc;
+        }
     }
     *s = r * ps;
     *c = pc;
@@ -223,49 +231,44 @@ __device__ __forceinline__ double icp_det6_reg(const float (&A0)[6][6])
     return det;
 }
 
-// cv::solve(A, b, DECOMP_SVD) replacement: Gaussian elimination with partial pivoting in
-// double, back substitution in the serial order (oracle/tf_oracle.c:solve6)
-__device__ __forceinline__ void icp_solve6_reg(const float (&Af)[6][6], const float (&bf)[6], float (&x)[6])
+// cv::solve(A, b, DECOMP_SVD) replacement (oracle/tf_oracle.c:solve6, same operation order):
+// LDL^T of the symmetric normal matrix in double with one reciprocal per pivot, then forward,
+// diagonal and backward substitution -- ~270 uniform operations with short dependency chains
+// (the pivoting elimination it replaces issued ~2.5x as many, 21 of them full divisions)
+__device__ __forceinline__ void icp_solve6_ldl(const float (&Af)[6][6], const float (&bf)[6], float (&x)[6])
 {
-    double A[6][6], b[6];
+    double L[6][6], d[6], r[6], y[6], xs[6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        b[i] = bf[i];
+    for (int j = 0; j < 6; ++j) {
+        double w[6];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) A[i][j] = Af[i][j];
-    }
+        for (int k = 0; k < j; ++k) w[k] = L[j][k] * d[k];
+        double dj = Af[j][j];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        double best = fabs(A[i][i]);
-        int k = i;
+        for (int k = 0; k < j; ++k) dj = dj - L[j][k] * w[k];
+        d[j] = dj;
+        r[j] = 1.0 / dj;
 #pragma unroll
-        for (int j = i + 1; j < 6; ++j) { double v = fabs(A[j][i]); if (v > best) { best = v; k = j; } }
-        k = __builtin_amdgcn_readfirstlane(k);          // uniform: swaps become scalar branches
-        if (k != i) {
+        for (int i = j + 1; i < 6; ++i) {
+            double sacc = Af[i][j];
 #pragma unroll
-            for (int r = i + 1; r < 6; ++r)
-                if (r == k) {
-#pragma unroll
-                    for (int c = 0; c < 6; ++c) { double t = A[i][c]; A[i][c] = A[r][c]; A[r][c] = t; }
-                    double t = b[i]; b[i] = b[r]; b[r] = t;
-                }
-        }
-        double piv = A[i][i];
-#pragma unroll
-        for (int j = i + 1; j < 6; ++j) {
-            double l = A[j][i] / piv;
-#pragma unroll
-            for (int c = i; c < 6; ++c) A[j][c] = A[j][c] - l * A[i][c];
-            b[j] = b[j] - l * b[i];
+            for (int k = 0; k < j; ++k) sacc = sacc - L[i][k] * w[k];
+            L[i][j] = sacc * r[j];
         }
     }
-    double xs[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double sacc = bf[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) sacc = sacc - L[i][k] * y[k];
+        y[i] = sacc;
+    }
 #pragma unroll
     for (int i = 5; i >= 0; --i) {
-        double sacc = b[i];
+        double sacc = y[i] * r[i];
 #pragma unroll
-        for (int c = i + 1; c < 6; ++c) sacc = sacc - A[i][c] * xs[c];
-        xs[i] = sacc / A[i][i];
+        for (int k = i + 1; k < 6; ++k) sacc = sacc - L[k][i] * xs[k];
+        xs[i] = sacc;
     }
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = (float)xs[i];
@@ -407,7 +410,7 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
         return;
     }
     float rv[6];
-    icp_solve6_reg(Am, bv, rv);
+    icp_solve6_ldl(Am, bv, rv);
     ICP_TS(5);
     float R[9], tinc[12], A[12];
     icp_rodrigues(rv, R);
@@ -455,6 +458,7 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 #define IP_PART (IP_BCAST + 16)                  // SCHED 2: 8 residue-class partials, double-buffered
 #define IP_NPART 8                               // residue classes of the final tree's first five steps
 #define IP_LDS_PAD (56 * 1024)
+#define IP_DETW (IP_WAVES - 1)                   // SCHED 3: the wave that runs the det check off the critical path
 
 struct IcpFrameArgs {
     IcpLevel lv[TF_LEVELS];             // in processing order (coarse -> fine)
@@ -640,6 +644,12 @@ k_icp_frame(IcpFrameArgs a)
     for (int i = 0; i < 12; ++i) aff[i] = (i % 5 == 0) ? 1.0f : 0.0f;     // affine = Identity
     int status = 1, done = 0;
     float last_sums = 0.f;
+    // SCHED 3 runs the det check (projective_icp.cpp:197-203) of iteration k on wave IP_DETW
+    // while iteration k+1 computes its rows, and settles it before anything of k+1 is
+    // published: on failure the affine of k-1 is restored and the loop ends exactly where the
+    // serial order ends it.  The solve (wave 0) is the only serial work between two iterations.
+    float aff_prev[12], det_sm[27];
+    bool det_pending = false;
 
 #pragma unroll 1
     for (int li = 0; li < a.nlev && status == 1; ++li) {
@@ -672,6 +682,13 @@ k_icp_frame(IcpFrameArgs a)
         for (int it = 0; it < iters; ++it) {
             ++gen;
             IPT_REC(done, wg);
+            if (SCHED == 3 && det_pending && wave == IP_DETW) {
+                float Am[6][6], bv[6];
+                ip_unpack(det_sm, Am, bv);
+                const double det = icp_det6_reg(Am);
+                if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
+                IPT_REC_T(done - 1, 2 * ICP_NWG + 5, 64 * IP_DETW);
+            }
             // ---- per-CTA reductions -> column sum of this workgroup -> tagged slot
 #pragma unroll
             for (int rr = 0; rr < IP_SREG; ++rr) {
@@ -707,6 +724,15 @@ k_icp_frame(IcpFrameArgs a)
                 if (!(lane & 1) && (lane >> 1) < 27) red[sl][lane >> 1] = tot;
             }
             __syncthreads();
+            if (SCHED == 3 && det_pending) {                      // settle iteration k's det check
+                det_pending = false;
+                if (!det_ok_s) {
+                    status = 0;
+#pragma unroll
+                    for (int i = 0; i < 12; ++i) aff[i] = aff_prev[i];
+                    break;
+                }
+            }
             if (tid < 27) {
                 float sum = 0.f;                                   // 0 + P[w] + P[w+256] + ...
                 for (int sl = 0; sl < slots; ++sl) {
@@ -769,10 +795,10 @@ k_icp_frame(IcpFrameArgs a)
                     }
                     tv[q][x] = __uint_as_float((unsigned)v);
                 }
-                if (tid == 0) det_ok_s = 1;
+                if (SCHED == 2 && tid == 0) det_ok_s = 1;
                 const int any_timeout = __syncthreads_or(timeout);
                 IPT_REC(done, 2 * ICP_NWG + 0);
-                if (!any_timeout && wave < 2) {
+                if (!any_timeout && (SCHED == 3 ? (wave == 0 || wave == IP_DETW) : wave < 2)) {
                     // steps 4, 2, 1: ((P0+P4) + (P2+P6)) + ((P1+P5) + (P3+P7)); lane q holds sum q
                     float tot = 0.f;
                     if (lane < 27) {
@@ -785,13 +811,16 @@ k_icp_frame(IcpFrameArgs a)
                         sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), q));
                     ip_unpack(sm, Am, bv);
                     IPT_REC(done, 2 * ICP_NWG + 2);
-                    if (wave == 1) {                                   // det on its own wave
+                    if (SCHED == 3 && wave == IP_DETW) {               // det after the barrier
+#pragma unroll
+                        for (int q = 0; q < 27; ++q) det_sm[q] = sm[q];
+                    } else if (SCHED == 2 && wave == 1) {              // det on its own wave
                         const double det = icp_det6_reg(Am);           // projective_icp.cpp:197-203
                         if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
                         IPT_REC_T(done, 2 * ICP_NWG + 5, 64);
                     } else {                                           // solve -> Rodrigues -> compose
                         float rv[6], R[9], tinc[12];
-                        icp_solve6_reg(Am, bv, rv);                     // projective_icp.cpp:206-209
+                        icp_solve6_ldl(Am, bv, rv);                     // projective_icp.cpp:206-209
                         IPT_REC(done, 2 * ICP_NWG + 3);
                         icp_rodrigues(rv, R);
 #pragma unroll
@@ -810,7 +839,14 @@ k_icp_frame(IcpFrameArgs a)
                 }
                 __syncthreads();
                 IPT_REC(done, 2 * ICP_NWG + 1);
-                status = any_timeout ? 2 : (det_ok_s ? 1 : 0);
+                if (SCHED == 3) {
+                    status = any_timeout ? 2 : 1;
+                    det_pending = !any_timeout;
+#pragma unroll
+                    for (int i = 0; i < 12; ++i) aff_prev[i] = aff[i];
+                } else {
+                    status = any_timeout ? 2 : (det_ok_s ? 1 : 0);
+                }
                 if (SCHED == 2 && wave == 0 && lane <= 12) {           // broadcast affine + status
                     const float v = lane < 12 ? aff_s[lane] : (float)status;
                     ip_store(&tag[IP_BCAST + lane], ip_pack(gen, v));
@@ -867,7 +903,7 @@ k_icp_frame(IcpFrameArgs a)
                         ip_final_tree(tv, lane, sm);
                         ip_unpack(sm, Am, bv);
                         IPT_REC(done, 2 * ICP_NWG + 2);
-                        icp_solve6_reg(Am, bv, rv);                     // projective_icp.cpp:206-209
+                        icp_solve6_ldl(Am, bv, rv);                     // projective_icp.cpp:206-209
                         IPT_REC(done, 2 * ICP_NWG + 3);
                         icp_rodrigues(rv, R);
 #pragma unroll
@@ -928,6 +964,20 @@ k_icp_frame(IcpFrameArgs a)
             ++done;
             if (status != 1) break;
             __syncthreads();                       // red[] / aff_s reuse in the next iteration
+        }
+    }
+    if (SCHED == 3 && det_pending) {                              // the last iteration's det check
+        if (wave == IP_DETW) {
+            float Am[6][6], bv[6];
+            ip_unpack(det_sm, Am, bv);
+            const double det = icp_det6_reg(Am);
+            if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
+        }
+        __syncthreads();
+        if (!det_ok_s) {
+            status = 0;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) aff[i] = aff_prev[i];
         }
     }
     // ---- workgroup 0 records the frame's ICP result

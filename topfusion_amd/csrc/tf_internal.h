@@ -269,6 +269,9 @@ struct tf_ctx {
     // per-stage HIP-event timing on the context stream (tf_profile_*)
     int prof_enabled;
     unsigned prof_mask;      // stages timed (bit = tf_stage_id)
+    int prof_period;         // time every prof_period-th enqueued frame (1 = every frame)
+    long long prof_seq;      // frames enqueued since profiling was configured
+    unsigned char prof_slot_on[TF_PROF_RING];   // batch slot carries stage events
     hipEvent_t prof_ev[2 * TF_NUM_STAGES * TF_PROF_RING];
     double prof_ms[TF_NUM_STAGES];
     long long prof_count[TF_NUM_STAGES];

@@ -128,9 +128,9 @@ class TopFu:
         return bool(v.value)
 
     # -- per-stage HIP-event timing ----------------------------------------------------
-    def profile(self, enable=True, stages=None):
+    def profile(self, enable=True, stages=None, every=1):
         """Time every stage (enable=True), none, or only the named stages (HIP events on the
-        context stream; each timed stage costs GPU time of its own)."""
+        context stream; each timed stage costs GPU time of its own), on every `every`-th frame."""
         if stages is None:
             L.check(L.load().tf_profile_enable(self._h, int(enable)), "tf_profile_enable")
         else:
@@ -138,6 +138,7 @@ class TopFu:
             for s in stages:
                 mask |= 1 << L.STAGE_NAMES.index(s)
             L.check(L.load().tf_profile_stages(self._h, mask if enable else 0), "tf_profile_stages")
+        L.check(L.load().tf_profile_sample(self._h, int(every)), "tf_profile_sample")
         L.check(L.load().tf_profile_reset(self._h), "tf_profile_reset")
 
     def profile_read(self):
