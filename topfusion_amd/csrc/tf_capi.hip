@@ -90,7 +90,7 @@ static bool params_valid(const tf_params* p)
 static void ctx_free(tf_ctx* c)
 {
     if (!c) return;
-    void* bufs[] = { c->hash, c->excessList, c->vba, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
+    void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockBox, c->blockZ, c->blockTiles, c->blockOff, c->edChunk, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->frame_ok, c->frame_mode };
@@ -186,7 +186,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     ALLOC(c->hash, sizeof(TfHashEntry) * (size_t)c->n_total);
     ALLOC(c->excessList, sizeof(int) * (size_t)pin->n_excess);
-    ALLOC(c->vba, sizeof(TfVoxel) * (size_t)pin->n_blocks * TF_BLK3);
+    ALLOC(c->vba_guard, sizeof(TfVoxel) * ((size_t)pin->n_blocks + 1) * TF_BLK3);
+    c->vba = c->vba_guard + TF_BLK3;
     ALLOC(c->allocList, sizeof(int) * (size_t)pin->n_blocks);
     ALLOC(c->bgrid, sizeof(int2) * (size_t)TF_GRID_DIM * TF_GRID_DIM * TF_GRID_DIM);
     ALLOC(c->allocType, ntot_pad);
@@ -237,7 +238,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     s0.icp_ok = 1;
     e = hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_ticket, 0, 64, c->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(c->bgrid, 0xff, sizeof(int2) * (size_t)TF_GRID_DIM * TF_GRID_DIM * TF_GRID_DIM, c->stream);
+    if (e == hipSuccess) e = tfk_grid_clear(c);
+    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)c->vba_guard, 0x7fff, TF_BLK3, c->stream);   // Voxel_s()
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_tagged, 0, sizeof(unsigned long long) * TF_ICP_TAG_WORDS, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->allocType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->winnerKey, 0xff, sizeof(int) * ntot_pad, c->stream);

@@ -151,6 +151,22 @@ __device__ __forceinline__ float tf_short_to_float(int s)
     return fmaf(fmaf(-q0, 32767.0f, x), r, q0);
 }
 
+// x / 32767.0f for any float |x| < 2^21 (the SDF interpolation and gradient divisions), IEEE-
+// exact in three operations: q0 = x * RN(1/32767), e = fma(q0, 32767, -x), q = fma(-e, RN(1/32767),
+// q0).  Checked against the division for every float below 2^21 in magnitude, both signs,
+// zeros and denormals included (tools/check_div32767.c; tests/test_oracle.py samples it).
+__device__ __forceinline__ float tf_div32767(float x)
+{
+    const float r = 1.0f / 32767.0f;
+    const float q0 = x * r;
+    return fmaf(-fmaf(q0, 32767.0f, -x), r, q0);
+}
+
+// A missing block's VBA offset in the block grid: the render side reads voxels relative to a
+// guard block of Voxel_s() values placed just before the VBA (tf_ctx::vba_guard), so a voxel
+// load needs no "is the block there" select -- it lands in the guard and reads (32767, 0).
+#define TF_VOFF_NONE (-TF_BLK3)
+
 // Block grid: a dense TF_GRID_DIM^3 array over block coordinates [-HALF, HALF) holding, for
 // every block findVoxel would find, (hash entry index, VBA voxel offset = ptr*512), else
 // (-1,-1).  It mirrors the hash exactly (written wherever a block is allocated, cleared on
@@ -220,6 +236,7 @@ struct tf_ctx {
     TfHashEntry* hash;
     int* excessList;
     TfVoxel* vba;
+    TfVoxel* vba_guard;      // allocation: one guard block of Voxel_s() (TF_VOFF_NONE reads), then vba
     int* allocList;
     int2* bgrid;             // block grid (TF_GRID_*), mirrors the hash
     // SceneReconstructionEngine temporaries
@@ -287,6 +304,7 @@ hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / ray
 hipError_t tfk_reset_scene(tf_ctx* c);
 hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot);   // frame end + ResetScene if ICP failed
 hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a hash upload)
+hipError_t tfk_grid_clear(tf_ctx* c);     // every cell (-1, TF_VOFF_NONE)
 hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0);   // snapshot: + the frame's renderImage snapshot
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);

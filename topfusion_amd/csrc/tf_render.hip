@@ -13,13 +13,15 @@
 
 struct SceneView {
     const TfHashEntry* hash;
-    const TfVoxel* vba;
+    const TfVoxel* vba;      // the guard block before the VBA (tf_ctx::vba_guard): voxel offsets are voff + TF_BLK3 + lin
     const int2* grid;        // block grid (tf_internal.h, TF_GRID_*)
     unsigned mask;
     int n_buckets;
 };
 
-struct RCache { int bx, by, bz, voff; };   // VoxelBlockHash::IndexCache (VoxelBlockHash.hpp:58-62)
+// VoxelBlockHash::IndexCache (VoxelBlockHash.hpp:58-62): the cached block position decides castRay's
+// visibility marks; the cached pointer is never needed (voxels are read through the grid)
+struct RCache { int bx, by, bz; };
 
 // ---------------------------------------------------------------------------------------
 // Voxel access through the block grid.  readVoxel (RepresentationAccess.hpp:73-104) walks a
@@ -50,53 +52,67 @@ __device__ __forceinline__ int2 blk_walk(const SceneView& s, int bx, int by, int
     while (true) {
         const TfHashEntry e = s.hash[hi];
         if (e.x == (short)bx && e.y == (short)by && e.z == (short)bz && e.ptr >= 0) return make_int2(hi, e.ptr * TF_BLK3);
-        if (e.offset < 1) return make_int2(-1, -1);
+        if (e.offset < 1) return make_int2(-1, TF_VOFF_NONE);
         hi = s.n_buckets + e.offset - 1;
     }
 }
 
-// Lookups of the 2x2x2 block set {X[i]} x {Y[j]} x {Z[k]} (corner c = i + 2j + 4k), returning
-// (hash entry index, VBA voxel offset) per corner, or (-1,-1) when findVoxel fails.  Every grid
-// load is issued unconditionally (a cell outside the grid loads cell 0 and is replaced by the
-// hash walk afterwards), so the eight loads are in flight together: one memory round trip.
+// Cell byte offsets of the 2x2x2 block set {X[i]} x {Y[j]} x {Z[k]} (corner c = i + 2j + 4k;
+// X[1] - X[0] etc. are 0 or 1): the base cell's plus the per-axis steps.  False when a block lies
+// outside the grid (then the offsets are meaningless and blk_lookup_slow answers).
+__device__ __forceinline__ bool blk_offsets8(const int (&X)[2], const int (&Y)[2], const int (&Z)[2], unsigned (&o)[8])
+{
+    const unsigned x0 = (unsigned)(X[0] + TF_GRID_HALF), y0 = (unsigned)(Y[0] + TF_GRID_HALF), z0 = (unsigned)(Z[0] + TF_GRID_HALF);
+    const unsigned x1 = (unsigned)(X[1] + TF_GRID_HALF), y1 = (unsigned)(Y[1] + TF_GRID_HALF), z1 = (unsigned)(Z[1] + TF_GRID_HALF);
+    const unsigned base = ((z0 << (2 * TF_GRID_LOG)) | (y0 << TF_GRID_LOG) | x0) * 8u;
+    const unsigned dx = (x1 - x0) * 8u, dy = (y1 - y0) << (TF_GRID_LOG + 3), dz = (z1 - z0) << (2 * TF_GRID_LOG + 3);
+    o[0] = base; o[1] = base + dx; o[2] = base + dy; o[3] = o[1] + dy;
+    o[4] = base + dz; o[5] = o[1] + dz; o[6] = o[2] + dz; o[7] = o[3] + dz;
+    return (x0 | x1 | y0 | y1 | z0 | z1) < (unsigned)TF_GRID_DIM;
+}
+// (hash entry index, VBA voxel offset) per corner, or (-1, TF_VOFF_NONE) when findVoxel fails
+__device__ __forceinline__ void blk_load8(const SceneView& s, const unsigned (&o)[8], int2 (&g)[8])
+{
+#pragma unroll
+    for (int c = 0; c < 8; ++c) g[c] = ld_off<int2>(s.grid, o[c]);
+}
+// the rare case (a block outside the grid, i.e. beyond +-128 blocks): cell or hash walk per corner.
+// Callers take it for the whole wave, so the common path's loads stay unbranched and in flight
+// together.
+__device__ __forceinline__ void blk_lookup_slow(const SceneView& s, const int (&X)[2], const int (&Y)[2], const int (&Z)[2],
+                                             int2 (&g)[8])
+{
+    for (int c = 0; c < 8; ++c) {
+        const int bx = X[c & 1], by = Y[(c >> 1) & 1], bz = Z[c >> 2];
+        g[c] = tf_grid_in(bx, by, bz) ? s.grid[tf_grid_cell(bx, by, bz)] : blk_walk(s, bx, by, bz);
+    }
+}
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
 __device__ __forceinline__ void blk_find8(const SceneView& s, const int (&X)[2], const int (&Y)[2], const int (&Z)[2],
                                           int (&hidx)[8], int (&voff)[8])
 {
-    unsigned gx[2], gy[2], gz[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        gx[i] = (unsigned)(X[i] + TF_GRID_HALF); gy[i] = (unsigned)(Y[i] + TF_GRID_HALF); gz[i] = (unsigned)(Z[i] + TF_GRID_HALF);
-    }
-    bool in[8];
+    unsigned o[8];
     int2 g[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const unsigned x = gx[c & 1], y = gy[(c >> 1) & 1], z = gz[c >> 2];
-        in[c] = (x | y | z) < (unsigned)TF_GRID_DIM;
-        const unsigned cell = (z << (2 * TF_GRID_LOG)) | (y << TF_GRID_LOG) | x;
-        g[c] = ld_off<int2>(s.grid, (in[c] ? cell : 0u) * 8u);
-    }
-    bool all_in = true;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) all_in = all_in && in[c];
-    if (!all_in) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-            if (!in[c]) g[c] = blk_walk(s, X[c & 1], Y[(c >> 1) & 1], Z[c >> 2]);
-    }
+    const bool in = blk_offsets8(X, Y, Z, o);
+    if (wave_any(!in)) blk_lookup_slow(s, X, Y, Z, g);
+    else blk_load8(s, o, g);
 #pragma unroll
     for (int c = 0; c < 8; ++c) { hidx[c] = g[c].x; voff[c] = g[c].y; }
 }
 
-// raw Voxel_s word (sdf = low 16 bits, w = bits 16-23); unallocated -> Voxel_s() = (32767, 0).
-// The load is unconditional (voxel 0 when the block is missing) so neighbouring reads batch;
-// VBA byte offsets fit 32 bits (<= 2^21 blocks x 2 KiB).
-__device__ __forceinline__ unsigned vox_raw(const SceneView& s, int voff, int x, int y, int z)
+// raw Voxel_s word (sdf = low 16 bits, w = bits 16-23) of voxel `lin` of the block at VBA offset
+// voff, read relative to the guard block before the VBA (SceneView::vba): a missing block
+// (voff = TF_VOFF_NONE) reads the guard's Voxel_s() = (32767, 0).  Byte offsets fit 32 bits
+// (<= 2^21 blocks x 2 KiB).
+__device__ __forceinline__ unsigned vox_at(const SceneView& s, int voff, int lin_g)
 {
-    const unsigned off = (unsigned)((voff + vlin(x, y, z)) & ~(voff >> 31));   // voxel 0 when voff < 0 (no branch)
-    const unsigned r = ld_off<unsigned>(s.vba, off * 4u);
-    return voff >= 0 ? r : 0x7fffu;
+    return ld_off<unsigned>(s.vba, (unsigned)(voff + lin_g) * 4u);
 }
+// in-block index of voxel coordinate p along one axis, pre-scaled; the guard shift rides on z
+__device__ __forceinline__ int lin_x(int x) { return x & 7; }
+__device__ __forceinline__ int lin_y(int y) { return (y & 7) << 3; }
+__device__ __forceinline__ int lin_zg(int z) { return ((z & 7) << 6) + TF_BLK3; }
 __device__ __forceinline__ float raw_sdf(unsigned r) { return (float)(short)(r & 0xffffu); }
 __device__ __forceinline__ float raw_w(unsigned r) { return (float)((r >> 16) & 0xffu); }
 
@@ -115,6 +131,23 @@ __device__ __forceinline__ int sel8(const int (&v)[8], int i)
     return r;
 }
 
+// v[ux + 2uy + 4uz] for per-axis bits: a 3-level select tree (7 selects on 3 shared conditions)
+// (the empty asm keeps the selects as selects: left alone the optimiser rebuilds the tree
+// into a dynamically indexed private array in scratch)
+template <typename T>
+__device__ __forceinline__ T sel_tree(const T (&v)[8], bool ux, bool uy, bool uz)
+{
+    T w[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { w[c] = v[c]; asm volatile("" : "+v"(w[c])); }
+    const T a0 = ux ? w[1] : w[0], a1 = ux ? w[3] : w[2], a2 = ux ? w[5] : w[4], a3 = ux ? w[7] : w[6];
+    const T b0 = uy ? a1 : a0, b1 = uy ? a3 : a2;
+    return uz ? b1 : b0;
+}
+
+// ROUND (the reference's (int)ROUND(x) for the uninterpolated read)
+__device__ __forceinline__ int tf_round(float x) { return (int)((x < 0) ? (x - 0.5f) : (x + 0.5f)); }
+
 // the 8 interpolation corners of pt (floor .. floor+1) in the read order of
 // readFromSDF_float_interpolated (RepresentationAccess.hpp:137-162): corner c = (c&1, c>>1&1, c>>2)
 struct Corners {
@@ -122,33 +155,70 @@ struct Corners {
     float cx, cy, cz;        // fractions
     int bx, by, bz;          // block of floor(pt)
     int sx, sy, sz;          // 1 when floor+1 is in the next block along that axis
-    int hidx[8], voff[8];    // per corner: hash entry / VBA offset of its block
+    int cu;                  // ROUND(pt) = corner (cu&1, cu>>1&1, cu>>2) (the uninterpolated read)
+    int hU;                  // hash entry of ROUND(pt)'s block (-1: none)
+    unsigned valid;          // bit c: corner c's block exists
+    int voff[8];             // per corner: VBA offset of its block (TF_VOFF_NONE: none)
     unsigned raw[8];         // per corner: voxel word
 };
 
-__device__ __forceinline__ void corners_fetch(const SceneView& s, const float* pt, Corners& q)
+// A step's corner lookups in phases -- corners_prep (VALU only: floors, blocks, grid offsets),
+// the grid loads, corners_vox (block offsets -> the eight voxel loads) -- so that two rays
+// interleaved as grid(A) grid(B) vox(A) vox(B) share one round trip per phase.
+__device__ __forceinline__ bool corners_prep(const float* pt, Corners& q, unsigned (&o)[8])
 {
     const float ffx = floorf(pt[0]), ffy = floorf(pt[1]), ffz = floorf(pt[2]);
     q.fx = (int)ffx; q.fy = (int)ffy; q.fz = (int)ffz;
     q.cx = pt[0] - ffx; q.cy = pt[1] - ffy; q.cz = pt[2] - ffz;
     q.bx = vblk(q.fx); q.by = vblk(q.fy); q.bz = vblk(q.fz);
     q.sx = vblk(q.fx + 1) - q.bx; q.sy = vblk(q.fy + 1) - q.by; q.sz = vblk(q.fz + 1) - q.bz;
+    q.cu = (tf_round(pt[0]) - q.fx) + 2 * (tf_round(pt[1]) - q.fy) + 4 * (tf_round(pt[2]) - q.fz);
     const int X[2] = { q.bx, q.bx + q.sx }, Y[2] = { q.by, q.by + q.sy }, Z[2] = { q.bz, q.bz + q.sz };
-    blk_find8(s, X, Y, Z, q.hidx, q.voff);
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-        q.raw[c] = vox_raw(s, q.voff[c], q.fx + (c & 1), q.fy + ((c >> 1) & 1), q.fz + (c >> 2));
+    return blk_offsets8(X, Y, Z, o);
 }
-
+__device__ __forceinline__ void corners_slow(const SceneView& s, const Corners& q, int2 (&g)[8])
+{
+    const int X[2] = { q.bx, q.bx + q.sx }, Y[2] = { q.by, q.by + q.sy }, Z[2] = { q.bz, q.bz + q.sz };
+    blk_lookup_slow(s, X, Y, Z, g);
+}
+__device__ __forceinline__ void corners_blocks(Corners& q, const int2 (&g)[8])
+{
+    int hidx[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { hidx[c] = g[c].x; q.voff[c] = g[c].y; }
+    q.valid = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) q.valid |= (q.voff[c] >= 0 ? 1u : 0u) << c;
+    q.hU = sel_tree(hidx, (q.cu & 1) != 0, (q.cu & 2) != 0, (q.cu & 4) != 0);
+}
+__device__ __forceinline__ void corners_vox(const SceneView& s, Corners& q)
+{
+    const int lx[2] = { lin_x(q.fx), lin_x(q.fx + 1) }, ly[2] = { lin_y(q.fy), lin_y(q.fy + 1) };
+    const int lz[2] = { lin_zg(q.fz), lin_zg(q.fz + 1) };
+#pragma unroll
+    for (int c = 0; c < 8; ++c) q.raw[c] = vox_at(s, q.voff[c], lx[c & 1] + ly[(c >> 1) & 1] + lz[c >> 2]);
+}
+// the block lookups of pt's corners (one grid round trip; the wave takes the slow path together)
+__device__ __forceinline__ void corners_lookup(const SceneView& s, const float* pt, Corners& q)
+{
+    unsigned o[8];
+    int2 g[8];
+    const bool in = corners_prep(pt, q, o);
+    if (wave_any(!in)) corners_slow(s, q, g);
+    else blk_load8(s, o, g);
+    corners_blocks(q, g);
+}
+__device__ __forceinline__ void corners_fetch(const SceneView& s, const float* pt, Corners& q)
+{
+    corners_lookup(s, pt, q);
+    corners_vox(s, q);
+}
 // the IndexCache after the 8 serial corner reads: the block of the last corner whose block exists
 __device__ __forceinline__ void corners_cache(const Corners& q, RCache* k)
 {
-    int last = -1;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) last = q.voff[c] >= 0 ? c : last;
-    if (last >= 0) {
+    if (q.valid) {
+        const int last = 31 - __builtin_clz(q.valid);
         k->bx = q.bx + ((last & 1) & q.sx); k->by = q.by + (((last >> 1) & 1) & q.sy); k->bz = q.bz + ((last >> 2) & q.sz);
-        k->voff = sel8(q.voff, last);
     }
 }
 
@@ -164,7 +234,7 @@ __device__ __forceinline__ float interp_sdf(const Corners& q)
     res2 = (1.0f - cx) * v1 + cx * v2;
     v1 = raw_sdf(q.raw[6]); v2 = raw_sdf(q.raw[7]);
     res2 = (1.0f - cy) * res2 + cy * ((1.0f - cx) * v1 + cx * v2);
-    return ((1.0f - cz) * res1 + cz * res2) / 32767.0f;
+    return tf_div32767((1.0f - cz) * res1 + cz * res2);
 }
 
 __device__ __forceinline__ float interp_sdf_conf(const Corners& q, float* conf)
@@ -184,10 +254,9 @@ __device__ __forceinline__ float interp_sdf_conf(const Corners& q, float* conf)
     res2 = (1.0f - cy) * res2 + cy * ((1.0f - cx) * v1 + cx * v2);
     res2_c = (1.0f - cy) * res2_c + cy * ((1.0f - cx) * v1_c + cx * v2_c);
     *conf = (1.0f - cz) * res1_c + cz * res2_c;
-    return ((1.0f - cz) * res1 + cz * res2) / 32767.0f;
+    return tf_div32767((1.0f - cz) * res1 + cz * res2);
 }
 
-__device__ __forceinline__ int tf_round(float x) { return (int)((x < 0) ? (x - 0.5f) : (x + 0.5f)); }
 
 struct RayArgs {
     SceneView s;
@@ -200,76 +269,118 @@ struct RayArgs {
     float oneOverVoxelSize, mu;
 };
 
-// castRay (VisualisationEngine_Shared.hpp:99-172).  One step = the uninterpolated read at
-// ROUND(pt) and, in the band, the interpolated read at pt.  ROUND(pt) is one of the eight
-// interpolation corners, so a step fetches the corners once (speculatively): one grid round
-// trip + one voxel round trip per step.
-template <bool MARK>
-__device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, int x, int y, float* pt)
+// castRay (VisualisationEngine_Shared.hpp:99-172), split into init / step / finish so that two
+// rays can be marched interleaved.  One step = the uninterpolated read at ROUND(pt) and, in the
+// band, the interpolated read at pt.  ROUND(pt) is one of the eight interpolation corners, so a
+// step fetches the corners once (speculatively): one grid round trip + one voxel round trip.
+struct Ray {
+    float pt[3], dir[3];
+    float totalLength, totalLengthMax, sdfValue;
+    RCache k;
+    bool active;             // inside castRay's while loop
+};
+
+__device__ __forceinline__ void ray_init(const RayArgs& a, const float* invM, int x, int y, Ray& R)
 {
     int locId2 = (int)floorf((float)x / TF_SUBSAMPLE) + (int)floorf((float)y / TF_SUBSAMPLE) * a.W;
     float2 vf = a.range[locId2];
-    float r[3], ps[3], pe[3], dir[3];
-    float sdfValue = 1.0f, confidence = 0.0f, stepLength;
-    const float stepScale = a.mu * a.oneOverVoxelSize;
+    float r[3], ps[3], pe[3];
     float pz = vf.x;
     float px = pz * (((float)x + a.ncx) * a.invfx);
     float py = pz * (((float)y + a.ncy) * a.invfy);
-    float totalLength = sqrtf(((0.0f + px * px) + py * py) + pz * pz) * a.oneOverVoxelSize;
+    R.totalLength = sqrtf(((0.0f + px * px) + py * py) + pz * pz) * a.oneOverVoxelSize;
     tf_m4v3(invM, px, py, pz, 1.0f, r);
     ps[0] = r[0] * a.oneOverVoxelSize; ps[1] = r[1] * a.oneOverVoxelSize; ps[2] = r[2] * a.oneOverVoxelSize;
     pz = vf.y;
     px = pz * (((float)x + a.ncx) * a.invfx);
     py = pz * (((float)y + a.ncy) * a.invfy);
-    float totalLengthMax = sqrtf(((0.0f + px * px) + py * py) + pz * pz) * a.oneOverVoxelSize;
+    R.totalLengthMax = sqrtf(((0.0f + px * px) + py * py) + pz * pz) * a.oneOverVoxelSize;
     tf_m4v3(invM, px, py, pz, 1.0f, r);
     pe[0] = r[0] * a.oneOverVoxelSize; pe[1] = r[1] * a.oneOverVoxelSize; pe[2] = r[2] * a.oneOverVoxelSize;
-    dir[0] = pe[0] - ps[0]; dir[1] = pe[1] - ps[1]; dir[2] = pe[2] - ps[2];
-    float dn = 1.0f / sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
-    dir[0] *= dn; dir[1] *= dn; dir[2] *= dn;
-    pt[0] = ps[0]; pt[1] = ps[1]; pt[2] = ps[2];
-    RCache k; k.bx = k.by = k.bz = 0x7fffffff; k.voff = -1;
-    while (totalLength < totalLengthMax) {
+    R.dir[0] = pe[0] - ps[0]; R.dir[1] = pe[1] - ps[1]; R.dir[2] = pe[2] - ps[2];
+    float dn = 1.0f / sqrtf(R.dir[0] * R.dir[0] + R.dir[1] * R.dir[1] + R.dir[2] * R.dir[2]);
+    R.dir[0] *= dn; R.dir[1] *= dn; R.dir[2] *= dn;
+    R.pt[0] = ps[0]; R.pt[1] = ps[1]; R.pt[2] = ps[2];
+    R.k.bx = R.k.by = R.k.bz = 0x7fffffff;
+    R.sdfValue = 1.0f;
+    R.active = R.totalLength < R.totalLengthMax;
+}
+
+// one pass of castRay's loop body on the fetched corners of R.pt
+// (q.raw is only read when ROUND(pt)'s block exists: a step in unallocated space needs no voxel)
+template <bool MARK>
+__device__ __forceinline__ void ray_step(const RayArgs& a, Ray& R, const Corners& q)
+{
+    const float stepScale = a.mu * a.oneOverVoxelSize;
+    // uninterpolated read at ROUND(pt) (readFromSDF_float_uninterpolated, :129-135)
+    const int ux = q.cu & 1, uy = (q.cu >> 1) & 1, uz = q.cu >> 2;
+    int vmIndex = 0;
+    const bool found = (q.valid >> q.cu) & 1u;
+    if (found) {
+        const int Ubx = q.bx + (ux & q.sx), Uby = q.by + (uy & q.sy), Ubz = q.bz + (uz & q.sz);
+        const bool hit = Ubx == R.k.bx && Uby == R.k.by && Ubz == R.k.bz;
+        vmIndex = hit ? 1 : q.hU + 1;
+        R.k.bx = Ubx; R.k.by = Uby; R.k.bz = Ubz;
+    }
+    // a missing block reads Voxel_s(): 32767 / 32767 = 1
+    float sdfValue = found ? tf_short_to_float((short)(sel_tree(q.raw, ux != 0, uy != 0, uz != 0) & 0xffffu)) : 1.0f;
+    if (MARK && vmIndex) a.visType[vmIndex - 1] = 1;
+    float stepLength;
+    if (!vmIndex) {
+        stepLength = (float)TF_BLK;
+    } else {
+        if ((sdfValue <= 0.1f) && (sdfValue >= -0.5f)) {
+            sdfValue = interp_sdf(q);
+            corners_cache(q, &R.k);
+        }
+        if (sdfValue <= 0.0f) { R.sdfValue = sdfValue; R.active = false; return; }   // the loop's break
+        float qq = sdfValue * stepScale;
+        stepLength = (qq < 1.0f) ? 1.0f : qq;
+    }
+    R.sdfValue = sdfValue;
+    R.pt[0] += stepLength * R.dir[0]; R.pt[1] += stepLength * R.dir[1]; R.pt[2] += stepLength * R.dir[2];
+    R.totalLength += stepLength;
+    R.active = R.totalLength < R.totalLengthMax;
+}
+
+// castRay's refinement at the surface: the step back onto it; true when there is one (then
+// ray_finish completes it on the fetched corners of R.pt)
+__device__ __forceinline__ bool ray_refine(const RayArgs& a, Ray& R)
+{
+    if (!(R.sdfValue <= 0.0f)) return false;
+    const float stepLength = R.sdfValue * (a.mu * a.oneOverVoxelSize);
+    R.pt[0] += stepLength * R.dir[0]; R.pt[1] += stepLength * R.dir[1]; R.pt[2] += stepLength * R.dir[2];
+    return true;
+}
+__device__ __forceinline__ float ray_finish(const RayArgs& a, Ray& R, const Corners& q)
+{
+    float confidence;
+    const float sdfValue = interp_sdf_conf(q, &confidence);
+    const float stepLength = sdfValue * (a.mu * a.oneOverVoxelSize);
+    R.pt[0] += stepLength * R.dir[0]; R.pt[1] += stepLength * R.dir[1]; R.pt[2] += stepLength * R.dir[2];
+    return confidence + 1.0f;
+}
+
+template <bool MARK>
+__device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, int x, int y, float* pt)
+{
+    Ray R;
+    ray_init(a, invM, x, y, R);
+    while (R.active) {
         Corners q;
-        corners_fetch(a.s, pt, q);
-        // uninterpolated read at ROUND(pt) (readFromSDF_float_uninterpolated, :129-135)
-        const int ux = tf_round(pt[0]) - q.fx, uy = tf_round(pt[1]) - q.fy, uz = tf_round(pt[2]) - q.fz;
-        const int cu = ux + 2 * uy + 4 * uz;
-        const int vu = sel8(q.voff, cu);
-        int vmIndex = 0;
-        if (vu >= 0) {
-            const int Ubx = q.bx + (ux & q.sx), Uby = q.by + (uy & q.sy), Ubz = q.bz + (uz & q.sz);
-            const bool hit = Ubx == k.bx && Uby == k.by && Ubz == k.bz;
-            vmIndex = hit ? 1 : sel8(q.hidx, cu) + 1;
-            k.bx = Ubx; k.by = Uby; k.bz = Ubz; k.voff = vu;
-        }
-        sdfValue = tf_short_to_float((short)((unsigned)sel8(reinterpret_cast<const int(&)[8]>(q.raw), cu) & 0xffffu));
-        if (MARK && vmIndex) a.visType[vmIndex - 1] = 1;
-        if (!vmIndex) {
-            stepLength = (float)TF_BLK;
-        } else {
-            if ((sdfValue <= 0.1f) && (sdfValue >= -0.5f)) {
-                sdfValue = interp_sdf(q);
-                corners_cache(q, &k);
-            }
-            if (sdfValue <= 0.0f) break;
-            float qq = sdfValue * stepScale;
-            stepLength = (qq < 1.0f) ? 1.0f : qq;
-        }
-        pt[0] += stepLength * dir[0]; pt[1] += stepLength * dir[1]; pt[2] += stepLength * dir[2];
-        totalLength += stepLength;
+        corners_lookup(a.s, R.pt, q);
+        // the voxel round trip only when some lane's ROUND(pt) block exists (free space
+        // between surfaces is stepped a block at a time on the grid alone)
+        if (wave_any((q.valid >> q.cu) & 1u)) corners_vox(a.s, q);
+        ray_step<MARK>(a, R, q);
     }
     float w = 0.0f;
-    if (sdfValue <= 0.0f) {
-        stepLength = sdfValue * stepScale;
-        pt[0] += stepLength * dir[0]; pt[1] += stepLength * dir[1]; pt[2] += stepLength * dir[2];
+    if (ray_refine(a, R)) {
         Corners q;
-        corners_fetch(a.s, pt, q);
-        sdfValue = interp_sdf_conf(q, &confidence);
-        stepLength = sdfValue * stepScale;
-        pt[0] += stepLength * dir[0]; pt[1] += stepLength * dir[1]; pt[2] += stepLength * dir[2];
-        w = confidence + 1.0f;
+        corners_fetch(a.s, R.pt, q);
+        w = ray_finish(a, R, q);
     }
+    pt[0] = R.pt[0]; pt[1] = R.pt[1]; pt[2] = R.pt[2];
     return w;
 }
 
@@ -278,7 +389,10 @@ __device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, 
 // computeNormalAndAngle (VisualisationEngine_Shared.hpp:187-203), drawPixelGrey (:272-276).
 // The 32 uncached reads cover pt's 4x4x4 neighbourhood (floor-1 .. floor+2): <= 2x2x2 blocks.
 // ---------------------------------------------------------------------------------------
-__device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
+// vtab: this thread's 8-entry slot in LDS (VTAB_STRIDE ints): the 2x2x2 block offsets, so each
+// of the 32 reads finds its block with one LDS load instead of an 8-way select.
+#define VTAB_STRIDE 9
+__device__ void sdf_normal(const SceneView& s, const float* pt, float* ret, int* vtab)
 {
     float ffx = floorf(pt[0]), ffy = floorf(pt[1]), ffz = floorf(pt[2]);
     int px = (int)ffx, py = (int)ffy, pz = (int)ffz;
@@ -289,13 +403,16 @@ __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
     int voff[8], hidx[8];
     const int X[2] = { bx, bx + sx }, Y[2] = { by, by + sy }, Z[2] = { bz, bz + sz };
     blk_find8(s, X, Y, Z, hidx, voff);
-    int ox[4], oy[4], oz[4];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) vtab[c] = voff[c];
+    int tx[4], ty[4], tz[4], lx[4], ly[4], lz[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        ox[d] = vblk(px - 1 + d) - bx; oy[d] = vblk(py - 1 + d) - by; oz[d] = vblk(pz - 1 + d) - bz;
+        tx[d] = vblk(px - 1 + d) - bx; ty[d] = 2 * (vblk(py - 1 + d) - by); tz[d] = 4 * (vblk(pz - 1 + d) - bz);
+        lx[d] = lin_x(px - 1 + d); ly[d] = lin_y(py - 1 + d); lz[d] = lin_zg(pz - 1 + d);
     }
-#define RV(dx, dy, dz) raw_sdf(vox_raw(s, sel8(voff, ox[(dx) + 1] + 2 * oy[(dy) + 1] + 4 * oz[(dz) + 1]), \
-                                       px + (dx), py + (dy), pz + (dz)))
+#define RV(dx, dy, dz) raw_sdf(vox_at(s, vtab[tx[(dx) + 1] + ty[(dy) + 1] + tz[(dz) + 1]], \
+                                      lx[(dx) + 1] + ly[(dy) + 1] + lz[(dz) + 1]))
     float f0 = RV(0, 0, 0), f1 = RV(1, 0, 0), f2 = RV(0, 1, 0), f3 = RV(1, 1, 0);
     float b0 = RV(0, 0, 1), b1 = RV(1, 0, 1), b2 = RV(0, 1, 1), b3 = RV(1, 1, 1);
     float t0, t1, t2, t3, p1, p2, v1;
@@ -306,7 +423,7 @@ __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
     p1 = f1 * ny * nz + f3 * cy * nz + b1 * ny * cz + b3 * cy * cz;
     t0 = RV(2, 0, 0); t1 = RV(2, 1, 0); t2 = RV(2, 0, 1); t3 = RV(2, 1, 1);
     p2 = t0 * ny * nz + t1 * cy * nz + t2 * ny * cz + t3 * cy * cz;
-    ret[0] = (p1 * nx + p2 * cx - v1) / 32767.0f;
+    ret[0] = tf_div32767(p1 * nx + p2 * cx - v1);
     p1 = f0 * nx * nz + f1 * cx * nz + b0 * nx * cz + b1 * cx * cz;
     t0 = RV(0, -1, 0); t1 = RV(1, -1, 0); t2 = RV(0, -1, 1); t3 = RV(1, -1, 1);
     p2 = t0 * nx * nz + t1 * cx * nz + t2 * nx * cz + t3 * cx * cz;
@@ -314,7 +431,7 @@ __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
     p1 = f2 * nx * nz + f3 * cx * nz + b2 * nx * cz + b3 * cx * cz;
     t0 = RV(0, 2, 0); t1 = RV(1, 2, 0); t2 = RV(0, 2, 1); t3 = RV(1, 2, 1);
     p2 = t0 * nx * nz + t1 * cx * nz + t2 * nx * cz + t3 * cx * cz;
-    ret[1] = (p1 * ny + p2 * cy - v1) / 32767.0f;
+    ret[1] = tf_div32767(p1 * ny + p2 * cy - v1);
     p1 = f0 * nx * ny + f1 * cx * ny + f2 * nx * cy + f3 * cx * cy;
     t0 = RV(0, 0, -1); t1 = RV(1, 0, -1); t2 = RV(0, 1, -1); t3 = RV(1, 1, -1);
     p2 = t0 * nx * ny + t1 * cx * ny + t2 * nx * cy + t3 * cx * cy;
@@ -322,16 +439,16 @@ __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret)
     p1 = b0 * nx * ny + b1 * cx * ny + b2 * nx * cy + b3 * cx * cy;
     t0 = RV(0, 0, 2); t1 = RV(1, 0, 2); t2 = RV(0, 1, 2); t3 = RV(1, 1, 2);
     p2 = t0 * nx * ny + t1 * cx * ny + t2 * nx * cy + t3 * cx * cy;
-    ret[2] = (p1 * nz + p2 * cz - v1) / 32767.0f;
+    ret[2] = tf_div32767(p1 * nz + p2 * cz - v1);
 #undef RV
 }
 
 // computeNormalAndAngle<TVoxel,TIndex> (VisualisationEngine_Shared.hpp:189-203): the SDF-gradient
 // normal at pt, normalised, and its angle to the light; false when the angle is not positive
 __device__ __forceinline__ bool sdf_normal_angle(const SceneView& s, const float* pt, float lx, float ly, float lz,
-                                                 float* nn, float* angle)
+                                                 float* nn, float* angle, int* vtab)
 {
-    sdf_normal(s, pt, nn);
+    sdf_normal(s, pt, nn, vtab);
     float ns = 1.0f / sqrtf(nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]);
     nn[0] *= ns; nn[1] *= ns; nn[2] *= ns;
     *angle = nn[0] * lx + nn[1] * ly + nn[2] * lz;
@@ -341,10 +458,11 @@ __device__ __forceinline__ bool sdf_normal_angle(const SceneView& s, const float
 // drawPixelGrey (VisualisationEngine_Shared.hpp:272-276)
 __device__ __forceinline__ unsigned char grey_of(float angle) { return (unsigned char)((0.8f * angle + 0.2f) * 255.0f); }
 
-__device__ __forceinline__ unsigned char grey_pixel(const SceneView& s, const float* pt, float lx, float ly, float lz)
+__device__ __forceinline__ unsigned char grey_pixel(const SceneView& s, const float* pt, float lx, float ly, float lz,
+                                                    int* vtab)
 {
     float nn[3], angle;
-    return sdf_normal_angle(s, pt, lx, ly, lz, nn, &angle) ? grey_of(angle) : (unsigned char)0;
+    return sdf_normal_angle(s, pt, lx, ly, lz, nn, &angle, vtab) ? grey_of(angle) : (unsigned char)0;
 }
 
 // XCD-aware tile order: consecutive image tiles land on the same XCD (and its L2)
@@ -372,8 +490,9 @@ __device__ __forceinline__ void raycast_tile(const RayArgs& a, const TfDevState*
     const float w = ray_march<MODE == 1>(a, M, x, y, pt);
     if (MODE == 2) {
         // renderImage: lightSource = -Vector3f(pose.getColumn(2)) (VisualisationEngine_CUDA.cu:243)
+        __shared__ int vtab[256 * VTAB_STRIDE];
         unsigned char v = 0;
-        if (w > 0) v = grey_pixel(a.s, pt, -M[8], -M[9], -M[10]);
+        if (w > 0) v = grey_pixel(a.s, pt, -M[8], -M[9], -M[10], &vtab[threadIdx.x * VTAB_STRIDE]);
         a.grey[x + y * a.W] = make_uchar4(v, v, v, v);
     } else {
         a.out[x + y * a.W] = make_float4(pt[0], pt[1], pt[2], w);
@@ -392,7 +511,8 @@ k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles
 // rays (castRay<true>, new range image), the second half renderImage's (castRay<false> +
 // grey, range snapshot).  Neither writes what the other reads, and a launch's run time is its
 // slowest waves' ray length: the halves fill each other's tails instead of each kernel
-// draining alone.
+// draining alone.  (Measured: marching both rays of a pixel interleaved in one thread, sharing
+// each step's round trips, is slower -- 142 VGPRs halve the resident waves.)
 __global__ void __launch_bounds__(256)
 k_raycast_pair(RayArgs ai, RayArgs ar, const TfDevState* __restrict__ st, int tiles_x, int n_tiles, int nb)
 {
@@ -402,7 +522,7 @@ k_raycast_pair(RayArgs ai, RayArgs ar, const TfDevState* __restrict__ st, int ti
 
 static void ray_args(tf_ctx* c, RayArgs& a)
 {
-    a.s.hash = c->hash; a.s.vba = c->vba; a.s.grid = c->bgrid; a.s.mask = (unsigned)(c->p.n_buckets - 1); a.s.n_buckets = c->p.n_buckets;
+    a.s.hash = c->hash; a.s.vba = c->vba_guard; a.s.grid = c->bgrid; a.s.mask = (unsigned)(c->p.n_buckets - 1); a.s.n_buckets = c->p.n_buckets;
     a.range = (const float2*)c->range; a.out = (float4*)c->raycast;
     a.visType = nullptr;
     a.grey = nullptr;
@@ -518,6 +638,7 @@ __global__ void __launch_bounds__(256)
 k_render_type(SceneView s, const float4* __restrict__ ray, int W, int H, float voxelSize,
               const TfDevState* __restrict__ st, uchar4* __restrict__ out)
 {
+    __shared__ int vtab[256 * VTAB_STRIDE];
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= W * H) return;
@@ -535,7 +656,7 @@ k_render_type(SceneView s, const float4* __restrict__ ray, int W, int H, float v
     }
     if (found) {
         const float pt[3] = { p.x, p.y, p.z };
-        found = sdf_normal_angle(s, pt, lx, ly, lz, nn, &angle);
+        found = sdf_normal_angle(s, pt, lx, ly, lz, nn, &angle, &vtab[threadIdx.x * VTAB_STRIDE]);
     }
     if (TYPE == TF_RENDER_COLOUR_FROM_NORMAL) {                      // processPixelNormal / drawPixelNormal
         if (found) {                                                 // r, g, b; alpha is left as it was (:305-310)
@@ -568,7 +689,7 @@ k_render_type(SceneView s, const float4* __restrict__ ray, int W, int H, float v
 
 hipError_t tfk_render_type(tf_ctx* c, int type)
 {
-    SceneView s; s.hash = c->hash; s.vba = c->vba; s.grid = c->bgrid; s.mask = (unsigned)(c->p.n_buckets - 1); s.n_buckets = c->p.n_buckets;
+    SceneView s; s.hash = c->hash; s.vba = c->vba_guard; s.grid = c->bgrid; s.mask = (unsigned)(c->p.n_buckets - 1); s.n_buckets = c->p.n_buckets;
     const int n = c->W * c->H;
     const dim3 g((n + 255) / 256), b(256);
     const float4* ray = (const float4*)c->raycast;

@@ -58,7 +58,7 @@ __global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_
     TfHashEntry e; e.x = e.y = e.z = e.pad = 0; e.offset = 0; e.ptr = -2;
     for (size_t i = tid; i < (size_t)n_total; i += stride) {
         const TfHashEntry o = hash[i];                       // clear the grid cells of live blocks
-        if (o.ptr >= 0 && tf_grid_in(o.x, o.y, o.z)) grid[tf_grid_cell(o.x, o.y, o.z)] = make_int2(-1, -1);
+        if (o.ptr >= 0 && tf_grid_in(o.x, o.y, o.z)) grid[tf_grid_cell(o.x, o.y, o.z)] = make_int2(-1, TF_VOFF_NONE);
         hash[i] = e;
     }
     for (size_t i = tid; i < (size_t)n_excess; i += stride) excessList[i] = (int)i;
@@ -95,9 +95,24 @@ __global__ void k_grid_build(const TfHashEntry* __restrict__ hash, int n_total, 
         grid_set(grid, hash[i], i);
 }
 
+__global__ void k_grid_clear(int4* __restrict__ grid2, size_t n2)
+{
+    const int4 none = make_int4(-1, TF_VOFF_NONE, -1, TF_VOFF_NONE);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += (size_t)gridDim.x * blockDim.x)
+        grid2[i] = none;
+}
+
+// every cell "no block" (-1, TF_VOFF_NONE)
+hipError_t tfk_grid_clear(tf_ctx* c)
+{
+    const size_t n2 = (size_t)TF_GRID_DIM * TF_GRID_DIM * TF_GRID_DIM / 2;
+    hipLaunchKernelGGL(k_grid_clear, dim3(4096), dim3(256), 0, c->stream, (int4*)c->bgrid, n2);
+    return hipGetLastError();
+}
+
 hipError_t tfk_grid_rebuild(tf_ctx* c)
 {
-    hipError_t e = hipMemsetAsync(c->bgrid, 0xff, sizeof(int2) * (size_t)TF_GRID_DIM * TF_GRID_DIM * TF_GRID_DIM, c->stream);
+    hipError_t e = tfk_grid_clear(c);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_grid_build, dim3(1024), dim3(256), 0, c->stream, c->hash, c->n_total, c->bgrid);
     return hipGetLastError();
