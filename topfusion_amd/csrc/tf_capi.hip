@@ -786,6 +786,7 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
     if (!p || n != bytes) return TF_INVALID_ARG;
     TF_CHECK(hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
     if (which == TF_BUF_HASH) TF_CHECK(tfk_grid_rebuild(c));       // keep the block grid exact
+    if (which == TF_BUF_HASH || which == TF_BUF_VBA) c->scene_external = 1;   // next reset: full clear
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }
@@ -807,6 +808,7 @@ extern "C" tf_status tf_set_counters(tf_ctx* c, int lastFreeBlockId, int lastFre
     c->st_host->lastFreeBlockId = lastFreeBlockId;
     c->st_host->lastFreeExcessListId = lastFreeExcessListId;
     c->st_host->noVisibleEntries = noVisibleEntries;
+    c->scene_external = 1;                                          // next reset: full clear
     TF_CHECK(hipMemcpyAsync(c->st, c->st_host, sizeof(TfDevState), hipMemcpyHostToDevice, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;

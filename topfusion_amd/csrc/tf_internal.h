@@ -61,7 +61,8 @@ struct TfDevState {
     int mode;                // this frame: 0 = frame-0 path (integrate only), 1 = tracking path
     int frame_counter;       // TopFu::frame_counter_
     int n_resets;            // resets taken after ICP failures
-    int pad2_[5];
+    unsigned reset_ticket;   // k_reset_scene: workgroups done (the last one resets the counters)
+    int pad2_[4];
     // renderImage of the frame runs on the context's render stream, overlapping the rest of
     // the frame and the next frame's preprocessing/ICP; it reads only this snapshot (taken on
     // the main stream once the previous render has finished: render_snapshot)
@@ -236,6 +237,7 @@ struct tf_ctx {
     TfHashEntry* hash;
     int* excessList;
     TfVoxel* vba;
+    int scene_external;      // scene buffers / counters set from the host since the last full reset
     TfVoxel* vba_guard;      // allocation: one guard block of Voxel_s() (TF_VOFF_NONE reads), then vba
     int* allocList;
     int2* bgrid;             // block grid (TF_GRID_*), mirrors the hash

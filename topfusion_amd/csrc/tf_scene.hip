@@ -30,7 +30,7 @@ __device__ __forceinline__ void load16(const unsigned char* p, unsigned long lon
 // ---------------------------------------------------------------------------------------
 __global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_blocks, TfHashEntry* hash,
                               int n_total, int* excessList, int n_excess, TfDevState* st, int2* grid, int on_failure,
-                              int* frame_ok, int* frame_mode, int slot)
+                              int* frame_ok, int* frame_mode, int slot, int full)
 {
     if (on_failure && blockIdx.x == 0 && threadIdx.x == 0) {
         // end of the device-driven frame (return values of topfu.cpp:209 / 264 / 329); only
@@ -53,16 +53,36 @@ __global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     uint4 vfill = make_uint4(32767u, 32767u, 32767u, 32767u);   // Voxel_s(): sdf 32767, w 0
     uint4* v4 = (uint4*)vba;
-    for (size_t i = tid; i < n_vox / 4; i += stride) v4[i] = vfill;
-    for (size_t i = tid; i < (size_t)n_blocks; i += stride) allocList[i] = (int)i;
     TfHashEntry e; e.x = e.y = e.z = e.pad = 0; e.offset = 0; e.ptr = -2;
-    for (size_t i = tid; i < (size_t)n_total; i += stride) {
-        const TfHashEntry o = hash[i];                       // clear the grid cells of live blocks
-        if (o.ptr >= 0 && tf_grid_in(o.x, o.y, o.z)) grid[tf_grid_cell(o.x, o.y, o.z)] = make_int2(-1, TF_VOFF_NONE);
-        hash[i] = e;
+    if (full) {
+        for (size_t i = tid; i < n_vox / 4; i += stride) v4[i] = vfill;
+        for (size_t i = tid; i < (size_t)n_blocks; i += stride) allocList[i] = (int)i;
+        for (size_t i = tid; i < (size_t)n_excess; i += stride) excessList[i] = (int)i;
+    } else {
+        // Same end state from what the frames wrote since the last full reset: allocation only
+        // pops the free lists (never writes them) and integration only writes blocks it was
+        // handed, so the blocks in use -- allocList[lastFreeBlockId+1 .. n_blocks-1] -- are the
+        // only ones not at Voxel_s(), and the free lists are still the identity.
+        const int first = st->lastFreeBlockId + 1 < 0 ? 0 : st->lastFreeBlockId + 1;
+        const size_t n_used4 = (size_t)(n_blocks - first) * (TF_BLK3 / 4);
+        for (size_t i = tid; i < n_used4; i += stride)
+            v4[(size_t)allocList[first + (int)(i / (TF_BLK3 / 4))] * (TF_BLK3 / 4) + i % (TF_BLK3 / 4)] = vfill;
     }
-    for (size_t i = tid; i < (size_t)n_excess; i += stride) excessList[i] = (int)i;
-    if (tid == 0) {
+    for (size_t i = tid; i < (size_t)n_total; i += stride) {
+        const TfHashEntry o = hash[i];                       // live entries (only they differ from e)
+        if (full || o.ptr >= 0) {
+            if (o.ptr >= 0 && tf_grid_in(o.x, o.y, o.z)) grid[tf_grid_cell(o.x, o.y, o.z)] = make_int2(-1, TF_VOFF_NONE);
+            hash[i] = e;
+        }
+    }
+    // the counters are reset by the last workgroup to finish (every workgroup has read
+    // lastFreeBlockId by then)
+    __shared__ int last_s;
+    __syncthreads();
+    if (threadIdx.x == 0) last_s = atomicAdd(&st->reset_ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (last_s && threadIdx.x == 0) {
+        st->reset_ticket = 0;
         st->lastFreeBlockId = n_blocks - 1;
         st->lastFreeExcessListId = n_excess - 1;
     }
@@ -72,15 +92,20 @@ hipError_t tfk_reset_scene(tf_ctx* c)
 {
     hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, c->vba, (size_t)c->p.n_blocks * TF_BLK3,
                        c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st, c->bgrid, 0,
-                       nullptr, nullptr, 0);
-    return hipGetLastError();
+                       nullptr, nullptr, 0, 1);
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) c->scene_external = 0;
+    return e;
 }
 
+// the frame's end (every frame; the reset part only when ICP failed): one workgroup per CU, so
+// a successful frame pays a small launch; a failed one clears only what the frames wrote (a
+// full clear when scene buffers were uploaded since the last full reset)
 hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot)
 {
-    hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, c->vba, (size_t)c->p.n_blocks * TF_BLK3,
+    hipLaunchKernelGGL(k_reset_scene, dim3(256), dim3(256), 0, c->stream, c->vba, (size_t)c->p.n_blocks * TF_BLK3,
                        c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st, c->bgrid, 1,
-                       c->frame_ok, c->frame_mode, slot);
+                       c->frame_ok, c->frame_mode, slot, c->scene_external);
     return hipGetLastError();
 }
 
