@@ -103,6 +103,41 @@ def omp_threads():
     return len(os.sched_getaffinity(0))
 
 
+def cpu_model():
+    """Host CPU model name and logical CPU count (report nproc and the model)."""
+    name = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return name, os.cpu_count()
+
+
+def hbm_stream_copy(device, gib=1.0, reps=10):
+    """Measured device-to-device copy bandwidth (read + write bytes / time, HIP events) beside
+    the 8 TB/s spec peak the roofline fractions use."""
+    import torch
+    n = int(gib * (1 << 30)) // 4
+    x = torch.empty(n, dtype=torch.float32, device=device)
+    y = torch.empty_like(x)
+    y.copy_(x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del x, y
+    torch.cuda.empty_cache()
+    return 2.0 * n * 4 / (ms * 1e-3) / 1e9
+
+
 def cpu_baseline(frames, params_kw, seconds, omp=False):
     """Oracle (C restatement of the reference) on a bounded prefix of the same stream: the serial
     build (1 thread) or its OpenMP build (omp=True: independent pixels / CTAs / blocks over
@@ -323,6 +358,7 @@ def main():
                                          else "HIP events in the breakdown pass"}
             if dominant in roof_all:
                 roof = roof_all[dominant]
+        stream_gbs = round(hbm_stream_copy(f"cuda:{local_rank}"), 1)
         cpu = None
         if not args.no_cpu_baseline:
             # all cores: the OpenMP build of the oracle; 1 thread: the serial build (reported beside)
@@ -334,7 +370,8 @@ def main():
                              f"threads, allocation serial) on frames 0..{n - 1} of the same {args.config} stream, "
                              f"{W}x{H}, {dt:.1f} s, host CPU of the GPU box",
                    "single_thread": {"value": round(v1, 4), "cores": 1,
-                                     "sample": f"serial oracle on frames 0..{n1 - 1}, {dt1:.1f} s"}}
+                                     "sample": f"serial oracle on frames 0..{n1 - 1}, {dt1:.1f} s"},
+                   "cpu_model": cpu_model()[0], "nproc": cpu_model()[1]}
         out = {
             "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame",
             "value": round(value, 2),
@@ -363,6 +400,7 @@ def main():
             "visible_blocks_last": st["noVisibleEntries"],
             "allocated_blocks_last": int(tf.params().n_blocks - 1 - st["lastFreeBlockId"]),
             "roofline": roof,
+            "hbm_stream_copy_GBs": stream_gbs,
             "roofline_stages": roof_all,
             "icp_schedule": "persistent" if tf.icp_persistent() else "per_iteration",
             "cpu_baseline": cpu,
