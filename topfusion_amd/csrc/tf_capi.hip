@@ -265,6 +265,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     }
     e = tfk_reset_scene(c);                              // topfu.cpp:75
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = tfk_check_div3(c, pin->mu, &c->mu_exact3);   // integrate: eta / mu
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     {   // ICP schedule: one persistent launch per frame when all its workgroups fit at once
         const char* env = getenv("TFUSION_ICP_PERSISTENT");

@@ -163,6 +163,18 @@ __device__ __forceinline__ float tf_div32767(float x)
     return fmaf(-fmaf(q0, 32767.0f, -x), r, q0);
 }
 
+// x / d for a divisor d whose three-operation quotient is known exact (rd = RN(1/d)): q0 = x*rd,
+// e = fma(q0, d, -x), q = fma(-e, rd, q0) equals the IEEE division for every x of every binade
+// where no intermediate is subnormal; that is checked over all mantissas of one binade for
+// d = 1..257 (tools/check_div_consts.c) and, at tf_create, for the context's mu.  |x| < 2^-100
+// takes the division itself.
+__device__ __forceinline__ float tf_div_exact3(float x, float d, float rd)
+{
+    if (fabsf(x) < 0x1p-100f) return x / d;
+    const float q0 = x * rd;
+    return fmaf(-fmaf(q0, d, -x), rd, q0);
+}
+
 // A missing block's VBA offset in the block grid: the render side reads voxels relative to a
 // guard block of Voxel_s() values placed just before the VBA (tf_ctx::vba_guard), so a voxel
 // load needs no "is the block there" select -- it lands in the guard and reads (32767, 0).
@@ -238,6 +250,7 @@ struct tf_ctx {
     int* excessList;
     TfVoxel* vba;
     int scene_external;      // scene buffers / counters set from the host since the last full reset
+    int mu_exact3;           // eta / mu by tf_div_exact3 (checked on the device at tf_create)
     TfVoxel* vba_guard;      // allocation: one guard block of Voxel_s() (TF_VOFF_NONE reads), then vba
     int* allocList;
     int2* bgrid;             // block grid (TF_GRID_*), mirrors the hash
@@ -307,6 +320,7 @@ hipError_t tfk_reset_scene(tf_ctx* c);
 hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot);   // frame end + ResetScene if ICP failed
 hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a hash upload)
 hipError_t tfk_grid_clear(tf_ctx* c);     // every cell (-1, TF_VOFF_NONE)
+hipError_t tfk_check_div3(tf_ctx* c, float d, int* ok);   // tf_div_exact3(x, d) == x / d over a binade
 hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0);   // snapshot: + the frame's renderImage snapshot
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);

@@ -135,6 +135,40 @@ hipError_t tfk_grid_clear(tf_ctx* c)
     return hipGetLastError();
 }
 
+// tf_div_exact3 against the division for every mantissa of the binade [1, 2), both signs, on
+// the device's own arithmetic (scale invariance extends it to every binade without subnormal
+// intermediates)
+__global__ void k_check_div3(float d, int* ok)
+{
+    const unsigned m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= (1u << 23)) return;
+    const float rd = 1.0f / d;
+    const float x = __uint_as_float(0x3f800000u | m);
+    bool good = true;
+    for (int s = 0; s < 2; ++s) {
+        const float xx = s ? -x : x;
+        const float q0 = xx * rd;
+        const float q = fmaf(-fmaf(q0, d, -xx), rd, q0);
+        good = good && __float_as_uint(q) == __float_as_uint(xx / d);
+    }
+    if (!good) atomicAnd(ok, 0);
+}
+
+hipError_t tfk_check_div3(tf_ctx* c, float d, int* ok)
+{
+    int* dok = (int*)c->icp_ticket;              // scratch word (the ticket is idle at creation)
+    int one = 1;
+    hipError_t e = hipMemcpyAsync(dok, &one, sizeof(int), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_check_div3, dim3((1u << 23) / 256), dim3(256), 0, c->stream, d, dok);
+    e = hipMemcpyAsync(ok, dok, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    int zero = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(dok, &zero, sizeof(int), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return e;
+}
+
 hipError_t tfk_grid_rebuild(tf_ctx* c)
 {
     hipError_t e = tfk_grid_clear(c);
@@ -607,6 +641,8 @@ struct IntegArgs {
     int W, H;
     float fx, fy, cx, cy;
     float voxelSize, mu;
+    float inv_mu;                       // RN(1/mu) when mu_exact3 (eta / mu in three operations)
+    int mu_exact3;
     int maxW;
     // frame 0 of the device-driven frame: prev_ = curr_ (topfu.cpp:205 swaps the pyramids;
     // copying keeps the buffer pointers fixed); levels contiguous, n_maps float4 per map
@@ -615,7 +651,7 @@ struct IntegArgs {
 };
 
 __device__ __forceinline__ unsigned integ_voxel(unsigned vox, float px, float py, float pz, const float* M,
-                                                const IntegArgs& a)
+                                                const IntegArgs& a, const float* rw)
 {
     float pc[3];
     tf_m4v3(M, px, py, pz, 1.0f, pc);
@@ -630,11 +666,11 @@ __device__ __forceinline__ unsigned integ_voxel(unsigned vox, float px, float py
     short sdf = (short)(vox & 0xffff);
     int oldW = (vox >> 16) & 0xff;
     float oldF = tf_short_to_float(sdf);          // == (float)sdf / 32767.0f, exactly
-    float newF = eta / a.mu;
+    float newF = a.mu_exact3 ? tf_div_exact3(eta, a.mu, a.inv_mu) : eta / a.mu;
     newF = (1.0f < newF) ? 1.0f : newF;
     newF = (float)oldW * oldF + 1.0f * newF;
     int newW = oldW + 1;
-    newF /= (float)newW;
+    newF = tf_div_exact3(newF, (float)newW, rw[newW - 1]);     // newW in 1..256
     newW = (newW < a.maxW) ? newW : a.maxW;
     short nsdf = (short)(newF * 32767.0f);
     return ((unsigned)(unsigned short)nsdf) | ((unsigned)(newW & 0xff) << 16) | (vox & 0xff000000u);
@@ -654,14 +690,14 @@ __device__ __forceinline__ void nt_store16(uint4* p, uint4 v)
 
 // one lane's 4 consecutive voxels (16 B) of a block: update and store
 __device__ __forceinline__ void integ_chunk(uint4 v, const TfHashEntry& e, int vx, int vy, int vz, const float* M,
-                                            const IntegArgs& a, uint4* p)
+                                            const IntegArgs& a, uint4* p, const float* rw)
 {
     const int gx = e.x * TF_BLK, gy = e.y * TF_BLK, gz = e.z * TF_BLK;
     const float py = (float)(gy + vy) * a.voxelSize, pz = (float)(gz + vz) * a.voxelSize;
-    v.x = integ_voxel(v.x, (float)(gx + vx + 0) * a.voxelSize, py, pz, M, a);
-    v.y = integ_voxel(v.y, (float)(gx + vx + 1) * a.voxelSize, py, pz, M, a);
-    v.z = integ_voxel(v.z, (float)(gx + vx + 2) * a.voxelSize, py, pz, M, a);
-    v.w = integ_voxel(v.w, (float)(gx + vx + 3) * a.voxelSize, py, pz, M, a);
+    v.x = integ_voxel(v.x, (float)(gx + vx + 0) * a.voxelSize, py, pz, M, a, rw);
+    v.y = integ_voxel(v.y, (float)(gx + vx + 1) * a.voxelSize, py, pz, M, a, rw);
+    v.z = integ_voxel(v.z, (float)(gx + vx + 2) * a.voxelSize, py, pz, M, a, rw);
+    v.w = integ_voxel(v.w, (float)(gx + vx + 3) * a.voxelSize, py, pz, M, a, rw);
     nt_store16(p, v);
 }
 
@@ -669,6 +705,9 @@ __global__ void __launch_bounds__(256)
 k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
             const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba)
 {
+    __shared__ float rw[256];                    // RN(1/w), w = 1..256: the running average's divisors
+    rw[threadIdx.x] = 1.0f / (float)(threadIdx.x + 1);
+    __syncthreads();
     if (st->abort) return;
     if (a.n_maps > 0 && st->mode == 0) {
         const int stride = gridDim.x * 256;
@@ -699,8 +738,8 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
         // the voxel stream is read and written once per pass: non-temporal, so it does not
         // evict the depth image every voxel samples from L2
         uint4 v = nt_load16(p), v2 = nt_load16(p2);
-        if (e.ptr >= 0) integ_chunk(v, e, vx, vy, vz, M, a, p);
-        if (e2.ptr >= 0) integ_chunk(v2, e2, vx, vy, vz, M, a, p2);
+        if (e.ptr >= 0) integ_chunk(v, e, vx, vy, vz, M, a, p, rw);
+        if (e2.ptr >= 0) integ_chunk(v2, e2, vx, vy, vz, M, a, p2, rw);
     }
 }
 
@@ -714,6 +753,7 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path)
     a.dists = c->dists; a.W = c->W; a.H = c->H;
     a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy;
     a.voxelSize = c->p.voxelSize; a.mu = c->p.mu; a.maxW = c->p.maxW;
+    a.inv_mu = 1.0f / c->p.mu; a.mu_exact3 = c->mu_exact3;
     hipLaunchKernelGGL(k_integrate, dim3(2048), dim3(256), 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba);
     return hipGetLastError();
 }
