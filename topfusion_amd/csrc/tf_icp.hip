@@ -671,8 +671,11 @@ k_icp_frame(IcpFrameArgs a)
                 const int x = bx * 32 + (t & 31), y = by * 8 + (t >> 5);
                 const bool in = live && x < L.W && y < L.H;
                 xy[rr][j] = in ? 1 : -1;
-                float4 v = in ? L.vcurr[y * L.W + x] : make_float4(0.f, 0.f, 0.f, 0.f);
-                float4 n = in ? L.ncurr[y * L.W + x] : make_float4(0.f, 0.f, 0.f, 0.f);
+                // unconditional loads (pixel 0 when outside): a load under a per-lane condition
+                // is a branch, and the eight of a level start would be eight round trips
+                const int pi = in ? y * L.W + x : 0;
+                float4 v = L.vcurr[pi], n = L.ncurr[pi];
+                if (!in) { v = make_float4(0.f, 0.f, 0.f, 0.f); n = v; }
                 px[rr][j].vx = v.x; px[rr][j].vy = v.y; px[rr][j].vz = v.z;
                 px[rr][j].nx = n.x; px[rr][j].ny = n.y; px[rr][j].nz = n.z;
             }
@@ -714,8 +717,9 @@ k_icp_frame(IcpFrameArgs a)
                     const int x = bx * 32 + (t & 31), y = by * 8 + (t >> 5);
                     const bool in = x < L.W && y < L.H;
                     qxy[j] = in ? 1 : -1;
-                    const float4 v = in ? L.vcurr[y * L.W + x] : make_float4(0.f, 0.f, 0.f, 0.f);
-                    const float4 n = in ? L.ncurr[y * L.W + x] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const int pi = in ? y * L.W + x : 0;                 // unconditional loads
+                    float4 v = L.vcurr[pi], n = L.ncurr[pi];
+                    if (!in) { v = make_float4(0.f, 0.f, 0.f, 0.f); n = v; }
                     q[j].vx = v.x; q[j].vy = v.y; q[j].vz = v.z; q[j].nx = n.x; q[j].ny = n.y; q[j].nz = n.z;
                 }
                 float r[4][7];

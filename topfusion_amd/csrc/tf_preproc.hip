@@ -10,6 +10,8 @@
 #include "tf_internal.h"
 #include "tf_pose.h"
 
+typedef float tf_f2 __attribute__((ext_vector_type(2)));   // packed f32 pair (v_pk_* on gfx950)
+
 #define PRE_TX 32
 #define PRE_TY 8
 #define HALO 3
@@ -22,17 +24,42 @@ k_dists_bilateral(const uint16_t* __restrict__ src, size_t pitch, int W, int H, 
                   float* __restrict__ dists, uint16_t* __restrict__ dst)
 {
     __shared__ uint16_t tile[PRE_TY + 2 * HALO][PRE_TX + 2 * HALO + 2];
+    __shared__ float ftile[PRE_TY + 2 * HALO][PRE_TX + 2 * HALO + 2];
+    __shared__ float sptab[2 * HALO + 1][2 * HALO + 2];      // RN(space2 * ss) by (y-cy+3, x-cx+3)
     const int tx = threadIdx.x & (PRE_TX - 1), ty = threadIdx.x / PRE_TX;
     const int x0 = blockIdx.x * PRE_TX, y0 = blockIdx.y * PRE_TY;
-    for (int i = threadIdx.x; i < (PRE_TY + 2 * HALO) * (PRE_TX + 2 * HALO); i += 256) {
-        int ly = i / (PRE_TX + 2 * HALO), lx = i % (PRE_TX + 2 * HALO);
-        int gx = x0 + lx - HALO, gy = y0 + ly - HALO;
-        uint16_t v = 0;
-        if (gx >= 0 && gx < W && gy >= 0 && gy < H)
-            v = *(const uint16_t*)((const char*)src + (size_t)gy * pitch + (size_t)gx * 2);
-        tile[ly][lx] = v;
+    bool big = false;
+    {   // every load of the tile first (clamped to pixel 0 outside the image), then the LDS
+        // writes: one memory round trip instead of one per element
+        constexpr int NT = (PRE_TY + 2 * HALO) * (PRE_TX + 2 * HALO), PER = (NT + 255) / 256;
+        uint16_t vals[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            const int ly = i / (PRE_TX + 2 * HALO), lx = i % (PRE_TX + 2 * HALO);
+            const int gx = x0 + lx - HALO, gy = y0 + ly - HALO;
+            const bool in = i < NT && gx >= 0 && gx < W && gy >= 0 && gy < H;
+            const uint16_t v = *(const uint16_t*)((const char*)src + (in ? (size_t)gy * pitch + (size_t)gx * 2 : 0));
+            vals[k] = in ? v : (uint16_t)0;
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            if (i < NT) {
+                const int ly = i / (PRE_TX + 2 * HALO), lx = i % (PRE_TX + 2 * HALO);
+                tile[ly][lx] = vals[k];
+                ftile[ly][lx] = (float)vals[k];
+                big = big || vals[k] >= 46341;
+            }
+        }
     }
-    __syncthreads();
+    if (threadIdx.x < (2 * HALO + 1) * (2 * HALO + 1)) {
+        const int dy = threadIdx.x / (2 * HALO + 1) - HALO, dx = threadIdx.x % (2 * HALO + 1) - HALO;
+        sptab[dy + HALO][dx + HALO] = (float)(dx * dx + dy * dy) * ss;
+    }
+    // a depth difference of 46341 or more squares past INT_MAX, which the reference's int
+    // arithmetic wraps: such tiles take the integer loop
+    big = __syncthreads_or(big);
     const int x = x0 + tx, y = y0 + ty;
     if (x >= W || y >= H) return;
     const int value = tile[ty + HALO][tx + HALO];
@@ -45,16 +72,53 @@ k_dists_bilateral(const uint16_t* __restrict__ src, size_t pitch, int W, int H, 
     const int cxs = x - half > 0 ? x - half : 0;
     const int cys = y - half > 0 ? y - half : 0;
     float sum1 = 0.f, sum2 = 0.f;
-    for (int cy = cys; cy < tye; ++cy)
-        for (int cx = cxs; cx < txe; ++cx) {
-            int depth = tile[cy - y0 + HALO][cx - x0 + HALO];
-            float space2 = (float)((x - cx) * (x - cx) + (y - cy) * (y - cy));
-            unsigned dd = (unsigned)(value - depth);
-            float color2 = (float)(int)(dd * dd);
-            float weight = tf_exp(-(space2 * ss + color2 * sd));
-            sum1 += (float)depth * weight;
-            sum2 += weight;
+    if (!big) {
+        // two taps per step in packed f32 (v_pk_*): the same operations per tap as the integer
+        // loop below -- space2 * ss from the table, color2 = RN(d * d) == (float)(int)(d * d)
+        // for |d| < 46341, tf_exp's own steps (its t >= 128 branch cannot occur: the argument
+        // is <= 0) -- and the sums accumulated tap by tap in the reference's order
+        const tf_f2 vf = { (float)value, (float)value }, sdv = { sd, sd }, nl2e = { -1.44269504088896341f, -1.44269504088896341f };
+        for (int cy = cys; cy < tye; ++cy) {
+            const float* frow = &ftile[cy - y0 + HALO][0];
+            const float* srow = &sptab[y - cy + HALO][0];
+            for (int cx = cxs; cx < txe; cx += 2) {
+                const bool two = cx + 1 < txe;
+                const tf_f2 df = { frow[cx - x0 + HALO], frow[cx + 1 - x0 + HALO] };
+                const tf_f2 spp = { srow[x - cx + HALO], srow[x - cx - 1 + HALO + (two ? 0 : 1)] };
+                const tf_f2 dd = vf - df;
+                const tf_f2 c2 = dd * dd;
+                const tf_f2 arg = spp + c2 * sdv;
+                const tf_f2 t = arg * nl2e;                       // == (-arg) * log2(e)
+                const float k0 = rintf(t.x), k1 = rintf(t.y);
+                const tf_f2 k = { k0, k1 };
+                const tf_f2 f = t - k;
+                tf_f2 pp = { 1.5403530393381606e-4f, 1.5403530393381606e-4f };
+                pp = __builtin_elementwise_fma(pp, f, (tf_f2){ 1.3333558146428443e-3f, 1.3333558146428443e-3f });
+                pp = __builtin_elementwise_fma(pp, f, (tf_f2){ 9.6181291076284772e-3f, 9.6181291076284772e-3f });
+                pp = __builtin_elementwise_fma(pp, f, (tf_f2){ 5.5504108664821580e-2f, 5.5504108664821580e-2f });
+                pp = __builtin_elementwise_fma(pp, f, (tf_f2){ 2.4022650695910071e-1f, 2.4022650695910071e-1f });
+                pp = __builtin_elementwise_fma(pp, f, (tf_f2){ 6.9314718055994531e-1f, 6.9314718055994531e-1f });
+                pp = __builtin_elementwise_fma(pp, f, (tf_f2){ 1.0f, 1.0f });
+                const float w0 = (t.x > -125.0f) ? ldexpf(pp.x, (int)k0) : 0.0f;
+                const float w1 = (t.y > -125.0f) ? ldexpf(pp.y, (int)k1) : 0.0f;
+                const tf_f2 w = { w0, w1 };
+                const tf_f2 prod = df * w;
+                sum1 += prod.x; sum2 += w.x;
+                if (two) { sum1 += prod.y; sum2 += w.y; }
+            }
         }
+    } else {
+        for (int cy = cys; cy < tye; ++cy)
+            for (int cx = cxs; cx < txe; ++cx) {
+                int depth = tile[cy - y0 + HALO][cx - x0 + HALO];
+                float space2 = (float)((x - cx) * (x - cx) + (y - cy) * (y - cy));
+                unsigned dd = (unsigned)(value - depth);
+                float color2 = (float)(int)(dd * dd);
+                float weight = tf_exp(-(space2 * ss + color2 * sd));
+                sum1 += (float)depth * weight;
+                sum2 += weight;
+            }
+    }
     float q = sum1 / sum2;
     int v = (q == q) ? (int)rintf(q) : 0;                 // __float2int_rn
     uint16_t out = (uint16_t)v;
@@ -135,9 +199,22 @@ k_pyr_normals(PyrArgs a)
     const int X0 = blockIdx.x * PN_T0, Y0 = blockIdx.y * PN_T0;
     const int X1 = X0 / 2, Y1 = Y0 / 2, X2 = X0 / 4, Y2 = Y0 / 4;
     const int o0x = X0 - 6, o0y = Y0 - 6, o1x = X1 - 2, o1y = Y1 - 2;
-    for (int i = threadIdx.x; i < PN_R0 * PN_R0; i += 256) {
-        const int gy = o0y + i / PN_R0, gx = o0x + i % PN_R0;
-        s0[i] = (gx >= 0 && gx < W0 && gy >= 0 && gy < H0) ? a.d0[gy * W0 + gx] : 0;
+    {   // all loads of the staging tile first (clamped), then the LDS writes: one round trip
+        constexpr int PER = (PN_R0 * PN_R0 + 255) / 256;
+        uint16_t vals[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            const int gy = o0y + i / PN_R0, gx = o0x + i % PN_R0;
+            const bool in = i < PN_R0 * PN_R0 && gx >= 0 && gx < W0 && gy >= 0 && gy < H0;
+            const uint16_t v = a.d0[in ? gy * W0 + gx : 0];
+            vals[k] = in ? v : (uint16_t)0;
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            if (i < PN_R0 * PN_R0) s0[i] = vals[k];
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < PN_R1 * PN_R1; i += 256) {

@@ -719,19 +719,17 @@ struct IcpMapArgs {
     float voxelSize;
 };
 
+// processPixelICP of pixel (x, y) from it and its four neighbours (already loaded)
 __device__ __forceinline__ void icp_pixel(const IcpMapArgs& a, float lx, float ly, float lz, int x, int y,
-                                          float4* po, float4* no)
+                                          const float4& p, const float4& xp, const float4& xm, const float4& yp,
+                                          const float4& ym, float4* po, float4* no)
 {
-    const float4* ray = a.ray;
     const int W = a.W, H = a.H;
-    float4 p = ray[x + y * W];
     bool found = p.w > 0.0f;
     float n0 = 0, n1 = 0, n2 = 0;
     if (found) {
         if (y <= 1 || y >= H - 2 || x <= 1 || x >= W - 2) found = false;
         else {
-            float4 xp = ray[(x + 1) + y * W], yp = ray[x + (y + 1) * W];
-            float4 xm = ray[(x - 1) + y * W], ym = ray[x + (y - 1) * W];
             if (xp.w <= 0 || yp.w <= 0 || xm.w <= 0 || ym.w <= 0) found = false;
             else {
                 float dx0 = xp.x - xm.x, dx1 = xp.y - xm.y, dx2 = xp.z - xm.z;
@@ -786,13 +784,30 @@ k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
     const int W = a.W, H = a.H, w1 = W >> 1, h1 = H >> 1, w2 = W >> 2, h2 = H >> 2;
     const float lx = -st->M_ray[8], ly = -st->M_ray[9], lz = -st->M_ray[10];
     float4 v[4], n[4];
+    {
+        // the 4x4 neighbourhood of the quad minus its corners, twelve loads in flight together
+        // (clamped into the image: a clamped sample is only ever needed where processPixelICP's
+        // border test has already failed)
+        const int xb = 2 * x1, yb = 2 * y1;
+        float4 nb[4][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int x = 2 * x1 + (q & 1), y = 2 * y1 + (q >> 1);
-        if (x < W && y < H) {
-            icp_pixel(a, lx, ly, lz, x, y, &v[q], &n[q]);
-            a.pts[0][y * W + x] = v[q];
-            a.nrm[0][y * W + x] = n[q];
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if ((j == 0 || j == 3) && (i == 0 || i == 3)) continue;
+                const int xx = min(max(xb - 1 + i, 0), W - 1), yy = min(max(yb - 1 + j, 0), H - 1);
+                nb[j][i] = a.ray[yy * W + xx];
+            }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int qx = q & 1, qy = q >> 1;
+            const int x = xb + qx, y = yb + qy;
+            if (x < W && y < H) {
+                icp_pixel(a, lx, ly, lz, x, y, nb[1 + qy][1 + qx], nb[1 + qy][2 + qx], nb[1 + qy][qx],
+                          nb[2 + qy][1 + qx], nb[qy][1 + qx], &v[q], &n[q]);
+                a.pts[0][y * W + x] = v[q];
+                a.nrm[0][y * W + x] = n[q];
+            }
         }
     }
     if (x1 < w1 && y1 < h1) {
