@@ -971,6 +971,7 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
     int cdone = 0;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int4 b = a.box[i];
+        const float2 zr = a.z[i];            // (loaded with the box: one round trip)
         if (b.x < 0) continue;
         if (capped) {
             const int ch = i / ED_CHUNK;     // i grows monotonically: extend the chunk prefix
@@ -978,7 +979,6 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
             const unsigned need = (unsigned)a.tiles[i], off = cprefix + (unsigned)a.off[i];
             if (!(need && off + need <= a.cap)) continue;
         }
-        const float2 zr = a.z[i];
         const int zmin = __float_as_int(zr.x), zmax = __float_as_int(zr.y);   // positive floats order as ints
         const int bw = b.z - b.x + 1, npx = bw * (b.w - b.y + 1);
         for (int k = threadIdx.x; k < npx; k += 256) {

@@ -65,14 +65,36 @@ __global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_
         // only ones not at Voxel_s(), and the free lists are still the identity.
         const int first = st->lastFreeBlockId + 1 < 0 ? 0 : st->lastFreeBlockId + 1;
         const size_t n_used4 = (size_t)(n_blocks - first) * (TF_BLK3 / 4);
-        for (size_t i = tid; i < n_used4; i += stride)
-            v4[(size_t)allocList[first + (int)(i / (TF_BLK3 / 4))] * (TF_BLK3 / 4) + i % (TF_BLK3 / 4)] = vfill;
+        for (size_t i0 = tid; i0 < n_used4; i0 += 8 * stride) {   // 8 list loads in flight per lane
+            int blk[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const size_t i = i0 + k * stride;
+                blk[k] = allocList[first + (int)((i < n_used4 ? i : i0) / (TF_BLK3 / 4))];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const size_t i = i0 + k * stride;
+                if (i < n_used4) v4[(size_t)blk[k] * (TF_BLK3 / 4) + i % (TF_BLK3 / 4)] = vfill;
+            }
+        }
     }
-    for (size_t i = tid; i < (size_t)n_total; i += stride) {
-        const TfHashEntry o = hash[i];                       // live entries (only they differ from e)
-        if (full || o.ptr >= 0) {
-            if (o.ptr >= 0 && tf_grid_in(o.x, o.y, o.z)) grid[tf_grid_cell(o.x, o.y, o.z)] = make_int2(-1, TF_VOFF_NONE);
-            hash[i] = e;
+    for (size_t i0 = tid; i0 < (size_t)n_total; i0 += 8 * stride) {   // 8 entry loads in flight per lane
+        TfHashEntry o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const size_t i = i0 + k * stride;
+            o[k] = hash[i < (size_t)n_total ? i : i0];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const size_t i = i0 + k * stride;
+            // live entries (only they differ from e)
+            if (i < (size_t)n_total && (full || o[k].ptr >= 0)) {
+                if (o[k].ptr >= 0 && tf_grid_in(o[k].x, o[k].y, o[k].z))
+                    grid[tf_grid_cell(o[k].x, o[k].y, o[k].z)] = make_int2(-1, TF_VOFF_NONE);
+                hash[i] = e;
+            }
         }
     }
     // the counters are reset by the last workgroup to finish (every workgroup has read
@@ -650,18 +672,29 @@ struct IntegArgs {
     int n_maps;
 };
 
-__device__ __forceinline__ unsigned integ_voxel(unsigned vox, float px, float py, float pz, const float* M,
-                                                const IntegArgs& a, const float* rw)
+// computeUpdatedVoxelDepthInfo (SceneReconstructionEngine.hpp:23-71) in two halves, so that
+// a lane's eight voxels (two blocks) project first, their eight depth loads go out together,
+// and the updates follow -- a depth load under the projection's early returns is a branch,
+// and eight of them in a row were eight round trips.  integ_project: false when the voxel
+// projects behind the camera or outside [1, W-2] x [1, H-2]; else its depth-image index.
+__device__ __forceinline__ bool integ_project(float px, float py, float pz, const float* M, const IntegArgs& a,
+                                              float* z, int* idx)
 {
     float pc[3];
     tf_m4v3(M, px, py, pz, 1.0f, pc);
-    if (pc[2] <= 0) return vox;
+    *z = pc[2];
+    if (pc[2] <= 0) return false;
     float ix = a.fx * pc[0] / pc[2] + a.cx;
     float iy = a.fy * pc[1] / pc[2] + a.cy;
-    if ((ix < 1) || (ix > (float)(a.W - 2)) || (iy < 1) || (iy > (float)(a.H - 2))) return vox;
-    float depth_measure = a.dists[(int)(ix + 0.5f) + (int)(iy + 0.5f) * a.W];
+    if ((ix < 1) || (ix > (float)(a.W - 2)) || (iy < 1) || (iy > (float)(a.H - 2))) return false;
+    *idx = (int)(ix + 0.5f) + (int)(iy + 0.5f) * a.W;
+    return true;
+}
+__device__ __forceinline__ unsigned integ_update(unsigned vox, float depth_measure, float z, const IntegArgs& a,
+                                                 const float* rw)
+{
     if (depth_measure <= 0.0f) return vox;
-    float eta = depth_measure - pc[2];
+    float eta = depth_measure - z;
     if (eta < -a.mu) return vox;
     short sdf = (short)(vox & 0xffff);
     int oldW = (vox >> 16) & 0xff;
@@ -689,16 +722,35 @@ __device__ __forceinline__ void nt_store16(uint4* p, uint4 v)
 }
 
 // one lane's 4 consecutive voxels (16 B) of a block: update and store
-__device__ __forceinline__ void integ_chunk(uint4 v, const TfHashEntry& e, int vx, int vy, int vz, const float* M,
-                                            const IntegArgs& a, uint4* p, const float* rw)
+// the lane's four voxels of each of two blocks (ptr < 0: no block)
+__device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry& e, const TfHashEntry& e2, int vx,
+                                           int vy, int vz, const float* M, const IntegArgs& a, uint4* p, uint4* p2,
+                                           const float* rw)
 {
-    const int gx = e.x * TF_BLK, gy = e.y * TF_BLK, gz = e.z * TF_BLK;
-    const float py = (float)(gy + vy) * a.voxelSize, pz = (float)(gz + vz) * a.voxelSize;
-    v.x = integ_voxel(v.x, (float)(gx + vx + 0) * a.voxelSize, py, pz, M, a, rw);
-    v.y = integ_voxel(v.y, (float)(gx + vx + 1) * a.voxelSize, py, pz, M, a, rw);
-    v.z = integ_voxel(v.z, (float)(gx + vx + 2) * a.voxelSize, py, pz, M, a, rw);
-    v.w = integ_voxel(v.w, (float)(gx + vx + 3) * a.voxelSize, py, pz, M, a, rw);
-    nt_store16(p, v);
+    float z[8];
+    int di[8];
+    bool ok[8];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const TfHashEntry& h = b ? e2 : e;
+        const int gx = h.x * TF_BLK, gy = h.y * TF_BLK, gz = h.z * TF_BLK;
+        const float py = (float)(gy + vy) * a.voxelSize, pz = (float)(gz + vz) * a.voxelSize;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int idx = 0;
+            ok[4 * b + k] = h.ptr >= 0 && integ_project((float)(gx + vx + k) * a.voxelSize, py, pz, M, a, &z[4 * b + k], &idx);
+            di[4 * b + k] = ok[4 * b + k] ? idx : 0;
+        }
+    }
+    float dm[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dm[k] = a.dists[di[k]];
+    unsigned w[8] = { v.x, v.y, v.z, v.w, v2.x, v2.y, v2.z, v2.w };
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (ok[k]) w[k] = integ_update(w[k], dm[k], z[k], a, rw);
+    if (e.ptr >= 0) nt_store16(p, make_uint4(w[0], w[1], w[2], w[3]));
+    if (e2.ptr >= 0) nt_store16(p2, make_uint4(w[4], w[5], w[6], w[7]));
 }
 
 __global__ void __launch_bounds__(256)
@@ -729,17 +781,17 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
     const int stride = gridDim.x * 2;
     for (int i = blockIdx.x * 2 + half; i < n; i += 2 * stride) {
         const int i2 = i + stride;
-        const TfHashEntry e = hash[visibleIds[i]];
-        TfHashEntry e2;
-        e2.ptr = -1;
-        if (i2 < n) e2 = hash[visibleIds[i2]];
+        const bool has2 = i2 < n;                    // (loads unconditional: both chains together)
+        const int id1 = visibleIds[i], id2 = visibleIds[has2 ? i2 : i];
+        const TfHashEntry e = hash[id1];
+        TfHashEntry e2 = hash[id2];
+        if (!has2) e2.ptr = -1;
         uint4* p = (uint4*)(vba + (size_t)(e.ptr < 0 ? 0 : e.ptr) * TF_BLK3 + lin);
         uint4* p2 = (uint4*)(vba + (size_t)(e2.ptr < 0 ? 0 : e2.ptr) * TF_BLK3 + lin);
         // the voxel stream is read and written once per pass: non-temporal, so it does not
         // evict the depth image every voxel samples from L2
         uint4 v = nt_load16(p), v2 = nt_load16(p2);
-        if (e.ptr >= 0) integ_chunk(v, e, vx, vy, vz, M, a, p, rw);
-        if (e2.ptr >= 0) integ_chunk(v2, e2, vx, vy, vz, M, a, p2, rw);
+        integ_pair(v, v2, e, e2, vx, vy, vz, M, a, p, p2, rw);
     }
 }
 
