@@ -59,38 +59,6 @@ struct IcpLevel {
     float min_cosine, dist2;
 };
 
-// find_coresp (points variant) + row (proj_icp.cu:80-117, 365-377)
-__device__ __forceinline__ bool icp_row(const IcpLevel& L, const float* aff, int x, int y, float* row)
-{
-    if (x >= L.W || y >= L.H) return false;
-    const int W = L.W;
-    float4 sp = L.vcurr[y * W + x];
-    tf3 s = mk3(sp.x, sp.y, sp.z);
-    if (isnan(s.x)) return false;
-    tf3 R0 = mk3(aff[0], aff[1], aff[2]), R1 = mk3(aff[4], aff[5], aff[6]), R2 = mk3(aff[8], aff[9], aff[10]);
-    s = mk3(kdot(R0, s) + aff[3], kdot(R1, s) + aff[7], kdot(R2, s) + aff[11]);
-    float coox = fmaf(L.fx, s.x / s.z, L.cx);
-    float cooy = fmaf(L.fy, s.y / s.z, L.cy);
-    if (s.z <= 0 || coox < 0 || cooy < 0 || coox >= (float)L.W || cooy >= (float)L.H) return false;
-    int tx = (int)floorf(coox), ty = (int)floorf(cooy);     // point-sampled tex2D
-    float4 dp = L.vprev[ty * W + tx];
-    tf3 d = mk3(dp.x, dp.y, dp.z);
-    if (isnan(d.x)) return false;
-    tf3 sd = sub3(s, d);
-    if (kdot(sd, sd) > L.dist2) return false;
-    float4 ncp = L.ncurr[y * W + x];
-    tf3 nc = mk3(ncp.x, ncp.y, ncp.z);
-    tf3 ns = mk3(kdot(R0, nc), kdot(R1, nc), kdot(R2, nc));
-    float4 ndp = L.nprev[ty * W + tx];
-    tf3 nd = mk3(ndp.x, ndp.y, ndp.z);
-    if (fabsf(kdot(ns, nd)) < L.min_cosine) return false;
-    tf3 cr = kcross(s, nd);
-    row[0] = cr.x; row[1] = cr.y; row[2] = cr.z;
-    row[3] = nd.x; row[4] = nd.y; row[5] = nd.z;
-    row[6] = kdot(nd, sub3(d, s));
-    return true;
-}
-
 // One exchange step of the transposed butterfly: lanes with (lane & OFF) keep the upper half
 // of the N live sums, the others the lower half; each kept sum is completed with the
 // partner lane's copy, so every sum sees the same pairings as a full xor butterfly.  The
@@ -274,6 +242,12 @@ __device__ __forceinline__ void icp_solve6_ldl(const float (&Af)[6][6], const fl
     for (int i = 0; i < 6; ++i) x[i] = (float)xs[i];
 }
 
+// rows of 4 pixels per lane with the current-frame point/normal already in registers and both
+// previous-map gathers issued before the dependent tests (defined with the persistent kernel)
+struct IpPix { float vx, vy, vz, nx, ny, nz; };
+__device__ __forceinline__ void ip_rows4(const IcpLevel& L, const float* aff, const IpPix (&px)[4],
+                                         const int (&xy)[4], float (&r)[4][7]);
+
 __global__ void __launch_bounds__(64 * ICP_WAVES)
 k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsigned* __restrict__ ticket,
            int nwg, int slots, int last_iter)
@@ -291,14 +265,23 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
         const int cta = blockIdx.x + ICP_NWG * s;
         if (cta >= L.nct) break;
         const int bx = cta % L.gx, by = cta / L.gx;
-        float r[4][7];
+        // the CTA's current maps with unconditional loads, then ip_rows4 (the per-pixel
+        // per-pixel early returns make every load a branch: ~10 round trips per CTA)
+        IpPix q[4];
+        int qxy[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            int t = lane + 64 * j;
-            if (!icp_row(L, aff, bx * 32 + (t & 31), by * 8 + (t >> 5), r[j]))
-#pragma unroll
-                for (int k = 0; k < 7; ++k) r[j][k] = 0.f;
+            const int t = lane + 64 * j;
+            const int x = bx * 32 + (t & 31), y = by * 8 + (t >> 5);
+            const bool in = x < L.W && y < L.H;
+            qxy[j] = in ? 1 : -1;
+            const int pi = in ? y * L.W + x : 0;
+            float4 v = L.vcurr[pi], n = L.ncurr[pi];
+            if (!in) { v = make_float4(0.f, 0.f, 0.f, 0.f); n = v; }
+            q[j].vx = v.x; q[j].vy = v.y; q[j].vz = v.z; q[j].nx = n.x; q[j].ny = n.y; q[j].nz = n.z;
         }
+        float r[4][7];
+        ip_rows4(L, aff, q, qxy, r);
         // steps 128 and 64 of the halving tree in registers (partial_reduce order, proj_icp.cu:137-356)
         float v[32];
         int k = 0;
@@ -485,9 +468,9 @@ __device__ __forceinline__ unsigned long long ip_load(const unsigned long long* 
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// rows of one pixel (same arithmetic as icp_row), with the current-frame point/normal in
-// registers and both previous-map loads issued before any of the dependent tests
-struct IpPix { float vx, vy, vz, nx, ny, nz; };
+// find_coresp (points variant) + row (proj_icp.cu:80-117, 365-377) for 4 pixels per lane, with
+// the current-frame point/normal in registers and both previous-map loads issued before any of
+// the dependent tests (IpPix is declared above k_icp_iter)
 
 __device__ __forceinline__ void ip_rows4(const IcpLevel& L, const float* aff, const IpPix (&px)[4],
                                          const int (&xy)[4], float (&r)[4][7])
