@@ -236,6 +236,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     memset(&s0, 0, sizeof(s0));
     for (int i = 0; i < 12; ++i) s0.pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
     s0.icp_ok = 1;
+    s0.range_full = 1;
     e = hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_ticket, 0, 64, c->stream);
     if (e == hipSuccess) e = tfk_grid_clear(c);
@@ -788,6 +789,10 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
     TF_CHECK(hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
     if (which == TF_BUF_HASH) TF_CHECK(tfk_grid_rebuild(c));       // keep the block grid exact
     if (which == TF_BUF_HASH || which == TF_BUF_VBA) c->scene_external = 1;   // next reset: full clear
+    if (which == TF_BUF_RANGE) {        // next CreateExpectedDepths initialises the whole buffer again
+        static const int one = 1;
+        TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, range_full), &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    }
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }

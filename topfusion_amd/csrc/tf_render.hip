@@ -871,11 +871,19 @@ k_ed_project(EdArgs a, const TfDevState* __restrict__ st)
 {
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int tid = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
-    {   // range image init, two pixels per 16-byte store
+    if (st->range_full) {   // range image init, two pixels per 16-byte store
         const int npx = a.W * a.H;
         float4* r4 = (float4*)a.range;
         for (int i = tid; i < (npx >> 1); i += stride) r4[i] = make_float4(TF_FAR_AWAY, TF_VERY_CLOSE, TF_FAR_AWAY, TF_VERY_CLOSE);
         if ((npx & 1) && tid == 0) a.range[npx - 1] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
+    } else {
+        // Only the /8 region (row stride W, the reference's indexing) is ever filled or read; the
+        // rest of the buffer keeps the constants its last full initialisation wrote
+        const int rc = (a.W - 1) / TF_SUBSAMPLE + 1, rr = (a.H - 1) / TF_SUBSAMPLE + 1;
+        for (int i = tid; i < rc * rr; i += stride) {
+            const int y = i / rc, x = i - y * rc;
+            a.range[x + y * a.W] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
+        }
     }
     __shared__ int wsum[4];
     const int n = st->noVisibleEntries;
@@ -966,7 +974,10 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
     }
     const unsigned total = red[0];
     const bool capped = total > a.cap;
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->noTotalBlocks = (int)(capped ? a.cap : total);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->noTotalBlocks = (int)(capped ? a.cap : total);
+        st->range_full = 0;                  // (k_ed_project has read it: the previous launch)
+    }
     unsigned cprefix = 0;                    // tiles of chunks [0, cdone)
     int cdone = 0;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {

@@ -11,6 +11,7 @@
 //   * visible list: ordered compaction by hash index.
 #include "tf_internal.h"
 
+#define TF_INTEG_STREAM_BLOCKS 16384   // 32 MiB of voxels
 #define CHUNK 4096          // hash entries per workgroup in the scan passes (256 thr x 16)
 
 // byte i (0..15) of a 16-byte group held as two 64-bit words (no dynamic register indexing)
@@ -725,7 +726,7 @@ __device__ __forceinline__ void nt_store16(uint4* p, uint4 v)
 // the lane's four voxels of each of two blocks (ptr < 0: no block)
 __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry& e, const TfHashEntry& e2, int vx,
                                            int vy, int vz, const float* M, const IntegArgs& a, uint4* p, uint4* p2,
-                                           const float* rw)
+                                           const float* rw, bool stream)
 {
     float z[8];
     int di[8];
@@ -749,8 +750,13 @@ __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry&
 #pragma unroll
     for (int k = 0; k < 8; ++k)
         if (ok[k]) w[k] = integ_update(w[k], dm[k], z[k], a, rw);
-    if (e.ptr >= 0) nt_store16(p, make_uint4(w[0], w[1], w[2], w[3]));
-    if (e2.ptr >= 0) nt_store16(p2, make_uint4(w[4], w[5], w[6], w[7]));
+    if (stream) {
+        if (e.ptr >= 0) nt_store16(p, make_uint4(w[0], w[1], w[2], w[3]));
+        if (e2.ptr >= 0) nt_store16(p2, make_uint4(w[4], w[5], w[6], w[7]));
+    } else {
+        if (e.ptr >= 0) *p = make_uint4(w[0], w[1], w[2], w[3]);
+        if (e2.ptr >= 0) *p2 = make_uint4(w[4], w[5], w[6], w[7]);
+    }
 }
 
 __global__ void __launch_bounds__(256)
@@ -769,6 +775,10 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
         }
     }
     const int n = st->noVisibleEntries;
+    // a pass over more blocks than the L2s hold streams the voxels non-temporally (so they do
+    // not evict the depth image every voxel samples); a frame's few hundred blocks stay
+    // cached for the raycasts that read them next
+    const bool stream = n > TF_INTEG_STREAM_BLOCKS;
     float M[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) M[i] = st->M_alloc[i];
@@ -790,8 +800,10 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
         uint4* p2 = (uint4*)(vba + (size_t)(e2.ptr < 0 ? 0 : e2.ptr) * TF_BLK3 + lin);
         // the voxel stream is read and written once per pass: non-temporal, so it does not
         // evict the depth image every voxel samples from L2
-        uint4 v = nt_load16(p), v2 = nt_load16(p2);
-        integ_pair(v, v2, e, e2, vx, vy, vz, M, a, p, p2, rw);
+        uint4 v, v2;
+        if (stream) { v = nt_load16(p); v2 = nt_load16(p2); }
+        else { v = *p; v2 = *p2; }
+        integ_pair(v, v2, e, e2, vx, vy, vz, M, a, p, p2, rw, stream);
     }
 }
 
