@@ -244,6 +244,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_tagged, 0, sizeof(unsigned long long) * TF_ICP_TAG_WORDS, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->allocType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->winnerKey, 0xff, sizeof(int) * ntot_pad, c->stream);
+    // the request pass counts into these; every frame's k_vis_count returns them to zero
+    if (e == hipSuccess) e = hipMemsetAsync(c->allocCounts, 0, sizeof(int) * 2 * (size_t)c->alloc_chunks, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->visType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->visibleIds, 0, sizeof(int) * (size_t)pin->vis_capacity, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->raycast, 0, sizeof(float) * 4 * npx, c->stream);

@@ -63,7 +63,8 @@ struct TfDevState {
     int n_resets;            // resets taken after ICP failures
     unsigned reset_ticket;   // k_reset_scene: workgroups done (the last one resets the counters)
     int range_full;          // CreateExpectedDepths must initialise the whole range buffer (creation, upload)
-    int pad2_[3];
+    unsigned alloc_ticket;   // k_alloc_apply under exhaustion: workgroups done (the last one allocates)
+    int pad2_[2];
     // renderImage of the frame runs on the context's render stream, overlapping the rest of
     // the frame and the next frame's preprocessing/ICP; it reads only this snapshot (taken on
     // the main stream once the previous render has finished: render_snapshot)

@@ -6,8 +6,9 @@
 // 350-479).  Here every decision is deterministic and equal to the serial order:
 //   * allocation requests: per-entry atomicMax of key = pixel*64 + step (raster order,
 //     last writer wins); the winning block position is recomputed from the key;
-//   * block / excess slots: ordered by hash index through a two-pass chunked scan
-//     (exact serial semantics, including capacity exhaustion, via a one-wave fallback);
+//   * block / excess slots: ordered by hash index through a chunked scan whose per-chunk
+//     counts the request pass accumulates (exact serial semantics, including capacity
+//     exhaustion, via a one-thread fallback in the last workgroup);
 //   * visible list: ordered compaction by hash index.
 #include "tf_internal.h"
 
@@ -280,7 +281,8 @@ __device__ __forceinline__ bool alloc_segment(const AllocArgs& a, const float* i
 // visible type; otherwise an allocation request in the bucket (1) or at the chain end (2)
 __device__ __forceinline__ void alloc_probe(const AllocArgs& a, const TfHashEntry* __restrict__ hash,
                                             unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType,
-                                            int* __restrict__ winnerKey, int bx, int by, int bz, int key)
+                                            int* __restrict__ winnerKey, int* __restrict__ counts,
+                                            int bx, int by, int bz, int key)
 {
     {
         int hashIdx = tf_hash_index(bx, by, bz, a.mask);
@@ -307,7 +309,13 @@ __device__ __forceinline__ void alloc_probe(const AllocArgs& a, const TfHashEntr
             if (!found) {
                 allocType[hashIdx] = isExcess ? 2 : 1;
                 if (!isExcess) visType[hashIdx] = 1;
-                atomicMax(&winnerKey[hashIdx], key);   // raster-order last writer
+                // raster-order last writer; the first request of an entry this frame (the key
+                // was -1) counts it for its chunk (the hash is read-only here, so an entry's
+                // request type is the same for every requester)
+                if (atomicMax(&winnerKey[hashIdx], key) < 0) {
+                    atomicAdd(&counts[2 * (hashIdx / CHUNK)], 1);
+                    if (isExcess) atomicAdd(&counts[2 * (hashIdx / CHUNK) + 1], 1);
+                }
             }
         }
     }
@@ -315,7 +323,8 @@ __device__ __forceinline__ void alloc_probe(const AllocArgs& a, const TfHashEntr
 
 __global__ void __launch_bounds__(256)
 k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
-                 unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType, int* __restrict__ winnerKey)
+                 unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType, int* __restrict__ winnerKey,
+                 int* __restrict__ counts)
 {
     if (st->abort) return;
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -343,7 +352,7 @@ k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEnt
             const int i = i0 + j;
             if (i >= noSteps) break;
             if (g[j].x >= 0) { visType[g[j].x] = 1; continue; }     // found (ptr >= 0; ptr == -1 never exists)
-            alloc_probe(a, hash, allocType, visType, winnerKey, sbx[j], sby[j], sbz[j], key0 + i);
+            alloc_probe(a, hash, allocType, visType, winnerKey, counts, sbx[j], sby[j], sbz[j], key0 + i);
         }
     }
 }
@@ -421,97 +430,13 @@ __device__ __forceinline__ int block_sum(int v)
 // ---------------------------------------------------------------------------------------
 // allocateVoxelBlocksList_device (SceneReconstructionEngine_host.cu:350-415), ordered
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
-k_alloc_count(const TfDevState* __restrict__ st, const unsigned char* __restrict__ allocType, int n_total, int* counts)
+// capacity exhaustion: the exact serial semantics of allocateVoxelBlocksList in index order
+// (SceneReconstructionEngine_host.cu:350-415), one thread
+__device__ void alloc_serial(const AllocArgs& a, TfDevState* __restrict__ st, unsigned char* __restrict__ allocType,
+                             int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
+                             unsigned char* __restrict__ visType, const int* __restrict__ allocList,
+                             const int* __restrict__ excessList, const int* __restrict__ requestList, int total12)
 {
-    if (st->abort) return;
-    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
-    int c12 = 0, c2 = 0;
-    if (base < n_total) {
-        unsigned long long lo, hi;
-        load16(allocType + base, &lo, &hi);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { unsigned t = byte16(lo, hi, i); c12 += t != 0; c2 += t == 2; }
-    }
-    int t12 = block_sum(c12);
-    int t2 = block_sum(c2);
-    if (threadIdx.x == 0) { counts[2 * blockIdx.x] = t12; counts[2 * blockIdx.x + 1] = t2; }
-}
-
-__global__ void __launch_bounds__(256)
-k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int* __restrict__ counts,
-              unsigned char* __restrict__ allocType, int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
-              unsigned char* __restrict__ visType, const int* __restrict__ allocList,
-              const int* __restrict__ excessList, int* __restrict__ requestList, int n_total)
-{
-    if (st->abort) return;
-    // prefix and totals over the per-chunk counts
-    int p12 = 0, p2 = 0, a12 = 0, a2 = 0;
-    for (int h = threadIdx.x; h < n_chunks; h += 256) {
-        int c12 = counts[2 * h], c2 = counts[2 * h + 1];
-        a12 += c12; a2 += c2;
-        if (h < (int)blockIdx.x) { p12 += c12; p2 += c2; }
-    }
-    p12 = block_sum(p12); p2 = block_sum(p2); a12 = block_sum(a12); a2 = block_sum(a2);
-    const int v0 = st->lastFreeBlockId, e0 = st->lastFreeExcessListId;
-    const bool exhausted = (a12 > v0 + 1) || (a2 > e0 + 1);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->alloc_exhausted = exhausted ? 1 : 0;
-        st->pad_[0] = a12; st->pad_[1] = a2;
-    }
-    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
-    unsigned long long lo = 0, hi = 0;
-    int l12 = 0, l2 = 0;
-    if (base < n_total) {
-        load16(allocType + base, &lo, &hi);
-        for (int i = 0; i < 16; ++i) { unsigned t = byte16(lo, hi, i); l12 += t != 0; l2 += t == 2; }
-    }
-    int tmp;
-    int r12 = p12 + block_excl_scan(l12, &tmp);
-    int r2 = p2 + block_excl_scan(l2, &tmp);
-    if (l12 == 0) return;
-    const float* invM = st->invM_alloc;
-    for (int i = 0; i < 16; ++i) {
-        int t = (int)byte16(lo, hi, i);
-        if (!t) continue;
-        int idx = base + i;
-        requestList[r12] = idx;
-        if (!exhausted) {
-            short pos[3];
-            alloc_block_from_key(a, invM, winnerKey[idx], pos);
-            TfHashEntry e; e.x = pos[0]; e.y = pos[1]; e.z = pos[2]; e.pad = 0; e.offset = 0;
-            e.ptr = allocList[v0 - r12];
-            if (t == 1) {
-                hash[idx] = e;
-                grid_set(a.grid, e, idx);
-            } else {
-                int exlOffset = excessList[e0 - r2];
-                hash[idx].offset = exlOffset + 1;
-                hash[a.n_buckets + exlOffset] = e;
-                grid_set(a.grid, e, a.n_buckets + exlOffset);
-                visType[a.n_buckets + exlOffset] = 1;
-            }
-            allocType[idx] = 0;
-            winnerKey[idx] = -1;
-        }
-        r12++;
-        if (t == 2) r2++;
-    }
-}
-
-// counter update; on capacity exhaustion the exact serial semantics in index order
-__global__ void k_alloc_finish(AllocArgs a, TfDevState* __restrict__ st, unsigned char* __restrict__ allocType,
-                               int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
-                               unsigned char* __restrict__ visType, const int* __restrict__ allocList,
-                               const int* __restrict__ excessList, const int* __restrict__ requestList)
-{
-    if (st->abort) return;
-    const int total12 = st->pad_[0], total2 = st->pad_[1];
-    if (!st->alloc_exhausted) {
-        st->lastFreeBlockId -= total12;
-        st->lastFreeExcessListId -= total2;
-        return;
-    }
     int v = st->lastFreeBlockId, e = st->lastFreeExcessListId;
     for (int r = 0; r < total12; ++r) {
         int idx = requestList[r];
@@ -552,15 +477,105 @@ __global__ void k_alloc_finish(AllocArgs a, TfDevState* __restrict__ st, unsigne
     st->lastFreeExcessListId = e;
 }
 
+
+__global__ void __launch_bounds__(256)
+k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int* __restrict__ counts,
+              unsigned char* __restrict__ allocType, int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
+              unsigned char* __restrict__ visType, const int* __restrict__ allocList,
+              const int* __restrict__ excessList, int* __restrict__ requestList, int n_total)
+{
+    if (st->abort) return;
+    // prefix and totals over the per-chunk counts
+    int p12 = 0, p2 = 0, a12 = 0, a2 = 0;
+    for (int h = threadIdx.x; h < n_chunks; h += 256) {
+        int c12 = counts[2 * h], c2 = counts[2 * h + 1];
+        a12 += c12; a2 += c2;
+        if (h < (int)blockIdx.x) { p12 += c12; p2 += c2; }
+    }
+    p12 = block_sum(p12); p2 = block_sum(p2); a12 = block_sum(a12); a2 = block_sum(a2);
+    const int v0 = st->lastFreeBlockId, e0 = st->lastFreeExcessListId;
+    const bool exhausted = (a12 > v0 + 1) || (a2 > e0 + 1);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->alloc_exhausted = exhausted ? 1 : 0;
+        st->pad_[0] = a12; st->pad_[1] = a2;
+    }
+    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
+    unsigned long long lo = 0, hi = 0;
+    int l12 = 0, l2 = 0;
+    if (base < n_total) {
+        load16(allocType + base, &lo, &hi);
+        for (int i = 0; i < 16; ++i) { unsigned t = byte16(lo, hi, i); l12 += t != 0; l2 += t == 2; }
+    }
+    int tmp;
+    int r12 = p12 + block_excl_scan(l12, &tmp);
+    int r2 = p2 + block_excl_scan(l2, &tmp);
+    const float* invM = st->invM_alloc;
+    for (int i = 0; i < 16 && l12; ++i) {
+        int t = (int)byte16(lo, hi, i);
+        if (!t) continue;
+        int idx = base + i;
+        if (exhausted) requestList[r12] = idx;
+        else {
+            short pos[3];
+            alloc_block_from_key(a, invM, winnerKey[idx], pos);
+            TfHashEntry e; e.x = pos[0]; e.y = pos[1]; e.z = pos[2]; e.pad = 0; e.offset = 0;
+            e.ptr = allocList[v0 - r12];
+            if (t == 1) {
+                hash[idx] = e;
+                grid_set(a.grid, e, idx);
+            } else {
+                int exlOffset = excessList[e0 - r2];
+                hash[idx].offset = exlOffset + 1;
+                hash[a.n_buckets + exlOffset] = e;
+                grid_set(a.grid, e, a.n_buckets + exlOffset);
+                visType[a.n_buckets + exlOffset] = 1;
+            }
+            allocType[idx] = 0;
+            winnerKey[idx] = -1;
+        }
+        r12++;
+        if (t == 2) r2++;
+    }
+    // Without exhaustion the counters drop by the totals (k_vis_count, next launch: every
+    // workgroup here has read them).  With it, the workgroup that finishes last takes the
+    // requests in index order, serially; requestList is handed over with the agent-scope
+    // release -> ticket -> acquire of MI355X_MICROARCH.md "Valid forms".
+    if (!exhausted) return;
+    __shared__ int last_s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last_s = __hip_atomic_fetch_add(&st->alloc_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last_s || threadIdx.x != 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    st->alloc_ticket = 0;
+    alloc_serial(a, st, allocType, winnerKey, hash, visType, allocList, excessList, requestList, a12);
+}
+
+
 // ---------------------------------------------------------------------------------------
 // buildVisibleList_device<false> (SceneReconstructionEngine_host.cu:434-479) with
 // checkBlockVisibility<false> (SceneReconstructionEngine.hpp:300-375), ordered compaction
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
-k_vis_count(VisArgs v, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
-            unsigned char* __restrict__ visType, int* __restrict__ counts)
+k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+            unsigned char* __restrict__ visType, int* __restrict__ counts, int* __restrict__ allocCounts)
 {
     if (st->abort) return;
+    if (threadIdx.x == 0) {
+        // this frame's allocation is done: its chunk counters go back to zero for the next
+        // frame's requests, and (without exhaustion) the free-list counters drop by the totals
+        allocCounts[2 * blockIdx.x] = 0;
+        allocCounts[2 * blockIdx.x + 1] = 0;
+        if (blockIdx.x == 0 && !st->alloc_exhausted) {
+            st->lastFreeBlockId -= st->pad_[0];
+            st->lastFreeExcessListId -= st->pad_[1];
+        }
+    }
     const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
     int cnt = 0;
     if (base < v.n_total) {
@@ -639,16 +654,12 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot)
     hipLaunchKernelGGL(k_set_type3, dim3(256), dim3(256), 0, c->stream, v, c->st, c->hash, c->visibleIds, c->visType,
                        (const float2*)c->range, snapshot ? (float2*)c->range_render : nullptr);
     hipLaunchKernelGGL(k_alloc_requests, dim3((c->W + 15) / 16, (c->H + 15) / 16), dim3(256), 0, c->stream,
-                       a, c->st, c->hash, c->allocType, c->visType, c->winnerKey);
-    hipLaunchKernelGGL(k_alloc_count, dim3(c->alloc_chunks), dim3(256), 0, c->stream, c->st, c->allocType, c->n_total,
-                       c->allocCounts);
+                       a, c->st, c->hash, c->allocType, c->visType, c->winnerKey, c->allocCounts);
     hipLaunchKernelGGL(k_alloc_apply, dim3(c->alloc_chunks), dim3(256), 0, c->stream, a, c->st, c->alloc_chunks,
                        c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
                        c->requestList, c->n_total);
-    hipLaunchKernelGGL(k_alloc_finish, dim3(1), dim3(1), 0, c->stream, a, c->st, c->allocType, c->winnerKey, c->hash,
-                       c->visType, c->allocList, c->excessList, c->requestList);
     hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
-                       c->visCounts);
+                       c->visCounts, c->allocCounts);
     hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
                        c->visCounts, c->visType, c->visibleIds);
     return hipGetLastError();
