@@ -280,6 +280,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         if (sc && sc[0] >= '0' && sc[0] <= '3') c->icp_sched = sc[0] - '0';
         const char* rm = getenv("TFUSION_RENDER_MODE");
         c->render_mode = (rm && rm[0] >= '0' && rm[0] <= '3') ? rm[0] - '0' : 3;
+        const char* la = getenv("TFUSION_LOOKAHEAD");   // 0: every frame preprocesses itself
+        c->lookahead = !(la && la[0] == '0');
     }
     *out = c;
     return TF_OK;
@@ -355,6 +357,7 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
     for (int f = 0; f < n; ++f)
         for (int i = 0; i < TF_NUM_STAGES; ++i) {
             if (!c->prof_slot_on[first + f] || !((c->prof_mask >> i) & 1u) || !stage_ran(i, mode[f], ok[f])) continue;
+            if (i == TF_STAGE_PREPROCESS && !c->prof_slot_pre[first + f]) continue;   // done by the previous frame
             if (i == TF_STAGE_RAYCAST_RENDER && c->render_mode == 3) continue;   // fused into RAYCAST_ICP
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, prof_event(c, first + f, 2 * i), prof_event(c, first + f, 2 * i + 1)) == hipSuccess) {
@@ -370,18 +373,28 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
 // decided on the device: the preprocess kernel starts the frame (tf_frame_begin sets
 // st->mode), every later kernel checks st->mode / st->abort, and the gated reset kernel ends
 // it (frame counters, per-slot ok flag).  A batch is therefore enqueued back to back.
-static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, int slot)
+//
+// Lookahead (batches, fused render): when the batch holds the next frame, its preprocessing
+// runs in this frame's grid tails -- the bilateral pass in k_alloc_requests, computeDists +
+// pyramids + normals in k_raycast_pair -- and the next enqueue skips it (pre_done).  The
+// preprocessing is a pure function of the raw frame; the buffers it writes are past their last
+// reader of this frame by then (level-0 depth: this frame's pyramid pass; dists and the
+// current maps: its allocation, integration and ICP).  (Measured before: preprocessing on a
+// stream of its own costs more in cross-stream waits than the overlap saves.)
+static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, int slot,
+                               const uint16_t* next = nullptr, int pre_done = 0)
 {
     c->prof_slot_on[slot] = c->prof_enabled && (c->prof_seq++ % c->prof_period) == 0;
-    // preprocessing (topfu.cpp:166-197).  (Measured: on a stream of its own, overlapping the
-    // previous frame's tail, the cross-stream waits cost more than the overlap saves.)
-    STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, c->stream));
+    c->prof_slot_pre[slot] = !pre_done;
+    if (c->render_mode != 3) next = nullptr;
+    // preprocessing (topfu.cpp:166-197)
+    if (!pre_done) STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, c->stream));
     STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1));                           // frame begin + topfu.cpp:242-243 (tracking only)
     // the previous frame's renderImage (render stream) must be done before the scene changes
     // (modes 2 and 3 render on the main stream: no wait -- an event wait is a barrier packet,
     // a few microseconds of dispatch gap even when the event has long completed)
     if (c->render_mode <= 1) TF_CHECK(join_render(c));
-    STAGE(TF_STAGE_ALLOC, tfk_alloc(c, 1));                          // topfu.cpp:202 / 281 (+ renderImage snapshot)
+    STAGE(TF_STAGE_ALLOC, tfk_alloc(c, 1, next, pitch));                        // topfu.cpp:202 / 281 (+ renderImage snapshot)
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1));                  // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
     // renderImage (raycast + grey, topfu.cpp:284-285) on the render stream, behind integration;
     // it overlaps CreateExpectedDepths / CreateICPMaps and the next frame's preprocessing + ICP,
@@ -396,7 +409,7 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     }
     STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c));         // topfu.cpp:306
     if (c->render_mode == 3)    // CreateICPMaps raycast + renderImage in one launch (snapshot range)
-        STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c));            // topfu.cpp:284-285 + 307
+        STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, next, pitch));        // topfu.cpp:284-285 + 307
     else
         STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));              // CreateICPMaps, topfu.cpp:307
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps(c));                       // + resizePointsNormals :308-309
@@ -520,12 +533,15 @@ extern "C" tf_status tf_process_frame_host(tf_ctx* c, const uint16_t* host_depth
 extern "C" tf_status tf_process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t stride, int n, int* ok_out)
 {
     if (!c || !dev_frames || n < 0) return TF_INVALID_ARG;
+    int pre_done = 0;
     for (int first = 0; first < n; first += TF_PROF_RING) {
         const int m = n - first < TF_PROF_RING ? n - first : TF_PROF_RING;
         for (int i = 0; i < m; ++i) {
             const uint16_t* f = (const uint16_t*)((const char*)dev_frames + (size_t)(first + i) * stride);
-            tf_status s = enqueue_frame(c, f, (size_t)c->W * 2, i);
+            const uint16_t* next = (c->lookahead && first + i + 1 < n) ? (const uint16_t*)((const char*)f + stride) : nullptr;
+            tf_status s = enqueue_frame(c, f, (size_t)c->W * 2, i, next, pre_done);
             if (s != TF_OK) return s;
+            pre_done = next != nullptr && c->render_mode == 3;
         }
         tf_status s = finish_frames(c, 0, m, ok_out ? ok_out + first : nullptr);
         if (s != TF_OK && s != TF_ICP_FAIL) return s;

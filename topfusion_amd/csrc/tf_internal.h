@@ -298,6 +298,7 @@ struct tf_ctx {
     int n_resets;            // host mirror of st->n_resets
     int* frame_ok;           // per enqueued frame of a batch: 1 ok, 0 ICP failure (reset), -1 error
     int* frame_mode;         // per enqueued frame of a batch: st->mode it ran with
+    int lookahead;           // batches: the next frame's preprocessing in this frame's grid tails
     int alloc_chunks;        // N_tot / 4096
     int vis_chunks;
     // per-stage HIP-event timing on the context stream (tf_profile_*)
@@ -306,6 +307,7 @@ struct tf_ctx {
     int prof_period;         // time every prof_period-th enqueued frame (1 = every frame)
     long long prof_seq;      // frames enqueued since profiling was configured
     unsigned char prof_slot_on[TF_PROF_RING];   // batch slot carries stage events
+    unsigned char prof_slot_pre[TF_PROF_RING];  // batch slot ran its own preprocessing (no lookahead)
     hipEvent_t prof_ev[2 * TF_NUM_STAGES * TF_PROF_RING];
     double prof_ms[TF_NUM_STAGES];
     long long prof_count[TF_NUM_STAGES];
@@ -323,12 +325,14 @@ hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot);   // frame end + Res
 hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a hash upload)
 hipError_t tfk_grid_clear(tf_ctx* c);     // every cell (-1, TF_VOFF_NONE)
 hipError_t tfk_check_div3(tf_ctx* c, float d, int* ok);   // tf_div_exact3(x, d) == x / d over a binade
-hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0);   // snapshot: + the frame's renderImage snapshot
+hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0,       // snapshot: + the frame's renderImage snapshot
+                     const uint16_t* next = nullptr, size_t next_pitch = 0);   // next: + that frame's bilateral pass
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_type(tf_ctx* c, int type);   // RenderImage pixel stage (tf_render_type) on raycast
 hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);
-hipError_t tfk_raycast_pair(tf_ctx* c);   // CreateICPMaps raycast + renderImage, one launch (frame path)    // renderImage raycast + grey, fused (frame path, render stream)
+// CreateICPMaps raycast + renderImage, one launch (frame path); next: + that frame's dists/pyramid/normals
+hipError_t tfk_raycast_pair(tf_ctx* c, const uint16_t* next = nullptr, size_t next_pitch = 0);
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_expected_depths(tf_ctx* c);
 hipError_t tfk_frame0_matrices(tf_ctx* c);

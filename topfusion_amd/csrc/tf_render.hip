@@ -10,6 +10,7 @@
 //                   init+project, (cap check), fill with integer atomics on the positive
 //                   float bit patterns (the reference's float CAS loops, CUDAUtils.hpp:75-95)
 #include "tf_internal.h"
+#include "tf_preproc.h"
 
 struct SceneView {
     const TfHashEntry* hash;
@@ -514,10 +515,18 @@ k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles
 // draining alone.  (Measured: marching both rays of a pixel interleaved in one thread, sharing
 // each step's round trips, is slower -- 142 VGPRs halve the resident waves.)
 __global__ void __launch_bounds__(256)
-k_raycast_pair(RayArgs ai, RayArgs ar, const TfDevState* __restrict__ st, int tiles_x, int n_tiles, int nb)
+k_raycast_pair(RayArgs ai, RayArgs ar, const TfDevState* __restrict__ st, int tiles_x, int n_tiles, int nb,
+               PyrArgs next, int next_gx)
 {
     if ((int)blockIdx.x < nb) raycast_tile<1>(ai, st, blockIdx.x, tiles_x, n_tiles);
-    else raycast_tile<2>(ar, st, blockIdx.x - nb, tiles_x, n_tiles);
+    else if ((int)blockIdx.x < 2 * nb) raycast_tile<2>(ar, st, blockIdx.x - nb, tiles_x, n_tiles);
+    else {
+        // the batch's next frame: computeDists + pyramids + normals in this grid's tail (this
+        // frame's allocation and integration, the last readers of dists and of the current
+        // maps, are done; its bilateral pass ran in k_alloc_requests)
+        const int b = (int)blockIdx.x - 2 * nb;
+        pyr_normals_block(next, b % next_gx, b / next_gx);
+    }
 }
 
 static void ray_args(tf_ctx* c, RayArgs& a)
@@ -554,7 +563,7 @@ hipError_t tfk_raycast(tf_ctx* c, int update_visible)
 // the render stream behind the frame's integration and reads the range-image snapshot.
 // CreateICPMaps' raycast + the frame's renderImage in one launch (main stream, after
 // CreateExpectedDepths)
-hipError_t tfk_raycast_pair(tf_ctx* c)
+hipError_t tfk_raycast_pair(tf_ctx* c, const uint16_t* next, size_t next_pitch)
 {
     RayArgs ai, ar;
     ray_args(c, ai);
@@ -564,7 +573,15 @@ hipError_t tfk_raycast_pair(tf_ctx* c)
     ar.grey = c->grey;
     const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty;
     const int nb = (n + 7) / 8 * 8;
-    hipLaunchKernelGGL(k_raycast_pair, dim3(2 * nb), dim3(256), 0, c->stream, ai, ar, c->st, tx, n, nb);
+    BilArgs bn; PyrArgs pn;
+    int n_next = 0, next_gx = 1;
+    if (next) {
+        const hipError_t e = tf_pre_args(c, next, next_pitch, 1, &bn, &pn);
+        if (e != hipSuccess) return e;
+        next_gx = tf_div_up(c->W, PN_T0);
+        n_next = next_gx * tf_div_up(c->H, PN_T0);
+    } else pn = PyrArgs{};
+    hipLaunchKernelGGL(k_raycast_pair, dim3(2 * nb + n_next), dim3(256), 0, c->stream, ai, ar, c->st, tx, n, nb, pn, next_gx);
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 //     exhaustion, via a one-thread fallback in the last workgroup);
 //   * visible list: ordered compaction by hash index.
 #include "tf_internal.h"
+#include "tf_preproc.h"
 
 #define TF_INTEG_STREAM_BLOCKS 16384   // 32 MiB of voxels
 #define CHUNK 4096          // hash entries per workgroup in the scan passes (256 thr x 16)
@@ -324,10 +325,19 @@ __device__ __forceinline__ void alloc_probe(const AllocArgs& a, const TfHashEntr
 __global__ void __launch_bounds__(256)
 k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
                  unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType, int* __restrict__ winnerKey,
-                 int* __restrict__ counts)
+                 int* __restrict__ counts, int gx, int n_alloc, BilArgs next, int next_gx)
 {
+    if ((int)blockIdx.x >= n_alloc) {
+        // the batch's next frame: its bilateral pass in this grid's tail (it reads only that
+        // frame's raw depth and writes only the level-0 depth, which nothing of this frame
+        // reads after preprocessing; not gated by this frame's abort)
+        const int b = (int)blockIdx.x - n_alloc;
+        bilateral_block(next, b % next_gx, b / next_gx);
+        return;
+    }
     if (st->abort) return;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int bx = (int)blockIdx.x % gx, by = (int)blockIdx.x / gx;
+    const int x = bx * 16 + (threadIdx.x & 15), y = by * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.H) return;
     float point[3], dir[3]; int noSteps;
     if (!alloc_segment(a, st->invM_alloc, x, y, point, dir, &noSteps)) return;
@@ -644,7 +654,7 @@ static AllocArgs make_alloc_args(tf_ctx* c)
 
 // AllocateSceneFromDepth (SceneReconstructionEngine_host.cu:75-195) with the matrices
 // already in st->M_alloc / st->invM_alloc
-hipError_t tfk_alloc(tf_ctx* c, int snapshot)
+hipError_t tfk_alloc(tf_ctx* c, int snapshot, const uint16_t* next, size_t next_pitch)
 {
     AllocArgs a = make_alloc_args(c);
     VisArgs v;
@@ -653,8 +663,17 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot)
     v.W = c->W; v.H = c->H; v.n_total = c->n_total; v.cap = c->p.vis_capacity;
     hipLaunchKernelGGL(k_set_type3, dim3(256), dim3(256), 0, c->stream, v, c->st, c->hash, c->visibleIds, c->visType,
                        (const float2*)c->range, snapshot ? (float2*)c->range_render : nullptr);
-    hipLaunchKernelGGL(k_alloc_requests, dim3((c->W + 15) / 16, (c->H + 15) / 16), dim3(256), 0, c->stream,
-                       a, c->st, c->hash, c->allocType, c->visType, c->winnerKey, c->allocCounts);
+    const int gx = (c->W + 15) / 16, n_alloc = gx * ((c->H + 15) / 16);
+    BilArgs nb; PyrArgs np;
+    int n_next = 0, next_gx = 1;
+    if (next) {
+        const hipError_t e = tf_pre_args(c, next, next_pitch, 1, &nb, &np);
+        if (e != hipSuccess) return e;
+        next_gx = tf_div_up(c->W, PRE_TX);
+        n_next = next_gx * tf_div_up(c->H, PRE_TY);
+    } else nb = BilArgs{};
+    hipLaunchKernelGGL(k_alloc_requests, dim3(n_alloc + n_next), dim3(256), 0, c->stream,
+                       a, c->st, c->hash, c->allocType, c->visType, c->winnerKey, c->allocCounts, gx, n_alloc, nb, next_gx);
     hipLaunchKernelGGL(k_alloc_apply, dim3(c->alloc_chunks), dim3(256), 0, c->stream, a, c->st, c->alloc_chunks,
                        c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
                        c->requestList, c->n_total);
