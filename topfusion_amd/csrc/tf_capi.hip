@@ -98,7 +98,8 @@ static void ctx_free(tf_ctx* c)
     // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
     float4* maps[4] = { c->curr_pts[0], c->curr_nrm[0], c->prev_pts[0], c->prev_nrm[0] };
     for (float4* m : maps) if (m) (void)hipFree(m);
-    for (int l = 0; l < TF_LEVELS; ++l) if (c->depth_pyr[l]) (void)hipFree(c->depth_pyr[l]);
+    for (int l = 1; l < TF_LEVELS; ++l) if (c->depth_pyr[l]) (void)hipFree(c->depth_pyr[l]);
+    for (int k = 0; k < 2; ++k) if (c->d0_buf[k]) (void)hipFree(c->d0_buf[k]);
     if (c->st_host) (void)hipHostFree(c->st_host);
     for (int i = 0; i < 2 * TF_NUM_STAGES * TF_PROF_RING; ++i) if (c->prof_ev[i]) (void)hipEventDestroy(c->prof_ev[i]);
     if (c->ev_integrated) (void)hipEventDestroy(c->ev_integrated);
@@ -220,7 +221,9 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
             c->curr_pts[l] = c->curr_pts[l - 1] + off; c->curr_nrm[l] = c->curr_nrm[l - 1] + off;
             c->prev_pts[l] = c->prev_pts[l - 1] + off; c->prev_nrm[l] = c->prev_nrm[l - 1] + off;
         }
-        for (int l = 0; l < TF_LEVELS; ++l) ALLOC(c->depth_pyr[l], sizeof(uint16_t) * (size_t)c->lw[l] * c->lh[l]);
+        for (int l = 1; l < TF_LEVELS; ++l) ALLOC(c->depth_pyr[l], sizeof(uint16_t) * (size_t)c->lw[l] * c->lh[l]);
+        for (int k = 0; k < 2; ++k) ALLOC(c->d0_buf[k], sizeof(uint16_t) * (size_t)c->lw[0] * c->lh[0]);
+        c->depth_pyr[0] = c->d0_buf[0];
     }
     ALLOC(c->frame_ok, sizeof(int) * TF_PROF_RING);
     ALLOC(c->frame_mode, sizeof(int) * TF_PROF_RING);
@@ -281,7 +284,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         const char* rm = getenv("TFUSION_RENDER_MODE");
         c->render_mode = (rm && rm[0] >= '0' && rm[0] <= '3') ? rm[0] - '0' : 3;
         const char* la = getenv("TFUSION_LOOKAHEAD");   // 0: every frame preprocesses itself
-        c->lookahead = !(la && la[0] == '0');
+        c->lookahead = (la && la[0] >= '0' && la[0] <= '2') ? la[0] - '0' : 2;
     }
     *out = c;
     return TF_OK;
@@ -374,27 +377,39 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
 // st->mode), every later kernel checks st->mode / st->abort, and the gated reset kernel ends
 // it (frame counters, per-slot ok flag).  A batch is therefore enqueued back to back.
 //
-// Lookahead (batches, fused render): when the batch holds the next frame, its preprocessing
-// runs in this frame's grid tails -- the bilateral pass in k_alloc_requests, computeDists +
-// pyramids + normals in k_raycast_pair -- and the next enqueue skips it (pre_done).  The
-// preprocessing is a pure function of the raw frame; the buffers it writes are past their last
-// reader of this frame by then (level-0 depth: this frame's pyramid pass; dists and the
-// current maps: its allocation, integration and ICP).  (Measured before: preprocessing on a
-// stream of its own costs more in cross-stream waits than the overlap saves.)
+// Lookahead (batches, fused render): later frames' preprocessing runs in this frame's grid
+// tails and their enqueues skip it.  Two-frame (TFUSION_LOOKAHEAD=2, default): k_raycast_pair
+// of frame j runs frame j+1's computeDists + pyramids + normals and frame j+2's bilateral
+// pass, whose level-0 depth goes to the buffer of j's parity (d0_buf, ping-pong); the batch's
+// first frame also runs frame 1's bilateral pass in k_alloc_requests.  One-frame (1): frame
+// j+1's bilateral pass in k_alloc_requests, the rest in k_raycast_pair.  Preprocessing is a
+// pure function of the raw frame; what it writes is past its last reader of this frame by
+// then (level-0 depth: this frame's pyramid pass; dists and the current maps: this frame's
+// allocation, integration and ICP).  (Measured before: preprocessing on a stream of its own
+// costs more in cross-stream waits than the overlap saves.)
+struct TfFramePlan {
+    int pre_done;            // this frame's preprocessing ran in earlier launches
+    uint16_t* d0;            // this frame's level-0 depth buffer
+    TfAhead alloc_bil, pair_pyr, pair_bil;
+};
+
 static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, int slot,
-                               const uint16_t* next = nullptr, int pre_done = 0)
+                               const TfFramePlan* plan = nullptr)
 {
+    static const TfFramePlan none = { 0, nullptr, {}, {}, {} };
+    if (!plan || c->render_mode != 3) plan = &none;
+    uint16_t* d0 = plan->d0 ? plan->d0 : c->d0_buf[0];
     c->prof_slot_on[slot] = c->prof_enabled && (c->prof_seq++ % c->prof_period) == 0;
-    c->prof_slot_pre[slot] = !pre_done;
-    if (c->render_mode != 3) next = nullptr;
+    c->prof_slot_pre[slot] = !plan->pre_done;
     // preprocessing (topfu.cpp:166-197)
-    if (!pre_done) STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, c->stream));
+    if (!plan->pre_done) STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, c->stream, d0));
+    c->depth_pyr[0] = d0;
     STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1));                           // frame begin + topfu.cpp:242-243 (tracking only)
     // the previous frame's renderImage (render stream) must be done before the scene changes
     // (modes 2 and 3 render on the main stream: no wait -- an event wait is a barrier packet,
     // a few microseconds of dispatch gap even when the event has long completed)
     if (c->render_mode <= 1) TF_CHECK(join_render(c));
-    STAGE(TF_STAGE_ALLOC, tfk_alloc(c, 1, next, pitch));                        // topfu.cpp:202 / 281 (+ renderImage snapshot)
+    STAGE(TF_STAGE_ALLOC, tfk_alloc(c, 1, plan->alloc_bil, pitch));                        // topfu.cpp:202 / 281 (+ renderImage snapshot)
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1));                  // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
     // renderImage (raycast + grey, topfu.cpp:284-285) on the render stream, behind integration;
     // it overlaps CreateExpectedDepths / CreateICPMaps and the next frame's preprocessing + ICP,
@@ -409,7 +424,7 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     }
     STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c));         // topfu.cpp:306
     if (c->render_mode == 3)    // CreateICPMaps raycast + renderImage in one launch (snapshot range)
-        STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, next, pitch));        // topfu.cpp:284-285 + 307
+        STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch));        // topfu.cpp:284-285 + 307
     else
         STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));              // CreateICPMaps, topfu.cpp:307
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps(c));                       // + resizePointsNormals :308-309
@@ -533,15 +548,21 @@ extern "C" tf_status tf_process_frame_host(tf_ctx* c, const uint16_t* host_depth
 extern "C" tf_status tf_process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t stride, int n, int* ok_out)
 {
     if (!c || !dev_frames || n < 0) return TF_INVALID_ARG;
-    int pre_done = 0;
+    const int la = c->render_mode == 3 ? c->lookahead : 0;
+    auto frame = [&](int j) { return (const uint16_t*)((const char*)dev_frames + (size_t)j * stride); };
     for (int first = 0; first < n; first += TF_PROF_RING) {
         const int m = n - first < TF_PROF_RING ? n - first : TF_PROF_RING;
         for (int i = 0; i < m; ++i) {
-            const uint16_t* f = (const uint16_t*)((const char*)dev_frames + (size_t)(first + i) * stride);
-            const uint16_t* next = (c->lookahead && first + i + 1 < n) ? (const uint16_t*)((const char*)f + stride) : nullptr;
-            tf_status s = enqueue_frame(c, f, (size_t)c->W * 2, i, next, pre_done);
+            const int j = first + i;
+            TfFramePlan p = { la != 0 && j > 0, c->d0_buf[la ? j & 1 : 0], {}, {}, {} };
+            if (la && j + 1 < n) {
+                TfAhead next = { frame(j + 1), c->d0_buf[(j + 1) & 1] };
+                p.pair_pyr = next;
+                if (la == 1 || j == 0) p.alloc_bil = next;
+                if (la == 2 && j + 2 < n) p.pair_bil = TfAhead{ frame(j + 2), c->d0_buf[j & 1] };
+            }
+            tf_status s = enqueue_frame(c, frame(j), (size_t)c->W * 2, i, &p);
             if (s != TF_OK) return s;
-            pre_done = next != nullptr && c->render_mode == 3;
         }
         tf_status s = finish_frames(c, 0, m, ok_out ? ok_out + first : nullptr);
         if (s != TF_OK && s != TF_ICP_FAIL) return s;
@@ -619,7 +640,8 @@ extern "C" tf_status tf_stage_preprocess(tf_ctx* c, const uint16_t* dev_depth, s
     if (!c || !dev_depth) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
     TF_CHECK(clear_abort(c));
-    TF_CHECK(tfk_preprocess(c, dev_depth, pitch, c->stream));
+    TF_CHECK(tfk_preprocess(c, dev_depth, pitch, c->stream, c->d0_buf[0]));
+    c->depth_pyr[0] = c->d0_buf[0];
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }

@@ -278,7 +278,8 @@ struct tf_ctx {
     // frame buffers
     uint16_t* depth_in;      // staging for host uploads / pitched input
     float* dists;
-    uint16_t* depth_pyr[TF_LEVELS];
+    uint16_t* depth_pyr[TF_LEVELS];     // [0]: the level-0 buffer of the last frame preprocessed (one of d0_buf)
+    uint16_t* d0_buf[2];     // level-0 depth, ping-pong by batch frame parity (two-frame lookahead)
     float4* curr_pts[TF_LEVELS];
     float4* curr_nrm[TF_LEVELS];
     float4* prev_pts[TF_LEVELS];
@@ -298,7 +299,7 @@ struct tf_ctx {
     int n_resets;            // host mirror of st->n_resets
     int* frame_ok;           // per enqueued frame of a batch: 1 ok, 0 ICP failure (reset), -1 error
     int* frame_mode;         // per enqueued frame of a batch: st->mode it ran with
-    int lookahead;           // batches: the next frame's preprocessing in this frame's grid tails
+    int lookahead;           // batches: later frames' preprocessing in this frame's grid tails (0 off, 1 next frame, 2 two frames)
     int alloc_chunks;        // N_tot / 4096
     int vis_chunks;
     // per-stage HIP-event timing on the context stream (tf_profile_*)
@@ -316,7 +317,7 @@ struct tf_ctx {
 // ---------------------------------------------------------------------------------------
 // launchers (one per kernel family); all enqueue on ctx->stream
 // ---------------------------------------------------------------------------------------
-hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStream_t strm);   // no st access
+hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStream_t strm, uint16_t* d0);   // no st access
 hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin = 0);   // frame_begin: frame path (tf_frame_begin)
 int tfk_icp_persistent_ok(tf_ctx* c);      // k_icp_frame fits (co-residency, slot count)
 hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / raycast matrices
@@ -325,14 +326,19 @@ hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot);   // frame end + Res
 hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a hash upload)
 hipError_t tfk_grid_clear(tf_ctx* c);     // every cell (-1, TF_VOFF_NONE)
 hipError_t tfk_check_div3(tf_ctx* c, float d, int* ok);   // tf_div_exact3(x, d) == x / d over a binade
+// a later frame of the batch whose preprocessing (part) runs in a frame kernel's grid tail
+struct TfAhead {
+    const uint16_t* src;     // raw depth (nullptr: none)
+    uint16_t* d0;            // its level-0 depth buffer (d0_buf)
+};
 hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0,       // snapshot: + the frame's renderImage snapshot
-                     const uint16_t* next = nullptr, size_t next_pitch = 0);   // next: + that frame's bilateral pass
+                     TfAhead bil = TfAhead{}, size_t pitch = 0);   // bil: + that frame's bilateral pass
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_type(tf_ctx* c, int type);   // RenderImage pixel stage (tf_render_type) on raycast
 hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);
 // CreateICPMaps raycast + renderImage, one launch (frame path); next: + that frame's dists/pyramid/normals
-hipError_t tfk_raycast_pair(tf_ctx* c, const uint16_t* next = nullptr, size_t next_pitch = 0);
+hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = TfAhead{}, size_t pitch = 0);   // + dists/pyramid/normals of pyr, bilateral of bil
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_expected_depths(tf_ctx* c);
 hipError_t tfk_frame0_matrices(tf_ctx* c);

@@ -1,7 +1,8 @@
 // tf_preproc.h -- the depth preprocessing front-end's per-workgroup bodies,
-// shared by its own kernels (tf_preproc.hip) and by the frame kernels that run the NEXT
-// frame's preprocessing in their grid's tail when a batch supplies it (k_alloc_requests:
-// bilateral; k_raycast_pair: computeDists + pyramids + normals; tf_capi.hip enqueue_frame).
+// shared by its own kernels (tf_preproc.hip) and by the frame kernels that run later frames'
+// preprocessing in their grid's tail when a batch supplies them (k_raycast_pair: the next
+// frame's computeDists + pyramids + normals and the bilateral pass of the one after;
+// k_alloc_requests: a bilateral pass at the batch start; tf_capi.hip enqueue_frame).
 #pragma once
 #include "tf_internal.h"
 #include "tf_pose.h"
@@ -274,4 +275,4 @@ __device__ __forceinline__ void pyr_normals_block(const PyrArgs& a, int bx, int 
 
 
 static inline int tf_div_up(int a, int b) { return (a + b - 1) / b; }
-hipError_t tf_pre_args(tf_ctx* c, const uint16_t* depth, size_t pitch, int lookahead, BilArgs* b, PyrArgs* a);
+hipError_t tf_pre_args(tf_ctx* c, const uint16_t* depth, size_t pitch, int lookahead, uint16_t* d0, BilArgs* b, PyrArgs* a);

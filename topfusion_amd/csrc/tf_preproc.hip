@@ -15,7 +15,7 @@ __global__ void __launch_bounds__(256) k_pyr_normals(PyrArgs a) { pyr_normals_bl
 // the preprocessing arguments of raw frame `depth`; lookahead: the frame-path split in which
 // the bilateral pass leaves dists alone (the current frame's allocation / integration still
 // read them) and the pyramid pass writes them
-hipError_t tf_pre_args(tf_ctx* c, const uint16_t* depth, size_t pitch, int lookahead, BilArgs* b, PyrArgs* a)
+hipError_t tf_pre_args(tf_ctx* c, const uint16_t* depth, size_t pitch, int lookahead, uint16_t* d0, BilArgs* b, PyrArgs* a)
 {
     const tf_params& p = c->p;
     float sigma_depth = p.bilateral_sigma_depth * 1000.0f;       // meters -> mm (imgproc.cu:53)
@@ -26,11 +26,11 @@ hipError_t tf_pre_args(tf_ctx* c, const uint16_t* depth, size_t pitch, int looka
     b->do_trunc = p.icp_truncate_depth_dist > 0;
     b->trunc_mm = (unsigned)(uint16_t)(p.icp_truncate_depth_dist * 1000.f);   // imgproc.cu:87
     b->dists = lookahead ? nullptr : c->dists;
-    b->dst = c->depth_pyr[0];
+    b->dst = d0;
     a->raw = lookahead ? depth : nullptr; a->raw_pitch = pitch;
     a->dists = c->dists;
     a->sigma3 = sigma_depth * 3.0f;                                                    // imgproc.cu:138
-    a->d0 = c->depth_pyr[0]; a->d1 = c->depth_pyr[1]; a->d2 = c->depth_pyr[2];
+    a->d0 = d0; a->d1 = c->depth_pyr[1]; a->d2 = c->depth_pyr[2];
     for (int l = 0; l < TF_LEVELS; ++l) {
         int div = 1 << l;                                 // Intr::operator()(level), precomp.cpp:10-14
         a->pts[l] = c->curr_pts[l]; a->nrm[l] = c->curr_nrm[l];
@@ -40,10 +40,10 @@ hipError_t tf_pre_args(tf_ctx* c, const uint16_t* depth, size_t pitch, int looka
     return hipSuccess;
 }
 
-hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStream_t strm)
+hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStream_t strm, uint16_t* d0)
 {
     BilArgs b; PyrArgs a;
-    hipError_t e = tf_pre_args(c, depth, pitch, 0, &b, &a);
+    hipError_t e = tf_pre_args(c, depth, pitch, 0, d0, &b, &a);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_dists_bilateral, dim3(tf_div_up(c->W, PRE_TX), tf_div_up(c->H, PRE_TY)), dim3(256), 0, strm, b);
     hipLaunchKernelGGL(k_pyr_normals, dim3(tf_div_up(c->W, PN_T0), tf_div_up(c->H, PN_T0)), dim3(256), 0, strm, a);

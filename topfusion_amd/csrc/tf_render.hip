@@ -516,17 +516,18 @@ k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles
 // each step's round trips, is slower -- 142 VGPRs halve the resident waves.)
 __global__ void __launch_bounds__(256)
 k_raycast_pair(RayArgs ai, RayArgs ar, const TfDevState* __restrict__ st, int tiles_x, int n_tiles, int nb,
-               PyrArgs next, int next_gx)
+               PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx)
 {
-    if ((int)blockIdx.x < nb) raycast_tile<1>(ai, st, blockIdx.x, tiles_x, n_tiles);
-    else if ((int)blockIdx.x < 2 * nb) raycast_tile<2>(ar, st, blockIdx.x - nb, tiles_x, n_tiles);
-    else {
-        // the batch's next frame: computeDists + pyramids + normals in this grid's tail (this
-        // frame's allocation and integration, the last readers of dists and of the current
-        // maps, are done; its bilateral pass ran in k_alloc_requests)
-        const int b = (int)blockIdx.x - 2 * nb;
-        pyr_normals_block(next, b % next_gx, b / next_gx);
-    }
+    const int b = (int)blockIdx.x;
+    if (b < nb) raycast_tile<1>(ai, st, b, tiles_x, n_tiles);
+    else if (b < 2 * nb) raycast_tile<2>(ar, st, b - nb, tiles_x, n_tiles);
+    // Later frames of the batch in this grid's tail, not gated by this frame's abort: the next
+    // frame's computeDists + pyramids + normals (this frame's allocation and integration, the
+    // last readers of dists and of the current maps, are done; its level-0 depth was filtered
+    // a launch or more ago), then the bilateral pass of the frame after it (into the other
+    // level-0 buffer: this frame's, whose last reader was its own pyramid pass)
+    else if (b < 2 * nb + n_pyr) pyr_normals_block(pyr, (b - 2 * nb) % pyr_gx, (b - 2 * nb) / pyr_gx);
+    else bilateral_block(bil, (b - 2 * nb - n_pyr) % bil_gx, (b - 2 * nb - n_pyr) / bil_gx);
 }
 
 static void ray_args(tf_ctx* c, RayArgs& a)
@@ -563,7 +564,7 @@ hipError_t tfk_raycast(tf_ctx* c, int update_visible)
 // the render stream behind the frame's integration and reads the range-image snapshot.
 // CreateICPMaps' raycast + the frame's renderImage in one launch (main stream, after
 // CreateExpectedDepths)
-hipError_t tfk_raycast_pair(tf_ctx* c, const uint16_t* next, size_t next_pitch)
+hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch)
 {
     RayArgs ai, ar;
     ray_args(c, ai);
@@ -573,15 +574,22 @@ hipError_t tfk_raycast_pair(tf_ctx* c, const uint16_t* next, size_t next_pitch)
     ar.grey = c->grey;
     const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty;
     const int nb = (n + 7) / 8 * 8;
-    BilArgs bn; PyrArgs pn;
-    int n_next = 0, next_gx = 1;
-    if (next) {
-        const hipError_t e = tf_pre_args(c, next, next_pitch, 1, &bn, &pn);
+    BilArgs bb = BilArgs{}, bx; PyrArgs pp = PyrArgs{}, px;
+    int n_pyr = 0, pyr_gx = 1, n_bil = 0, bil_gx = 1;
+    if (pyr.src) {
+        const hipError_t e = tf_pre_args(c, pyr.src, pitch, 1, pyr.d0, &bx, &pp);
         if (e != hipSuccess) return e;
-        next_gx = tf_div_up(c->W, PN_T0);
-        n_next = next_gx * tf_div_up(c->H, PN_T0);
-    } else pn = PyrArgs{};
-    hipLaunchKernelGGL(k_raycast_pair, dim3(2 * nb + n_next), dim3(256), 0, c->stream, ai, ar, c->st, tx, n, nb, pn, next_gx);
+        pyr_gx = tf_div_up(c->W, PN_T0);
+        n_pyr = pyr_gx * tf_div_up(c->H, PN_T0);
+    }
+    if (bil.src) {
+        const hipError_t e = tf_pre_args(c, bil.src, pitch, 1, bil.d0, &bb, &px);
+        if (e != hipSuccess) return e;
+        bil_gx = tf_div_up(c->W, PRE_TX);
+        n_bil = bil_gx * tf_div_up(c->H, PRE_TY);
+    }
+    hipLaunchKernelGGL(k_raycast_pair, dim3(2 * nb + n_pyr + n_bil), dim3(256), 0, c->stream, ai, ar, c->st, tx, n, nb,
+                       pp, n_pyr, pyr_gx, bb, bil_gx);
     return hipGetLastError();
 }
 

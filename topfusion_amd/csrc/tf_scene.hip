@@ -328,9 +328,9 @@ k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEnt
                  int* __restrict__ counts, int gx, int n_alloc, BilArgs next, int next_gx)
 {
     if ((int)blockIdx.x >= n_alloc) {
-        // the batch's next frame: its bilateral pass in this grid's tail (it reads only that
-        // frame's raw depth and writes only the level-0 depth, which nothing of this frame
-        // reads after preprocessing; not gated by this frame's abort)
+        // a later frame of the batch: its bilateral pass in this grid's tail (it reads only that
+        // frame's raw depth and writes only its level-0 depth buffer; not gated by this
+        // frame's abort)
         const int b = (int)blockIdx.x - n_alloc;
         bilateral_block(next, b % next_gx, b / next_gx);
         return;
@@ -654,7 +654,7 @@ static AllocArgs make_alloc_args(tf_ctx* c)
 
 // AllocateSceneFromDepth (SceneReconstructionEngine_host.cu:75-195) with the matrices
 // already in st->M_alloc / st->invM_alloc
-hipError_t tfk_alloc(tf_ctx* c, int snapshot, const uint16_t* next, size_t next_pitch)
+hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch)
 {
     AllocArgs a = make_alloc_args(c);
     VisArgs v;
@@ -666,8 +666,8 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, const uint16_t* next, size_t next_
     const int gx = (c->W + 15) / 16, n_alloc = gx * ((c->H + 15) / 16);
     BilArgs nb; PyrArgs np;
     int n_next = 0, next_gx = 1;
-    if (next) {
-        const hipError_t e = tf_pre_args(c, next, next_pitch, 1, &nb, &np);
+    if (bil.src) {
+        const hipError_t e = tf_pre_args(c, bil.src, pitch, 1, bil.d0, &nb, &np);
         if (e != hipSuccess) return e;
         next_gx = tf_div_up(c->W, PRE_TX);
         n_next = next_gx * tf_div_up(c->H, PRE_TY);
