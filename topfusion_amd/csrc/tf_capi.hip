@@ -285,6 +285,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         c->render_mode = (rm && rm[0] >= '0' && rm[0] <= '3') ? rm[0] - '0' : 3;
         const char* la = getenv("TFUSION_LOOKAHEAD");   // 0: every frame preprocesses itself
         c->lookahead = (la && la[0] >= '0' && la[0] <= '2') ? la[0] - '0' : 2;
+        const char* fe = getenv("TFUSION_FUSE_ED");     // 0: k_ed_project as its own launch
+        c->fuse_ed = !(fe && fe[0] == '0');
     }
     *out = c;
     return TF_OK;
@@ -410,7 +412,8 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     // a few microseconds of dispatch gap even when the event has long completed)
     if (c->render_mode <= 1) TF_CHECK(join_render(c));
     STAGE(TF_STAGE_ALLOC, tfk_alloc(c, 1, plan->alloc_bil, pitch));                        // topfu.cpp:202 / 281 (+ renderImage snapshot)
-    STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1));                  // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
+    // (+ CreateExpectedDepths' projection pass in the same grid when fuse_ed)
+    STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1, c->fuse_ed));     // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
     // renderImage (raycast + grey, topfu.cpp:284-285) on the render stream, behind integration;
     // it overlaps CreateExpectedDepths / CreateICPMaps and the next frame's preprocessing + ICP,
     // none of which writes what it reads (the scene, the range snapshot, M_render)
@@ -422,7 +425,7 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
         STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c, c->rstream));
         TF_CHECK(hipEventRecord(c->ev_rendered, c->rstream));
     }
-    STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c));         // topfu.cpp:306
+    STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c, c->fuse_ed));   // topfu.cpp:306
     if (c->render_mode == 3)    // CreateICPMaps raycast + renderImage in one launch (snapshot range)
         STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch));        // topfu.cpp:284-285 + 307
     else

@@ -1,0 +1,111 @@
+// tf_ed.h -- CreateExpectedDepths' projection pass (VisualisationEngine_CUDA.cu:119-173) as a
+// workgroup-level device function, shared by k_ed_project (tf_render.hip) and the leading
+// workgroups of k_integrate (tf_scene.hip), which run it beside integration.
+#pragma once
+#include "tf_internal.h"
+
+struct EdArgs {
+    const TfHashEntry* hash;
+    const int* visibleIds;
+    float2* range;
+    int4* box; float2* z; int* tiles; int* off; int* chunk;
+    int W, H;
+    float fx, fy, cx, cy, voxelSize;
+    unsigned cap;
+};
+
+#define ED_CHUNK 256     // visible entries per projection chunk (one workgroup pass)
+
+// memsetKernel(FAR_AWAY, VERY_CLOSE) + ProjectSingleBlock (VisualisationEngine_Shared.hpp:33-77).
+// Visible entries are processed in chunks of 256 (thread t of a chunk pass = entry
+// chunk*256 + t).  Each chunk stores its tile total and every entry its exclusive tile offset
+// inside the chunk, so the MAX_RENDERING_BLOCKS cap (VisualisationHelper.cu:70-74) is applied
+// by k_ed_fill from plain prefix sums: no counter atomics, no last-workgroup ticket, no fence.
+// Runs as workgroup `bid` of `nblk`: its own launch (k_ed_project) or the leading workgroups
+// of k_integrate's grid (the stages share no data: both only read the visible list).
+__device__ __forceinline__ void ed_project_block(const EdArgs& a, const TfDevState* __restrict__ st, int bid, int nblk)
+{
+    if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
+    const int tid = bid * 256 + threadIdx.x, stride = nblk * 256;
+    if (st->range_full) {   // range image init, two pixels per 16-byte store
+        const int npx = a.W * a.H;
+        float4* r4 = (float4*)a.range;
+        for (int i = tid; i < (npx >> 1); i += stride) r4[i] = make_float4(TF_FAR_AWAY, TF_VERY_CLOSE, TF_FAR_AWAY, TF_VERY_CLOSE);
+        if ((npx & 1) && tid == 0) a.range[npx - 1] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
+    } else {
+        // Only the /8 region (row stride W, the reference's indexing) is ever filled or read; the
+        // rest of the buffer keeps the constants its last full initialisation wrote
+        const int rc = (a.W - 1) / TF_SUBSAMPLE + 1, rr = (a.H - 1) / TF_SUBSAMPLE + 1;
+        for (int i = tid; i < rc * rr; i += stride) {
+            const int y = i / rc, x = i - y * rc;
+            a.range[x + y * a.W] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
+        }
+    }
+    __shared__ int wsum[4];
+    const int n = st->noVisibleEntries;
+    const int nchunks = (n + ED_CHUNK - 1) / ED_CHUNK;
+    const float* M = st->M_alloc;          // pose.inv() (topfu.cpp:306)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int ch = bid; ch < nchunks; ch += nblk) {
+        const int i = ch * ED_CHUNK + threadIdx.x;
+        int ntiles = 0;
+        if (i < n) {
+            TfHashEntry e = a.hash[a.visibleIds[i]];
+            int4 box = make_int4(-1, -1, -1, -1);
+            float2 zr = make_float2(0.f, 0.f);
+            if (e.ptr >= 0) {
+                int ulx = a.W / TF_SUBSAMPLE, uly = a.H / TF_SUBSAMPLE, lrx = -1, lry = -1;
+                float zmin = TF_FAR_AWAY, zmax = TF_VERY_CLOSE;
+                for (int corner = 0; corner < 8; ++corner) {
+                    short tx = (short)(e.x + ((corner & 1) ? 1 : 0));
+                    short ty = (short)(e.y + ((corner & 2) ? 1 : 0));
+                    short tz = (short)(e.z + ((corner & 4) ? 1 : 0));
+                    float q[3];
+                    tf_m4v3(M, (float)tx * (float)TF_BLK * a.voxelSize, (float)ty * (float)TF_BLK * a.voxelSize,
+                            (float)tz * (float)TF_BLK * a.voxelSize, 1.0f, q);
+                    if ((double)q[2] < 1e-6) continue;
+                    float p2x = (a.fx * q[0] / q[2] + a.cx) / (float)TF_SUBSAMPLE;
+                    float p2y = (a.fy * q[1] / q[2] + a.cy) / (float)TF_SUBSAMPLE;
+                    if ((float)ulx > floorf(p2x)) ulx = (int)floorf(p2x);
+                    if ((float)lrx < ceilf(p2x)) lrx = (int)ceilf(p2x);
+                    if ((float)uly > floorf(p2y)) uly = (int)floorf(p2y);
+                    if ((float)lry < ceilf(p2y)) lry = (int)ceilf(p2y);
+                    if (zmin > q[2]) zmin = q[2];
+                    if (zmax < q[2]) zmax = q[2];
+                }
+                if (ulx < 0) ulx = 0;
+                if (uly < 0) uly = 0;
+                if (lrx >= a.W) lrx = a.W - 1;
+                if (lry >= a.H) lry = a.H - 1;
+                bool valid = !(ulx > lrx || uly > lry);
+                if (valid && zmin < TF_VERY_CLOSE) zmin = TF_VERY_CLOSE;
+                if (valid && zmax < TF_VERY_CLOSE) valid = false;
+                if (valid) {
+                    int nbx = (int)ceilf((float)(lrx - ulx + 1) / TF_RB_SIZE);
+                    int nby = (int)ceilf((float)(lry - uly + 1) / TF_RB_SIZE);
+                    ntiles = nbx * nby;
+                    box = make_int4(ulx, uly, lrx, lry);
+                    zr = make_float2(zmin, zmax);
+                }
+            }
+            a.box[i] = box; a.z[i] = zr; a.tiles[i] = ntiles;
+        }
+        // exclusive prefix of the tile counts inside the chunk (wave scan + 4 wave totals)
+        int incl = ntiles;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            int v = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += v;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int base = 0;
+        for (int w = 0; w < wv; ++w) base += wsum[w];
+        if (i < n) a.off[i] = base + incl - ntiles;
+        if (threadIdx.x == 0) a.chunk[ch] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+}
+
+
+void tf_ed_args(tf_ctx* c, EdArgs* out);    // tf_render.hip: the context's expected-depth buffers

@@ -299,6 +299,7 @@ struct tf_ctx {
     int n_resets;            // host mirror of st->n_resets
     int* frame_ok;           // per enqueued frame of a batch: 1 ok, 0 ICP failure (reset), -1 error
     int* frame_mode;         // per enqueued frame of a batch: st->mode it ran with
+    int fuse_ed;             // CreateExpectedDepths' projection pass inside k_integrate's grid (TFUSION_FUSE_ED, 1)
     int lookahead;           // batches: later frames' preprocessing in this frame's grid tails (0 off, 1 next frame, 2 two frames)
     int alloc_chunks;        // N_tot / 4096
     int vis_chunks;
@@ -333,14 +334,17 @@ struct TfAhead {
 };
 hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0,       // snapshot: + the frame's renderImage snapshot
                      TfAhead bil = TfAhead{}, size_t pitch = 0);   // bil: + that frame's bilateral pass
-hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0);   // frame_path: + frame-0 map copy
+// frame_path: + frame-0 map copy; with_ed: CreateExpectedDepths' projection pass in the
+// grid's first TF_ED_BLOCKS workgroups (then tfk_expected_depths(c, 1) runs only the fill)
+hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0, int with_ed = 0);
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_type(tf_ctx* c, int type);   // RenderImage pixel stage (tf_render_type) on raycast
 hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);
 // CreateICPMaps raycast + renderImage, one launch (frame path); next: + that frame's dists/pyramid/normals
 hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = TfAhead{}, size_t pitch = 0);   // + dists/pyramid/normals of pyr, bilateral of bil
 hipError_t tfk_icp_maps(tf_ctx* c);
-hipError_t tfk_expected_depths(tf_ctx* c);
+hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0);
+#define TF_ED_BLOCKS 256         // workgroups of the expected-depth projection pass
 hipError_t tfk_frame0_matrices(tf_ctx* c);
 
 enum { TF_POSE_ALLOC = 1, TF_POSE_RAY = 2, TF_POSE_ALLOC_NOINV = 4 };

@@ -874,106 +874,12 @@ hipError_t tfk_icp_maps(tf_ctx* c)
 // ---------------------------------------------------------------------------------------
 // CreateExpectedDepths
 // ---------------------------------------------------------------------------------------
-struct EdArgs {
-    const TfHashEntry* hash;
-    const int* visibleIds;
-    float2* range;
-    int4* box; float2* z; int* tiles; int* off; int* chunk;
-    int W, H;
-    float fx, fy, cx, cy, voxelSize;
-    unsigned cap;
-};
+#include "tf_ed.h"
 
-#define ED_CHUNK 256     // visible entries per projection chunk (one workgroup pass)
-
-// memsetKernel(FAR_AWAY, VERY_CLOSE) + ProjectSingleBlock (VisualisationEngine_Shared.hpp:33-77).
-// Visible entries are processed in chunks of 256 (thread t of a chunk pass = entry
-// chunk*256 + t).  Each chunk stores its tile total and every entry its exclusive tile offset
-// inside the chunk, so the MAX_RENDERING_BLOCKS cap (VisualisationHelper.cu:70-74) is applied
-// by k_ed_fill from plain prefix sums: no counter atomics, no last-workgroup ticket, no fence.
 __global__ void __launch_bounds__(256)
 k_ed_project(EdArgs a, const TfDevState* __restrict__ st)
 {
-    if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
-    const int tid = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
-    if (st->range_full) {   // range image init, two pixels per 16-byte store
-        const int npx = a.W * a.H;
-        float4* r4 = (float4*)a.range;
-        for (int i = tid; i < (npx >> 1); i += stride) r4[i] = make_float4(TF_FAR_AWAY, TF_VERY_CLOSE, TF_FAR_AWAY, TF_VERY_CLOSE);
-        if ((npx & 1) && tid == 0) a.range[npx - 1] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
-    } else {
-        // Only the /8 region (row stride W, the reference's indexing) is ever filled or read; the
-        // rest of the buffer keeps the constants its last full initialisation wrote
-        const int rc = (a.W - 1) / TF_SUBSAMPLE + 1, rr = (a.H - 1) / TF_SUBSAMPLE + 1;
-        for (int i = tid; i < rc * rr; i += stride) {
-            const int y = i / rc, x = i - y * rc;
-            a.range[x + y * a.W] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
-        }
-    }
-    __shared__ int wsum[4];
-    const int n = st->noVisibleEntries;
-    const int nchunks = (n + ED_CHUNK - 1) / ED_CHUNK;
-    const float* M = st->M_alloc;          // pose.inv() (topfu.cpp:306)
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-        const int i = ch * ED_CHUNK + threadIdx.x;
-        int ntiles = 0;
-        if (i < n) {
-            TfHashEntry e = a.hash[a.visibleIds[i]];
-            int4 box = make_int4(-1, -1, -1, -1);
-            float2 zr = make_float2(0.f, 0.f);
-            if (e.ptr >= 0) {
-                int ulx = a.W / TF_SUBSAMPLE, uly = a.H / TF_SUBSAMPLE, lrx = -1, lry = -1;
-                float zmin = TF_FAR_AWAY, zmax = TF_VERY_CLOSE;
-                for (int corner = 0; corner < 8; ++corner) {
-                    short tx = (short)(e.x + ((corner & 1) ? 1 : 0));
-                    short ty = (short)(e.y + ((corner & 2) ? 1 : 0));
-                    short tz = (short)(e.z + ((corner & 4) ? 1 : 0));
-                    float q[3];
-                    tf_m4v3(M, (float)tx * (float)TF_BLK * a.voxelSize, (float)ty * (float)TF_BLK * a.voxelSize,
-                            (float)tz * (float)TF_BLK * a.voxelSize, 1.0f, q);
-                    if ((double)q[2] < 1e-6) continue;
-                    float p2x = (a.fx * q[0] / q[2] + a.cx) / (float)TF_SUBSAMPLE;
-                    float p2y = (a.fy * q[1] / q[2] + a.cy) / (float)TF_SUBSAMPLE;
-                    if ((float)ulx > floorf(p2x)) ulx = (int)floorf(p2x);
-                    if ((float)lrx < ceilf(p2x)) lrx = (int)ceilf(p2x);
-                    if ((float)uly > floorf(p2y)) uly = (int)floorf(p2y);
-                    if ((float)lry < ceilf(p2y)) lry = (int)ceilf(p2y);
-                    if (zmin > q[2]) zmin = q[2];
-                    if (zmax < q[2]) zmax = q[2];
-                }
-                if (ulx < 0) ulx = 0;
-                if (uly < 0) uly = 0;
-                if (lrx >= a.W) lrx = a.W - 1;
-                if (lry >= a.H) lry = a.H - 1;
-                bool valid = !(ulx > lrx || uly > lry);
-                if (valid && zmin < TF_VERY_CLOSE) zmin = TF_VERY_CLOSE;
-                if (valid && zmax < TF_VERY_CLOSE) valid = false;
-                if (valid) {
-                    int nbx = (int)ceilf((float)(lrx - ulx + 1) / TF_RB_SIZE);
-                    int nby = (int)ceilf((float)(lry - uly + 1) / TF_RB_SIZE);
-                    ntiles = nbx * nby;
-                    box = make_int4(ulx, uly, lrx, lry);
-                    zr = make_float2(zmin, zmax);
-                }
-            }
-            a.box[i] = box; a.z[i] = zr; a.tiles[i] = ntiles;
-        }
-        // exclusive prefix of the tile counts inside the chunk (wave scan + 4 wave totals)
-        int incl = ntiles;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            int v = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += v;
-        }
-        if (lane == 63) wsum[wv] = incl;
-        __syncthreads();
-        int base = 0;
-        for (int w = 0; w < wv; ++w) base += wsum[w];
-        if (i < n) a.off[i] = base + incl - ntiles;
-        if (threadIdx.x == 0) a.chunk[ch] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        __syncthreads();
-    }
+    ed_project_block(a, st, blockIdx.x, gridDim.x);
 }
 
 // fillBlocks_device (VisualisationHelper.cu:105-121): per-pixel min/max of the block z-range.
@@ -1026,15 +932,22 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
     }
 }
 
-hipError_t tfk_expected_depths(tf_ctx* c)
+void tf_ed_args(tf_ctx* c, EdArgs* out)
 {
-    EdArgs a;
+    EdArgs& a = *out;
     a.hash = c->hash; a.visibleIds = c->visibleIds; a.range = (float2*)c->range;
     a.box = c->blockBox; a.z = c->blockZ; a.tiles = c->blockTiles; a.off = c->blockOff; a.chunk = c->edChunk;
     a.W = c->W; a.H = c->H;
     a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy; a.voxelSize = c->p.voxelSize;
     a.cap = (unsigned)c->p.max_render_blocks;
-    hipLaunchKernelGGL(k_ed_project, dim3(256), dim3(256), 0, c->stream, a, c->st);
+}
+
+// project_done: k_ed_project's pass already ran in the frame's k_integrate grid (tf_ctx::fuse_ed)
+hipError_t tfk_expected_depths(tf_ctx* c, int project_done)
+{
+    EdArgs a;
+    tf_ed_args(c, &a);
+    if (!project_done) hipLaunchKernelGGL(k_ed_project, dim3(TF_ED_BLOCKS), dim3(256), 0, c->stream, a, c->st);
     hipLaunchKernelGGL(k_ed_fill, dim3(512), dim3(256), 0, c->stream, a, c->st);
     return hipGetLastError();
 }

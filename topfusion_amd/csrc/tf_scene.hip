@@ -12,6 +12,7 @@
 //   * visible list: ordered compaction by hash index.
 #include "tf_internal.h"
 #include "tf_preproc.h"
+#include "tf_ed.h"
 
 #define TF_INTEG_STREAM_BLOCKS 16384   // 32 MiB of voxels
 #define CHUNK 4096          // hash entries per workgroup in the scan passes (256 thr x 16)
@@ -791,15 +792,20 @@ __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry&
 
 __global__ void __launch_bounds__(256)
 k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
-            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba)
+            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed, int ed_blocks)
 {
+    // the first ed_blocks workgroups run CreateExpectedDepths' projection pass (it reads only
+    // the visible list and the pose; integration writes only voxels): one launch and its
+    // dispatch gap fewer per frame
+    if ((int)blockIdx.x < ed_blocks) { ed_project_block(ed, st, blockIdx.x, ed_blocks); return; }
+    const int bid = blockIdx.x - ed_blocks, nblk = gridDim.x - ed_blocks;
     __shared__ float rw[256];                    // RN(1/w), w = 1..256: the running average's divisors
     rw[threadIdx.x] = 1.0f / (float)(threadIdx.x + 1);
     __syncthreads();
     if (st->abort) return;
     if (a.n_maps > 0 && st->mode == 0) {
-        const int stride = gridDim.x * 256;
-        for (int k = blockIdx.x * 256 + threadIdx.x; k < a.n_maps; k += stride) {
+        const int stride = nblk * 256;
+        for (int k = bid * 256 + threadIdx.x; k < a.n_maps; k += stride) {
             a.prev_pts[k] = a.curr_pts[k];
             a.prev_nrm[k] = a.curr_nrm[k];
         }
@@ -818,8 +824,8 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
     // two blocks per half-workgroup per pass, their id / entry / voxel loads issued before
     // either is computed: twice the bytes in flight per wave (at C3 scale, 2^21 blocks, the
     // pass is a stream over 8.6 GB)
-    const int stride = gridDim.x * 2;
-    for (int i = blockIdx.x * 2 + half; i < n; i += 2 * stride) {
+    const int stride = nblk * 2;
+    for (int i = bid * 2 + half; i < n; i += 2 * stride) {
         const int i2 = i + stride;
         const bool has2 = i2 < n;                    // (loads unconditional: both chains together)
         const int id1 = visibleIds[i], id2 = visibleIds[has2 ? i2 : i];
@@ -837,7 +843,7 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
     }
 }
 
-hipError_t tfk_integrate(tf_ctx* c, int frame_path)
+hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
 {
     IntegArgs a;
     a.curr_pts = c->curr_pts[0]; a.curr_nrm = c->curr_nrm[0]; a.prev_pts = c->prev_pts[0]; a.prev_nrm = c->prev_nrm[0];
@@ -848,6 +854,10 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path)
     a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy;
     a.voxelSize = c->p.voxelSize; a.mu = c->p.mu; a.maxW = c->p.maxW;
     a.inv_mu = 1.0f / c->p.mu; a.mu_exact3 = c->mu_exact3;
-    hipLaunchKernelGGL(k_integrate, dim3(2048), dim3(256), 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba);
+    EdArgs ed = {};
+    if (with_ed) tf_ed_args(c, &ed);
+    const int edb = with_ed ? TF_ED_BLOCKS : 0;
+    hipLaunchKernelGGL(k_integrate, dim3(2048 + edb), dim3(256), 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba,
+                       ed, edb);
     return hipGetLastError();
 }
