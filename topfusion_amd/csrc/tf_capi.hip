@@ -287,6 +287,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         c->lookahead = (la && la[0] >= '0' && la[0] <= '2') ? la[0] - '0' : 2;
         const char* fe = getenv("TFUSION_FUSE_ED");     // 0: k_ed_project as its own launch
         c->fuse_ed = !(fe && fe[0] == '0');
+        const char* fn = getenv("TFUSION_FUSE_END");    // 0: the frame end as its own launch
+        c->fuse_end = !(fn && fn[0] == '0');
     }
     *out = c;
     return TF_OK;
@@ -430,14 +432,17 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
         STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch));        // topfu.cpp:284-285 + 307
     else
         STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));              // CreateICPMaps, topfu.cpp:307
-    STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps(c));                       // + resizePointsNormals :308-309
+    // (+ the frame end in the same grid when fuse_end, render modes 2-3: no render stream reads
+    // the scene behind it)
+    const bool end_fused = c->fuse_end && c->render_mode >= 2;
+    STAGE(TF_STAGE_ICP_MAPS, end_fused ? tfk_icp_maps_end(c, slot) : tfk_icp_maps(c));   // + resizePointsNormals :308-309
     if (c->render_mode == 1) {   // render behind the frame's tail: it overlaps the next frame's ICP
         TF_CHECK(hipEventRecord(c->ev_integrated, c->stream));
         TF_CHECK(hipStreamWaitEvent(c->rstream, c->ev_integrated, 0));
         STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c, c->rstream));
         TF_CHECK(hipEventRecord(c->ev_rendered, c->rstream));
     }
-    TF_CHECK(tfk_reset_scene_on_failure(c, slot));                   // frame end; topfu.cpp:263-264
+    if (!end_fused) TF_CHECK(tfk_reset_scene_on_failure(c, slot));  // frame end; topfu.cpp:263-264
     return TF_OK;
 }
 

@@ -299,6 +299,7 @@ struct tf_ctx {
     int n_resets;            // host mirror of st->n_resets
     int* frame_ok;           // per enqueued frame of a batch: 1 ok, 0 ICP failure (reset), -1 error
     int* frame_mode;         // per enqueued frame of a batch: st->mode it ran with
+    int fuse_end;            // frame end in k_icp_maps' grid, render modes 2-3 (TFUSION_FUSE_END, 1)
     int fuse_ed;             // CreateExpectedDepths' projection pass inside k_integrate's grid (TFUSION_FUSE_ED, 1)
     int lookahead;           // batches: later frames' preprocessing in this frame's grid tails (0 off, 1 next frame, 2 two frames)
     int alloc_chunks;        // N_tot / 4096
@@ -343,6 +344,9 @@ hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);
 // CreateICPMaps raycast + renderImage, one launch (frame path); next: + that frame's dists/pyramid/normals
 hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = TfAhead{}, size_t pitch = 0);   // + dists/pyramid/normals of pyr, bilateral of bil
 hipError_t tfk_icp_maps(tf_ctx* c);
+// CreateICPMaps + the frame end (tfk_reset_scene_on_failure) in one grid (tf_ctx::fuse_end)
+hipError_t tfk_icp_maps_end(tf_ctx* c, int slot);
+#define TF_END_BLOCKS 256        // workgroups of the frame-end / in-frame reset pass
 hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0);
 #define TF_ED_BLOCKS 256         // workgroups of the expected-depth projection pass
 hipError_t tfk_frame0_matrices(tf_ctx* c);

@@ -11,6 +11,7 @@
 //                   float bit patterns (the reference's float CAS loops, CUDAUtils.hpp:75-95)
 #include "tf_internal.h"
 #include "tf_preproc.h"
+#include "tf_reset.h"
 
 struct SceneView {
     const TfHashEntry* hash;
@@ -799,13 +800,12 @@ __device__ __forceinline__ void resize4(const float4* v, const float4* n, float4
 // from the level-1 values staged in LDS.  Every level-0 pixel is evaluated once (levels 1/2
 // are computed from the level-0 results, exactly as the reference's resize of the level-0
 // maps).
-__global__ void __launch_bounds__(256)
-k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
+__device__ __forceinline__ void icp_maps_block(const IcpMapArgs& a, const TfDevState* __restrict__ st, int bx, int by)
 {
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     __shared__ float4 v1s[16][17], n1s[16][17];
     const int lx1 = threadIdx.x & 15, ly1 = threadIdx.x >> 4;
-    const int x1 = blockIdx.x * 16 + lx1, y1 = blockIdx.y * 16 + ly1;
+    const int x1 = bx * 16 + lx1, y1 = by * 16 + ly1;
     const int W = a.W, H = a.H, w1 = W >> 1, h1 = H >> 1, w2 = W >> 2, h2 = H >> 2;
     const float lx = -st->M_ray[8], ly = -st->M_ray[9], lz = -st->M_ray[10];
     float4 v[4], n[4];
@@ -846,7 +846,7 @@ k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
     __syncthreads();
     if (threadIdx.x < 64) {
         const int lx2 = threadIdx.x & 7, ly2 = threadIdx.x >> 3;
-        const int x2 = blockIdx.x * 8 + lx2, y2 = blockIdx.y * 8 + ly2;
+        const int x2 = bx * 8 + lx2, y2 = by * 8 + ly2;
         if (x2 < w2 && y2 < h2) {
             float4 vv[4], nn[4], po, no;
 #pragma unroll
@@ -861,6 +861,24 @@ k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
     }
 }
 
+__global__ void __launch_bounds__(256)
+k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
+{
+    icp_maps_block(a, st, blockIdx.x, blockIdx.y);
+}
+
+// CreateICPMaps' tiles, then TF_END_BLOCKS workgroups of the frame end (bookkeeping; the
+// ResetScene of topfu.cpp:263-264 when ICP failed).  The two share nothing: the maps pass
+// reads the raycast and writes the previous-frame maps, and does nothing on a failed frame;
+// the frame end writes the pose / counters only, and the scene only on a failed frame.
+__global__ void __launch_bounds__(256)
+k_icp_maps_end(IcpMapArgs a, ResetArgs r, int gx, int nmaps)
+{
+    const int b = blockIdx.x;
+    if (b < nmaps) icp_maps_block(a, r.st, b % gx, b / gx);
+    else reset_scene_block(r, b - nmaps, TF_END_BLOCKS);
+}
+
 hipError_t tfk_icp_maps(tf_ctx* c)
 {
     IcpMapArgs a;
@@ -868,6 +886,19 @@ hipError_t tfk_icp_maps(tf_ctx* c)
     for (int l = 0; l < TF_LEVELS; ++l) { a.pts[l] = c->prev_pts[l]; a.nrm[l] = c->prev_nrm[l]; }
     a.W = c->W; a.H = c->H; a.voxelSize = c->p.voxelSize;
     hipLaunchKernelGGL(k_icp_maps, dim3((c->W + 31) / 32, (c->H + 31) / 32), dim3(256), 0, c->stream, a, c->st);
+    return hipGetLastError();
+}
+
+hipError_t tfk_icp_maps_end(tf_ctx* c, int slot)
+{
+    IcpMapArgs a;
+    a.ray = (const float4*)c->raycast;
+    for (int l = 0; l < TF_LEVELS; ++l) { a.pts[l] = c->prev_pts[l]; a.nrm[l] = c->prev_nrm[l]; }
+    a.W = c->W; a.H = c->H; a.voxelSize = c->p.voxelSize;
+    ResetArgs r;
+    tf_reset_args(c, &r, 1, slot);
+    const int gx = (c->W + 31) / 32, nmaps = gx * ((c->H + 31) / 32);
+    hipLaunchKernelGGL(k_icp_maps_end, dim3(nmaps + TF_END_BLOCKS), dim3(256), 0, c->stream, a, r, gx, nmaps);
     return hipGetLastError();
 }
 

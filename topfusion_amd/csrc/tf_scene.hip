@@ -13,6 +13,7 @@
 #include "tf_internal.h"
 #include "tf_preproc.h"
 #include "tf_ed.h"
+#include "tf_reset.h"
 
 #define TF_INTEG_STREAM_BLOCKS 16384   // 32 MiB of voxels
 #define CHUNK 4096          // hash entries per workgroup in the scan passes (256 thr x 16)
@@ -32,93 +33,29 @@ __device__ __forceinline__ void load16(const unsigned char* p, unsigned long lon
 // ---------------------------------------------------------------------------------------
 // ResetScene (SceneReconstructionEngine_host.cu:51-73)
 // ---------------------------------------------------------------------------------------
-__global__ void k_reset_scene(TfVoxel* vba, size_t n_vox, int* allocList, int n_blocks, TfHashEntry* hash,
-                              int n_total, int* excessList, int n_excess, TfDevState* st, int2* grid, int on_failure,
-                              int* frame_ok, int* frame_mode, int slot, int full)
+__global__ void __launch_bounds__(256) k_reset_scene(ResetArgs r)
 {
-    if (on_failure && blockIdx.x == 0 && threadIdx.x == 0) {
-        // end of the device-driven frame (return values of topfu.cpp:209 / 264 / 329); only
-        // frame_counter / n_resets / pose change here, never the mode / icp_ok read below
-        const int mode = st->mode, icp_ok = st->icp_ok;
-        int ok;
-        if (mode == 0) { st->frame_counter = 1; ok = 1; }
-        else if (icp_ok < 0) ok = -1;                       // persistent ICP lost a peer
-        else if (icp_ok == 0) {                             // return reset(), false
-            st->n_resets++;
-            st->frame_counter = 0;
-            for (int i = 0; i < 12; ++i) st->pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
-            ok = 0;
-        } else { st->frame_counter++; ok = 1; }
-        frame_ok[slot] = ok;
-        frame_mode[slot] = mode;
-    }
-    if (on_failure && !(st->mode == 1 && st->icp_ok == 0)) return;   // topfu.cpp:263-264 only
-    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    uint4 vfill = make_uint4(32767u, 32767u, 32767u, 32767u);   // Voxel_s(): sdf 32767, w 0
-    uint4* v4 = (uint4*)vba;
-    TfHashEntry e; e.x = e.y = e.z = e.pad = 0; e.offset = 0; e.ptr = -2;
-    if (full) {
-        for (size_t i = tid; i < n_vox / 4; i += stride) v4[i] = vfill;
-        for (size_t i = tid; i < (size_t)n_blocks; i += stride) allocList[i] = (int)i;
-        for (size_t i = tid; i < (size_t)n_excess; i += stride) excessList[i] = (int)i;
-    } else {
-        // Same end state from what the frames wrote since the last full reset: allocation only
-        // pops the free lists (never writes them) and integration only writes blocks it was
-        // handed, so the blocks in use -- allocList[lastFreeBlockId+1 .. n_blocks-1] -- are the
-        // only ones not at Voxel_s(), and the free lists are still the identity.
-        const int first = st->lastFreeBlockId + 1 < 0 ? 0 : st->lastFreeBlockId + 1;
-        const size_t n_used4 = (size_t)(n_blocks - first) * (TF_BLK3 / 4);
-        for (size_t i0 = tid; i0 < n_used4; i0 += 8 * stride) {   // 8 list loads in flight per lane
-            int blk[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const size_t i = i0 + k * stride;
-                blk[k] = allocList[first + (int)((i < n_used4 ? i : i0) / (TF_BLK3 / 4))];
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const size_t i = i0 + k * stride;
-                if (i < n_used4) v4[(size_t)blk[k] * (TF_BLK3 / 4) + i % (TF_BLK3 / 4)] = vfill;
-            }
-        }
-    }
-    for (size_t i0 = tid; i0 < (size_t)n_total; i0 += 8 * stride) {   // 8 entry loads in flight per lane
-        TfHashEntry o[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const size_t i = i0 + k * stride;
-            o[k] = hash[i < (size_t)n_total ? i : i0];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const size_t i = i0 + k * stride;
-            // live entries (only they differ from e)
-            if (i < (size_t)n_total && (full || o[k].ptr >= 0)) {
-                if (o[k].ptr >= 0 && tf_grid_in(o[k].x, o[k].y, o[k].z))
-                    grid[tf_grid_cell(o[k].x, o[k].y, o[k].z)] = make_int2(-1, TF_VOFF_NONE);
-                hash[i] = e;
-            }
-        }
-    }
-    // the counters are reset by the last workgroup to finish (every workgroup has read
-    // lastFreeBlockId by then)
-    __shared__ int last_s;
-    __syncthreads();
-    if (threadIdx.x == 0) last_s = atomicAdd(&st->reset_ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (last_s && threadIdx.x == 0) {
-        st->reset_ticket = 0;
-        st->lastFreeBlockId = n_blocks - 1;
-        st->lastFreeExcessListId = n_excess - 1;
-    }
+    reset_scene_block(r, blockIdx.x, gridDim.x);
+}
+
+void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot)
+{
+    r->vba = c->vba; r->n_vox = (size_t)c->p.n_blocks * TF_BLK3;
+    r->allocList = c->allocList; r->n_blocks = c->p.n_blocks;
+    r->hash = c->hash; r->n_total = c->n_total;
+    r->excessList = c->excessList; r->n_excess = c->p.n_excess;
+    r->st = c->st; r->grid = c->bgrid;
+    r->on_failure = on_failure;
+    r->frame_ok = on_failure ? c->frame_ok : nullptr; r->frame_mode = on_failure ? c->frame_mode : nullptr;
+    r->slot = on_failure ? slot : 0;
+    r->full = on_failure ? c->scene_external : 1;
 }
 
 hipError_t tfk_reset_scene(tf_ctx* c)
 {
-    hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, c->vba, (size_t)c->p.n_blocks * TF_BLK3,
-                       c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st, c->bgrid, 0,
-                       nullptr, nullptr, 0, 1);
+    ResetArgs r;
+    tf_reset_args(c, &r, 0, 0);
+    hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, r);
     const hipError_t e = hipGetLastError();
     if (e == hipSuccess) c->scene_external = 0;
     return e;
@@ -129,9 +66,9 @@ hipError_t tfk_reset_scene(tf_ctx* c)
 // full clear when scene buffers were uploaded since the last full reset)
 hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot)
 {
-    hipLaunchKernelGGL(k_reset_scene, dim3(256), dim3(256), 0, c->stream, c->vba, (size_t)c->p.n_blocks * TF_BLK3,
-                       c->allocList, c->p.n_blocks, c->hash, c->n_total, c->excessList, c->p.n_excess, c->st, c->bgrid, 1,
-                       c->frame_ok, c->frame_mode, slot, c->scene_external);
+    ResetArgs r;
+    tf_reset_args(c, &r, 1, slot);
+    hipLaunchKernelGGL(k_reset_scene, dim3(TF_END_BLOCKS), dim3(256), 0, c->stream, r);
     return hipGetLastError();
 }
 
