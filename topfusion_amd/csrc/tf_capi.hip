@@ -91,7 +91,7 @@ static void ctx_free(tf_ctx* c)
 {
     if (!c) return;
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
-                     c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
+                     c->requestList, c->visCounts, c->visFlags, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockBox, c->blockZ, c->blockTiles, c->blockOff, c->edChunk, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->frame_ok, c->frame_mode };
     for (void* b : bufs) if (b) (void)hipFree(b);
@@ -196,6 +196,9 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->allocCounts, sizeof(int) * 2 * (size_t)c->alloc_chunks);
     ALLOC(c->requestList, sizeof(int) * (size_t)c->n_total);
     ALLOC(c->visCounts, sizeof(int) * (size_t)c->vis_chunks);
+    ALLOC(c->visFlags, sizeof(unsigned long long) * (size_t)c->vis_chunks);
+    e = hipMemset(c->visFlags, 0, sizeof(unsigned long long) * (size_t)c->vis_chunks);   // epoch 0: never a launch's
+    if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     ALLOC(c->visibleIds, sizeof(int) * (size_t)pin->vis_capacity);
     ALLOC(c->visType, ntot_pad);
     ALLOC(c->range, sizeof(float) * 2 * npx);
@@ -289,6 +292,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         c->fuse_ed = !(fe && fe[0] == '0');
         const char* fn = getenv("TFUSION_FUSE_END");    // 0: the frame end as its own launch
         c->fuse_end = !(fn && fn[0] == '0');
+        const char* vs = getenv("TFUSION_VIS_SCAN");    // 1: one look-back scan launch (A/B: no faster)
+        c->vis_scan = vs && vs[0] == '1';
     }
     *out = c;
     return TF_OK;

@@ -262,6 +262,7 @@ struct tf_ctx {
     int* allocCounts;        // per-chunk counts (2 ints per chunk)
     int* requestList;        // ordered request indices
     int* visCounts;
+    unsigned long long* visFlags;   // k_vis_scan look-back words (epoch | flag | prefix), one per chunk
     // RenderState_VH
     int* visibleIds;
     unsigned char* visType;
@@ -299,6 +300,8 @@ struct tf_ctx {
     int n_resets;            // host mirror of st->n_resets
     int* frame_ok;           // per enqueued frame of a batch: 1 ok, 0 ICP failure (reset), -1 error
     int* frame_mode;         // per enqueued frame of a batch: st->mode it ran with
+    int vis_scan;            // visible-list compaction as one look-back scan launch (TFUSION_VIS_SCAN, 0)
+    unsigned vis_epoch;      // k_vis_scan launches enqueued (the look-back words' tag)
     int fuse_end;            // frame end in k_icp_maps' grid, render modes 2-3 (TFUSION_FUSE_END, 1)
     int fuse_ed;             // CreateExpectedDepths' projection pass inside k_integrate's grid (TFUSION_FUSE_ED, 1)
     int lookahead;           // batches: later frames' preprocessing in this frame's grid tails (0 off, 1 next frame, 2 two frames)
