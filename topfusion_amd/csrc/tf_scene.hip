@@ -832,15 +832,20 @@ __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry&
     }
 }
 
+template <bool WITH_ED>
 __global__ void __launch_bounds__(256)
 k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
-            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed, int ed_blocks)
+            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed)
 {
-    // the first ed_blocks workgroups run CreateExpectedDepths' projection pass (it reads only
-    // the visible list and the pose; integration writes only voxels): one launch and its
-    // dispatch gap fewer per frame
-    if ((int)blockIdx.x < ed_blocks) { ed_project_block(ed, st, blockIdx.x, ed_blocks); return; }
-    const int bid = blockIdx.x - ed_blocks, nblk = gridDim.x - ed_blocks;
+    // WITH_ED: the first TF_ED_BLOCKS workgroups run CreateExpectedDepths' projection pass (it
+    // reads only the visible list and the pose; integration writes only voxels): one launch
+    // and its dispatch gap fewer per frame.  The stand-alone instance (stage entry points, C3I)
+    // has no such branch: its grid-stride loop is the plain one.
+    int bid = blockIdx.x, nblk = gridDim.x;
+    if (WITH_ED) {
+        if (bid < TF_ED_BLOCKS) { ed_project_block(ed, st, bid, TF_ED_BLOCKS); return; }
+        bid -= TF_ED_BLOCKS; nblk -= TF_ED_BLOCKS;
+    }
     __shared__ float rw[256];                    // RN(1/w), w = 1..256: the running average's divisors
     rw[threadIdx.x] = 1.0f / (float)(threadIdx.x + 1);
     __syncthreads();
@@ -897,9 +902,13 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
     a.voxelSize = c->p.voxelSize; a.mu = c->p.mu; a.maxW = c->p.maxW;
     a.inv_mu = 1.0f / c->p.mu; a.mu_exact3 = c->mu_exact3;
     EdArgs ed = {};
-    if (with_ed) tf_ed_args(c, &ed);
-    const int edb = with_ed ? TF_ED_BLOCKS : 0;
-    hipLaunchKernelGGL(k_integrate, dim3(2048 + edb), dim3(256), 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba,
-                       ed, edb);
+    if (with_ed) {
+        tf_ed_args(c, &ed);
+        hipLaunchKernelGGL(k_integrate<true>, dim3(2048 + TF_ED_BLOCKS), dim3(256), 0, c->stream, a, c->st, c->hash,
+                           c->visibleIds, c->vba, ed);
+    } else {
+        hipLaunchKernelGGL(k_integrate<false>, dim3(2048), dim3(256), 0, c->stream, a, c->st, c->hash, c->visibleIds,
+                           c->vba, ed);
+    }
     return hipGetLastError();
 }
