@@ -251,7 +251,7 @@ def test_capacity_exhaustion(oracle_mod):
     compare_scene(g, o, "exhausted")
 
 
-@pytest.mark.parametrize("render_mode", ["0", "1", "2", "3", "3-lookahead1", "3-no-lookahead", "3-unfused-ed", "3-unfused-end", "3-vis-scan"])
+@pytest.mark.parametrize("render_mode", ["0", "1", "2", "3", "3-lookahead1", "3-no-lookahead", "3-unfused-ed", "3-unfused-end", "3-vis-scan", "3-unfolded-t3"])
 def test_batched_frames_overlap(oracle_mod, monkeypatch, render_mode):
     """The device-driven batch path (tf_process_frames): frames enqueued back to back with no
     host sync, renderImage on the render stream overlapping the frame's tail and the next
@@ -263,7 +263,8 @@ def test_batched_frames_overlap(oracle_mod, monkeypatch, render_mode):
     default) or as its own launch (0), and the frame end (ResetScene on ICP failure) inside
     k_icp_maps' grid (TFUSION_FUSE_END=1, the default for modes 2-3) or as its own launch, and
     the visible-list compaction as count + apply launches (the default) or as one look-back
-    scan (TFUSION_VIS_SCAN=1).  Per-frame results, the last frame's grey image, the final pose and the whole
+    scan (TFUSION_VIS_SCAN=1), and setToType3 + the renderImage snapshot in the persistent
+    ICP grid's tail (TFUSION_FOLD_T3=1, the default for modes 2-3) or as their own launch.  Per-frame results, the last frame's grey image, the final pose and the whole
     scene match the oracle run frame by frame."""
     from parity_util import DeviceFrames
     from topfusion_amd import TopFu, default_params
@@ -272,6 +273,7 @@ def test_batched_frames_overlap(oracle_mod, monkeypatch, render_mode):
     monkeypatch.setenv("TFUSION_FUSE_ED", "0" if render_mode == "3-unfused-ed" else "1")
     monkeypatch.setenv("TFUSION_FUSE_END", "0" if render_mode == "3-unfused-end" else "1")
     monkeypatch.setenv("TFUSION_VIS_SCAN", "1" if render_mode == "3-vis-scan" else "0")
+    monkeypatch.setenv("TFUSION_FOLD_T3", "0" if render_mode == "3-unfolded-t3" else "1")
     cols, rows, n = 320, 240, 40          # 40 frames > one 32-frame enqueue group
     fx, fy, cx, cy = synth.intrinsics(cols, rows)
     args = dict(cols=cols, rows=rows, fx=fx, fy=fy, cx=cx, cy=cy)

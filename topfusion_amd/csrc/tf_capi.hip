@@ -294,6 +294,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         c->fuse_end = !(fn && fn[0] == '0');
         const char* vs = getenv("TFUSION_VIS_SCAN");    // 1: one look-back scan launch (A/B: no faster)
         c->vis_scan = vs && vs[0] == '1';
+        const char* ft = getenv("TFUSION_FOLD_T3");     // 0: k_set_type3 as its own launch
+        c->fold_t3 = !(ft && ft[0] == '0');
     }
     *out = c;
     return TF_OK;
@@ -413,12 +415,15 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     // preprocessing (topfu.cpp:166-197)
     if (!plan->pre_done) STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, c->stream, d0));
     c->depth_pyr[0] = d0;
-    STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1));                           // frame begin + topfu.cpp:242-243 (tracking only)
+    // (+ setToType3 / the renderImage snapshot in the ICP grid's tail: persistent SCHED-3 ICP,
+    // render inline -- no render stream reads the snapshot)
+    const bool t3_fold = c->fold_t3 && c->icp_persistent && c->icp_sched == 3 && c->render_mode >= 2;
+    STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1, t3_fold));                  // frame begin + topfu.cpp:242-243 (tracking only)
     // the previous frame's renderImage (render stream) must be done before the scene changes
     // (modes 2 and 3 render on the main stream: no wait -- an event wait is a barrier packet,
     // a few microseconds of dispatch gap even when the event has long completed)
     if (c->render_mode <= 1) TF_CHECK(join_render(c));
-    STAGE(TF_STAGE_ALLOC, tfk_alloc(c, 1, plan->alloc_bil, pitch));                        // topfu.cpp:202 / 281 (+ renderImage snapshot)
+    STAGE(TF_STAGE_ALLOC, tfk_alloc(c, t3_fold ? 2 : 1, plan->alloc_bil, pitch));                        // topfu.cpp:202 / 281 (+ renderImage snapshot)
     // (+ CreateExpectedDepths' projection pass in the same grid when fuse_ed)
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1, c->fuse_ed));     // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
     // renderImage (raycast + grey, topfu.cpp:284-285) on the render stream, behind integration;

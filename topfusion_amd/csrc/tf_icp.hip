@@ -154,6 +154,7 @@ __device__ __forceinline__ void icp_rodrigues(const float* rv, float* R)
 }
 
 #include "tf_pose.h"
+#include "tf_vis.h"
 
 // ---- 6x6 algebra, register resident: every lane runs the same fully unrolled code on
 // uniform data (static indices only; pivot rows selected by uniform branches) ------------------
@@ -453,7 +454,51 @@ struct IcpFrameArgs {
     int frame_begin;                    // frame path: the launch starts the frame (tf_frame_begin)
     TfDevState* st;
     unsigned long long* tag;            // [256][28] column sums, then [16] broadcast
+    // fold_t3: the frame's setToType3 + visibility test and renderImage snapshot (k_set_type3)
+    // run in this grid's tail, once the pose is known (frame path, SCHED 3, inline render)
+    int fold_t3;
+    VisArgs vis;
+    const TfHashEntry* hash;
+    const int* visibleIds;
+    unsigned char* visType;
+    const float2* range;
+    float2* snap;
 };
+
+// k_set_type3's work (render_snapshot + set_type3_pass) in every workgroup of the persistent
+// ICP grid after its last iteration: pose0 = poses_.back() read at launch (only workgroup 0
+// writes st->pose, after every hand-off); mode 0 = frame-0 path (pose as is), else status 1 =
+// ICP succeeded (pose0 * affine).  The matrices are those tf_set_pose_matrices derives,
+// computed by the same operations.
+__device__ void icp_fold_t3(const IcpFrameArgs& a, const float* pose0, const float* aff, int mode, int status)
+{
+    __shared__ float M_s[16], Mr_s[16];
+    TfDevState* st = a.st;
+    const bool go = mode == 0 || status == 1;              // !abort
+    if (threadIdx.x == 0) {
+        float pose[12], m[12];
+        for (int i = 0; i < 12; ++i) pose[i] = pose0[i];
+        if (mode != 0 && status == 1) tf_rigid_mul(pose, aff, pose);
+        if (mode != 0) tf_rigid_inv(pose, m);
+        else for (int i = 0; i < 12; ++i) m[i] = pose[i];
+        tf_rt_to_m4(m, M_s);
+        tf_rt_to_m4(pose, Mr_s);
+    }
+    __syncthreads();
+    // render_snapshot (tf_internal.h): M_render = M_ray (unchanged by a failed ICP), render_go
+    if (blockIdx.x == 0 && threadIdx.x < 16) st->M_render[threadIdx.x] = go ? Mr_s[threadIdx.x] : st->M_ray[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->render_go = (mode != 0 && go) ? 1 : 0;
+    if (!go) return;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    if (mode != 0) {
+        const int W = a.vis.W, rc = (W - 1) / TF_SUBSAMPLE + 1, rr = (a.vis.H - 1) / TF_SUBSAMPLE + 1;
+        for (int i = tid; i < rc * rr; i += stride) {
+            const int y = i / rc, x = i - y * rc;
+            a.snap[x + y * W] = a.range[x + y * W];
+        }
+    }
+    set_type3_pass(a.vis, st->noVisibleEntries, M_s, a.hash, a.visibleIds, a.visType, tid, stride);
+}
 
 __device__ __forceinline__ unsigned long long ip_pack(unsigned gen, float v)
 {
@@ -609,6 +654,8 @@ k_icp_frame(IcpFrameArgs a)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, wg = blockIdx.x;
     TfDevState* st = a.st;
     unsigned long long* tag = a.tag;
+    __shared__ float pose0_s[12];
+    if (a.fold_t3 && tid < 12) pose0_s[tid] = st->pose[tid];
     if (a.frame_begin) {
         // the device-driven frame starts here (TopFu::operator(), topfu.cpp:200): frame 0 of a
         // run (frame_counter == 0) takes the integrate-only path.  Workgroup 0 records the
@@ -616,7 +663,13 @@ k_icp_frame(IcpFrameArgs a)
         // frame's end wrote (so the preprocessing stream never touches the state)
         const bool frame0 = st->frame_counter == 0;
         if (wg == 0 && tid == 0) tf_frame_begin(st);
-        if (frame0) return;
+        if (frame0) {
+            if (a.fold_t3) {
+                __syncthreads();
+                icp_fold_t3(a, pose0_s, nullptr, 0, 1);
+            }
+            return;
+        }
     } else if (st->mode == 0) {
         return;                                // frame 0 runs no ICP (uniform over the grid)
     }
@@ -986,6 +1039,10 @@ k_icp_frame(IcpFrameArgs a)
             }
         }
     }
+    if (a.fold_t3) {
+        __syncthreads();
+        icp_fold_t3(a, pose0_s, aff, 1, status);
+    }
 }
 
 __global__ void k_icp_begin(TfDevState* st, int frame_begin)
@@ -1065,7 +1122,7 @@ int tfk_icp_persistent_ok(tf_ctx* c)
     return 1;
 }
 
-hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin)
+hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
 {
     const tf_params& p = c->p;
     const int levels = icp_used_levels(p);
@@ -1085,6 +1142,14 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin)
         a.frame_begin = frame_begin;
         a.st = c->st;
         a.tag = c->icp_tagged;
+        if (fold_t3 && c->icp_sched == 3 && pose_update && frame_begin) {
+            a.fold_t3 = 1;
+            a.vis.fx = c->p.fx; a.vis.fy = c->p.fy; a.vis.cx = c->p.cx; a.vis.cy = c->p.cy;
+            a.vis.factor = (float)TF_BLK * c->p.voxelSize;
+            a.vis.W = c->W; a.vis.H = c->H; a.vis.n_total = c->n_total; a.vis.cap = c->p.vis_capacity;
+            a.hash = c->hash; a.visibleIds = c->visibleIds; a.visType = c->visType;
+            a.range = (const float2*)c->range; a.snap = (float2*)c->range_render;
+        }
         // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
         // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up
         if (c->icp_sched == 3)

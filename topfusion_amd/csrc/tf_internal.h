@@ -302,6 +302,7 @@ struct tf_ctx {
     int* frame_mode;         // per enqueued frame of a batch: st->mode it ran with
     int vis_scan;            // visible-list compaction as one look-back scan launch (TFUSION_VIS_SCAN, 0)
     unsigned vis_epoch;      // k_vis_scan launches enqueued (the look-back words' tag)
+    int fold_t3;             // setToType3 + renderImage snapshot in the ICP grid's tail (TFUSION_FOLD_T3, 1)
     int fuse_end;            // frame end in k_icp_maps' grid, render modes 2-3 (TFUSION_FUSE_END, 1)
     int fuse_ed;             // CreateExpectedDepths' projection pass inside k_integrate's grid (TFUSION_FUSE_ED, 1)
     int lookahead;           // batches: later frames' preprocessing in this frame's grid tails (0 off, 1 next frame, 2 two frames)
@@ -323,7 +324,9 @@ struct tf_ctx {
 // launchers (one per kernel family); all enqueue on ctx->stream
 // ---------------------------------------------------------------------------------------
 hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStream_t strm, uint16_t* d0);   // no st access
-hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin = 0);   // frame_begin: frame path (tf_frame_begin)
+// fold_t3: k_set_type3's work in the persistent SCHED-3 ICP grid's tail (frame path; the
+// caller then passes snapshot = 2 to tfk_alloc)
+hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin = 0, int fold_t3 = 0);   // frame_begin: frame path (tf_frame_begin)
 int tfk_icp_persistent_ok(tf_ctx* c);      // k_icp_frame fits (co-residency, slot count)
 hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / raycast matrices
 hipError_t tfk_reset_scene(tf_ctx* c);

@@ -14,6 +14,7 @@
 #include "tf_preproc.h"
 #include "tf_ed.h"
 #include "tf_reset.h"
+#include "tf_vis.h"
 
 #define TF_INTEG_STREAM_BLOCKS 16384   // 32 MiB of voxels
 #define CHUNK 4096          // hash entries per workgroup in the scan passes (256 thr x 16)
@@ -138,41 +139,6 @@ hipError_t tfk_grid_rebuild(tf_ctx* c)
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_grid_build, dim3(1024), dim3(256), 0, c->stream, c->hash, c->n_total, c->bgrid);
     return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------
-// checkBlockVisibility<false> (SceneReconstructionEngine.hpp:300-375)
-// ---------------------------------------------------------------------------------------
-struct VisArgs {
-    float fx, fy, cx, cy;
-    float factor;                 // (float)SDF_BLOCK_SIZE * voxelSize
-    int W, H;
-    int n_total, cap;
-};
-
-__device__ __forceinline__ bool vis_point(const float* M, const float* pt, const VisArgs& v)
-{
-    float b[4];
-    tf_m4v(M, pt[0], pt[1], pt[2], pt[3], b);
-    if (b[2] < 1e-10f) return false;
-    float bx = v.fx * b[0] / b[2] + v.cx;
-    float by = v.fy * b[1] / b[2] + v.cy;
-    return bx >= 0 && bx < (float)v.W && by >= 0 && by < (float)v.H;
-}
-
-__device__ bool vis_block(const TfHashEntry& e, const float* M, const VisArgs& v)
-{
-    const float f = v.factor;
-    float pt[4] = { (float)e.x * f, (float)e.y * f, (float)e.z * f, 1.0f };
-    if (vis_point(M, pt, v)) return true;
-    pt[2] += f; if (vis_point(M, pt, v)) return true;                     // 0 0 1
-    pt[1] += f; if (vis_point(M, pt, v)) return true;                     // 0 1 1
-    pt[0] += f; if (vis_point(M, pt, v)) return true;                     // 1 1 1
-    pt[2] -= f; if (vis_point(M, pt, v)) return true;                     // 1 1 0
-    pt[1] -= f; if (vis_point(M, pt, v)) return true;                     // 1 0 0
-    pt[0] -= f; pt[1] += f; if (vis_point(M, pt, v)) return true;         // 0 1 0
-    pt[0] += f; pt[1] -= f; pt[2] += f; if (vis_point(M, pt, v)) return true;  // 1 0 1
-    return false;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -333,10 +299,7 @@ k_set_type3(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restric
     if (st->abort) return;
     const int n = st->noVisibleEntries;
     const float* M = st->M_alloc;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const int id = visibleIds[i];
-        visType[id] = vis_block(hash[id], M, v) ? 3 : 4;
-    }
+    set_type3_pass(v, n, M, hash, visibleIds, visType, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -699,8 +662,9 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch)
     v.fx = c->p.fx; v.fy = c->p.fy; v.cx = c->p.cx; v.cy = c->p.cy;
     v.factor = (float)TF_BLK * c->p.voxelSize;
     v.W = c->W; v.H = c->H; v.n_total = c->n_total; v.cap = c->p.vis_capacity;
-    hipLaunchKernelGGL(k_set_type3, dim3(256), dim3(256), 0, c->stream, v, c->st, c->hash, c->visibleIds, c->visType,
-                       (const float2*)c->range, snapshot ? (float2*)c->range_render : nullptr);
+    if (snapshot != 2)   // 2: the frame's ICP launch has done it (tfk_icp fold_t3)
+        hipLaunchKernelGGL(k_set_type3, dim3(256), dim3(256), 0, c->stream, v, c->st, c->hash, c->visibleIds, c->visType,
+                           (const float2*)c->range, snapshot ? (float2*)c->range_render : nullptr);
     const int gx = (c->W + 15) / 16, n_alloc = gx * ((c->H + 15) / 16);
     BilArgs nb; PyrArgs np;
     int n_next = 0, next_gx = 1;
