@@ -396,6 +396,10 @@ k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int*
               const int* __restrict__ excessList, int* __restrict__ requestList, int n_total)
 {
     if (st->abort) return;
+    // this chunk's request types, loaded before (and in flight with) the counts prefix
+    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
+    unsigned long long lo = 0, hi = 0;
+    if (base < n_total) load16(allocType + base, &lo, &hi);
     // prefix and totals over the per-chunk counts
     int p12 = 0, p2 = 0, a12 = 0, a2 = 0;
     for (int h = threadIdx.x; h < n_chunks; h += 256) {
@@ -410,13 +414,9 @@ k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int*
         st->alloc_exhausted = exhausted ? 1 : 0;
         st->pad_[0] = a12; st->pad_[1] = a2;
     }
-    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
-    unsigned long long lo = 0, hi = 0;
     int l12 = 0, l2 = 0;
-    if (base < n_total) {
-        load16(allocType + base, &lo, &hi);
+    if (base < n_total)
         for (int i = 0; i < 16; ++i) { unsigned t = byte16(lo, hi, i); l12 += t != 0; l2 += t == 2; }
-    }
     int tmp;
     int r12 = p12 + block_excl_scan(l12, &tmp);
     int r2 = p2 + block_excl_scan(l2, &tmp);
@@ -513,6 +513,10 @@ k_vis_apply(VisArgs v, TfDevState* __restrict__ st, int n_chunks, const int* __r
             const unsigned char* __restrict__ visType, int* __restrict__ visibleIds)
 {
     if (st->abort) return;
+    // this chunk's types, loaded before (and in flight with) the counts prefix
+    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
+    unsigned long long lo = 0, hi = 0;
+    if (base < v.n_total) load16(visType + base, &lo, &hi);
     int pre = 0, all = 0;
     for (int h = threadIdx.x; h < n_chunks; h += 256) {
         int c = counts[h];
@@ -521,13 +525,9 @@ k_vis_apply(VisArgs v, TfDevState* __restrict__ st, int n_chunks, const int* __r
     }
     pre = block_sum(pre); all = block_sum(all);
     if (blockIdx.x == 0 && threadIdx.x == 0) st->noVisibleEntries = all < v.cap ? all : v.cap;
-    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
-    unsigned long long lo = 0, hi = 0;
     int cnt = 0;
-    if (base < v.n_total) {
-        load16(visType + base, &lo, &hi);
+    if (base < v.n_total)
         for (int i = 0; i < 16; ++i) cnt += byte16(lo, hi, i) > 0;
-    }
     int tmp;
     int r = pre + block_excl_scan(cnt, &tmp);
     if (!cnt) return;
