@@ -475,6 +475,12 @@ __device__ void icp_fold_t3(const IcpFrameArgs& a, const float* pose0, const flo
     __shared__ float M_s[16], Mr_s[16];
     TfDevState* st = a.st;
     const bool go = mode == 0 || status == 1;              // !abort
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    // the thread's first previous-list entry, loaded while thread 0 derives the matrices
+    const int n = go ? st->noVisibleEntries : 0;
+    int id0 = -1;
+    TfHashEntry e0 = {};
+    if (tid < n) { id0 = a.visibleIds[tid]; e0 = a.hash[id0]; }
     if (threadIdx.x == 0) {
         float pose[12], m[12];
         for (int i = 0; i < 12; ++i) pose[i] = pose0[i];
@@ -489,7 +495,6 @@ __device__ void icp_fold_t3(const IcpFrameArgs& a, const float* pose0, const flo
     if (blockIdx.x == 0 && threadIdx.x < 16) st->M_render[threadIdx.x] = go ? Mr_s[threadIdx.x] : st->M_ray[threadIdx.x];
     if (blockIdx.x == 0 && threadIdx.x == 0) st->render_go = (mode != 0 && go) ? 1 : 0;
     if (!go) return;
-    const int tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     if (mode != 0) {
         const int W = a.vis.W, rc = (W - 1) / TF_SUBSAMPLE + 1, rr = (a.vis.H - 1) / TF_SUBSAMPLE + 1;
         for (int i = tid; i < rc * rr; i += stride) {
@@ -497,7 +502,8 @@ __device__ void icp_fold_t3(const IcpFrameArgs& a, const float* pose0, const flo
             a.snap[x + y * W] = a.range[x + y * W];
         }
     }
-    set_type3_pass(a.vis, st->noVisibleEntries, M_s, a.hash, a.visibleIds, a.visType, tid, stride);
+    if (id0 >= 0) a.visType[id0] = vis_block(e0, M_s, a.vis) ? 3 : 4;
+    set_type3_pass(a.vis, n, M_s, a.hash, a.visibleIds, a.visType, tid + stride, stride);
 }
 
 __device__ __forceinline__ unsigned long long ip_pack(unsigned gen, float v)
