@@ -27,38 +27,42 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 # stages that are one kernel launch per frame (persistent ICP), and that kernel's name
-KERNEL_OF_STAGE = {"icp": "k_icp_frame", "raycast_render": "k_raycast<2> (raycast + grey)",
+KERNEL_OF_STAGE = {"icp": "k_icp_frame",
                    "raycast_icp": "k_raycast_pair (CreateICPMaps castRay<true> + renderImage castRay + grey)",
                    "integrate": "k_integrate"}
 SINGLE_KERNEL_STAGES = tuple(KERNEL_OF_STAGE)
-# renderImage schedule (tf_capi.hip, TFUSION_RENDER_MODE): 3 (default) = fused with CreateICPMaps' raycast
-RENDER_FUSED = os.environ.get("TFUSION_RENDER_MODE", "3") == "3"
-if not RENDER_FUSED:
-    KERNEL_OF_STAGE["raycast_icp"] = "k_raycast<1>"
 
-# SURVEY.md §8d configs.  C3 raises the capacities past the reference's (2^21 blocks = 4 GiB of
-# voxels, 2^22 buckets, 2^20 excess) -- sized for 288 GB of HBM, not for the reference's GPU.
+# SURVEY.md §8d configs.  C3 raises the capacities past the reference's (2^21 - 1 blocks = 4 GiB
+# of voxels, the most the raycasts' 32-bit offsets address; 2^22 buckets, 2^20 excess) -- sized
+# for 288 GB of HBM, not for the reference's GPU.  steps are in units of --frames-per-step.
+C3_CAPACITY = dict(n_buckets=1 << 22, n_excess=1 << 20, n_blocks=(1 << 21) - 1, vis_capacity=1 << 21,
+                   max_render_blocks=1 << 20)
 CONFIGS = {
-    "C2": dict(cols=640, rows=480, voxel=0.005, capacity={}, walk=False, steps=200),
-    "C3": dict(cols=1280, rows=960, voxel=0.002,
-               capacity=dict(n_buckets=1 << 22, n_excess=1 << 20, n_blocks=1 << 21, vis_capacity=1 << 21,
-                             max_render_blocks=1 << 20), walk=False, steps=200),
+    "C2": dict(cols=640, rows=480, voxel=0.005, capacity={}, walk=False, steps=10),
+    "C3": dict(cols=1280, rows=960, voxel=0.002, capacity=C3_CAPACITY, walk=False, steps=10),
     # C5 hash stress: 10 mm voxels, 50 k-frame random walk (seed 13 + rank, <= 1 cm / 0.5 deg per
     # frame), reference capacities; frames rendered on the GPU (synth.render_depth_torch)
-    "C5": dict(cols=640, rows=480, voxel=0.01, capacity={}, walk=True, steps=50000),
+    "C5": dict(cols=640, rows=480, voxel=0.01, capacity={}, walk=True, steps=1563),
 }
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="timed frames (default: 200; C5: 50000)")
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=["C2", "C3", "C3I", "C5"], default="C2",
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps of --frames-per-step frames each (default: C2/C3 10, C5 1563 = 50 k frames)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed warm-up steps (default 2)")
+    ap.add_argument("--frames-per-step", type=int, default=32,
+                    help="frames per step: one tf_process_frames batch (32 = one enqueue group)")
+    ap.add_argument("--per-call-frames", type=int, default=64,
+                    help="frames of the per-call (one tf_process_frame per frame) rate beside the batched one; 0 = skip")
+    ap.add_argument("--config", choices=["C2", "C3", "C3I", "C3R", "C5"], default="C2",
                     help="C2: 640x480 orbit, 5 mm (BASELINE configs[1], the headline); "
                          "C3: 1280x960, 2 mm, capacities beyond the reference's (configs[2]); "
                          "C5: 10 mm hash stress, 50 k-frame random walk (configs[4]); "
-                         "C3I: IntegrateIntoScene alone over 2^21 active blocks at C3 geometry (HBM-bound)")
+                         "C3I: IntegrateIntoScene alone over 2^21 - 1 active blocks at C3 geometry (HBM-bound); "
+                         "C3R: both raycasts (CreateICPMaps castRay<true> + renderImage castRay + grey) over the same "
+                         "2^21 - 1 block scene")
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--voxel", type=float, default=None)
@@ -68,20 +72,16 @@ def parse():
     ap.add_argument("--profile-every", type=int, default=16,
                     help="timed region: HIP events around the dominant kernel on every N-th frame only "
                          "(an event pair is a few us of dispatch gap; 1 = every frame)")
-    ap.add_argument("--breakdown-frames", type=int, default=60, help="frames of the per-stage timing pass")
+    ap.add_argument("--breakdown-frames", type=int, default=64, help="frames of the per-stage timing pass")
     return ap.parse_args()
 
 
 def stage_bytes(stage, p, nvis, W, H):
     """Algorithmic HBM bytes of ONE launch of a stage."""
     if stage == "raycast_icp":
-        if RENDER_FUSED:
-            # default schedule (render mode 3): both raycasts in one launch -- float4 ray image +
-            # uchar4 grey image out, every visible block read once per raycast
-            return W * H * (16 + 4) + 2 * nvis * (2048 + 16)
-        return W * H * 16 + nvis * (2048 + 16)          # ray output float4 + every visible block once
-    if stage == "raycast_render":
-        return W * H * 4 + nvis * (2048 + 16)           # fused raycast + grey: uchar4 out + blocks once
+        # both raycasts in one launch: float4 ray image + uchar4 grey image out, every visible
+        # block read once per raycast
+        return W * H * (16 + 4) + 2 * nvis * (2048 + 16)
     if stage == "integrate":
         return nvis * (4096 + 20) + W * H * 4           # voxel R+W + entry/id + depth image
     if stage == "grey":
@@ -138,21 +138,44 @@ def hbm_stream_copy(device, gib=1.0, reps=10):
     return 2.0 * n * 4 / (ms * 1e-3) / 1e9
 
 
-def cpu_baseline(frames, params_kw, seconds, omp=False):
-    """Oracle (C restatement of the reference) on a bounded prefix of the same stream: the serial
-    build (1 thread) or its OpenMP build (omp=True: independent pixels / CTAs / blocks over
-    OMP_NUM_THREADS threads, the allocation pass serial; results identical)."""
+def cpu_run(frames, params_kw, n, omp):
+    """One timed run of the oracle over frames 0..n-1 from a fresh context (frame 0 takes the
+    integrate-only path, the rest track); returns seconds."""
     from oracle import oracle as O
     o = O.Oracle(O.default_params(**params_kw), omp=omp)
     t0 = time.perf_counter()
-    n = 0
-    while n < len(frames):
-        o(frames[n])
-        n += 1
-        if time.perf_counter() - t0 >= seconds and n >= 3:
-            break
-    dt = time.perf_counter() - t0
-    return n / dt, n, dt
+    for k in range(n):
+        o(frames[k])
+    return time.perf_counter() - t0
+
+
+def cpu_baseline_protocol(frames, params_kw, seconds, nt):
+    """BASELINE.md CPU protocol on the GPU box's host: for the OpenMP build (nt threads) and the
+    serial build, one warm-up run, then the median of 5 timed runs of a bounded sample of the
+    same stream (each run a fresh context over frames 0..n-1, n sized so the 5 runs take about
+    `seconds` / 2 per build); plus C1 (the frame-0 integrate-only path on frame 0, median of 5
+    after a warm-up) as ms/frame."""
+    res = {}
+    for name, omp in (("omp", True), ("serial", False)):
+        t_warm = cpu_run(frames, params_kw, 2, omp)                 # warm-up (also sizes the sample)
+        per = max(t_warm / 2, 1e-3)
+        n = int(max(3, min(len(frames), seconds / 2 / 5 / per)))
+        runs = sorted(cpu_run(frames, params_kw, n, omp) for _ in range(5))
+        c1 = sorted(cpu_run(frames, params_kw, 1, omp) for _ in range(6))[1:]   # first = warm-up
+        res[name] = {"fps": n / runs[2], "n": n, "runs_s": [round(r, 3) for r in runs],
+                     "c1_ms": 1000.0 * sorted(c1)[2]}
+    o, s1 = res["omp"], res["serial"]
+    model, nproc = cpu_model()
+    return {"value": round(o["fps"], 4), "unit": "frames/s", "cores": nt, "kind": "port",
+            "sample": f"oracle (C restatement, OpenMP build: per-pixel / per-CTA / per-block loops on {nt} threads, "
+                      f"allocation serial), frames 0..{o['n'] - 1} of the same stream from a fresh context; "
+                      f"median of 5 runs after 1 warm-up ({o['runs_s']} s); host CPU of the GPU box",
+            "c1_ms_per_frame": round(o["c1_ms"], 3),
+            "single_thread": {"value": round(s1["fps"], 4), "cores": 1,
+                              "sample": f"serial oracle, frames 0..{s1['n'] - 1}, median of 5 runs after 1 warm-up "
+                                        f"({s1['runs_s']} s)",
+                              "c1_ms_per_frame": round(s1["c1_ms"], 3)},
+            "cpu_model": model, "nproc": nproc}
 
 
 def combine_ranks(elapsed, frames, device, world):
@@ -169,12 +192,10 @@ def combine_ranks(elapsed, frames, device, world):
     return float(mx[0]), float(sm[0])
 
 
-def c3_integrate(args):
-    """C3I ("integrate over the active list is truly HBM-bound"): 2^21 active
-    voxel blocks (4 GiB of voxels) fill the 1280x960 frustum from 0.3 m on, every one in the
-    visible list; one IntegrateIntoScene pass per step against a wall at 1.5 m, all passes
-    back to back on the context stream, timed by HIP events.  Algorithmic bytes per pass:
-    Nvis x (4096 voxel R+W + 20 entry/id) + W x H x 4 (dists)."""
+def c3_scene():
+    """The C3 HBM-scale scene (~2 M active blocks): 2^21 - 1 voxel blocks
+    (4 GiB of voxels) fill the 1280x960 frustum in layers from 0.3 m on (to ~2.8 m), every one in
+    the visible list, uploaded as the hash + visible list; dists of a wall at 1.5 m."""
     import torch
     from topfusion_amd import TopFu, default_params, synth
     from topfusion_amd import _lib as L
@@ -207,20 +228,36 @@ def c3_integrate(args):
     tf.upload(L.TF_BUF_VISIBLE_IDS, ids)
     tf.set_counters(-1, p.n_excess - 1, nb)
     tf.stage_preprocess(np.full((H, W), 1500, np.uint16))   # dists of a wall at 1.5 m
+    return tf, p, W, H, vox, nb
+
+
+def _pmc(config, stage):
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            return (json.load(open(pmc_path)).get(config, {}) or {}).get(stage, {}) or {}
+        except Exception:
+            return {}
+    return {}
+
+
+def c3_integrate(args):
+    """C3I ("integrate over the active list is truly HBM-bound"): one
+    IntegrateIntoScene pass per step over the c3_scene() blocks against the wall at 1.5 m, all
+    passes back to back on the context stream, timed by HIP events.  Algorithmic bytes per
+    pass: Nvis x (4096 voxel R+W + 20 entry/id) + W x H x 4 (dists)."""
+    tf, p, W, H, vox, nb = c3_scene()
     I = np.eye(4, dtype=np.float32)[:3]
     tf.time_stage("integrate", I, 2)                        # warm-up
     ms = tf.time_stage("integrate", I, args.steps)
     b = nb * (4096 + 20) + W * H * 4
     ach = b / (ms * 1e-3) / 1e9
-    pmc = {}
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        pmc = (json.load(open(pmc_path)).get("C3I", {}) or {}).get("integrate", {})
+    pmc = _pmc("C3I", "integrate")
     out = {"metric": f"IntegrateIntoScene passes/sec over {nb} active voxel blocks @{W}x{H}, {vox * 1000:g} mm",
            "value": round(1000.0 / ms, 2), "unit": "passes/s", "n_gpus": 1, "steps": args.steps, "warmup": 2,
            "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
            "dtype": "f32", "data": "synthetic",
-           "config": {"workload": "C3I: k_integrate over 2^21 blocks filling the frustum from 0.3 m, wall at 1.5 m",
+           "config": {"workload": "C3I: k_integrate over 2^21 - 1 blocks filling the frustum from 0.3 m, wall at 1.5 m",
                       "cols": W, "rows": H, "voxel_m": vox, "active_blocks": int(nb), "parallelism": "replicas1"},
            "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": pmc.get("bytes_per_launch"),
@@ -230,12 +267,114 @@ def c3_integrate(args):
     tf.close()
 
 
+def c3_raycast(args):
+    """C3R ("integrate and raycast over the active list"): the c3_scene()
+    blocks after 4 integrate passes against the wall at 1.5 m (free space in front of it, the
+    surface band at it), the range image at RenderState's initial (0.2 m, 3.0 m); one step = one
+    k_raycast_pair launch -- CreateICPMaps' castRay<true> + renderImage's castRay + grey over
+    every pixel -- back to back, HIP events.  Algorithmic bytes per launch: W x H x (16 point
+    image + 4 grey image) + 2 x B x 2064, B = the blocks the ICP-map raycast reads (its
+    castRay<true> visibility marks, counted after the run)."""
+    from topfusion_amd import _lib as L
+    tf, p, W, H, vox, nb = c3_scene()
+    I = np.eye(4, dtype=np.float32)[:3]
+    tf.time_stage("integrate", I, 4)                        # the surface at 1.5 m
+    rng = np.empty((H, W, 2), np.float32)
+    rng[..., 0], rng[..., 1] = p.viewFrustum_min, p.viewFrustum_max
+    tf.upload(L.TF_BUF_RANGE, rng)
+    tf.upload(L.TF_BUF_VISIBLE_TYPE, np.zeros(tf.nbytes(L.TF_BUF_VISIBLE_TYPE), np.uint8))
+    tf.time_stage("raycast_render", I, 2)                   # warm-up
+    ms = tf.time_stage("raycast_render", I, args.steps)
+    touched = int((tf.visible_type() > 0).sum())
+    ray = tf.raycast_result()
+    hit = float((ray[..., 3] > 0).mean())
+    b = W * H * (16 + 4) + 2 * touched * (2048 + 16)
+    ach = b / (ms * 1e-3) / 1e9
+    pmc = _pmc("C3R", "raycast_icp")
+    out = {"metric": f"raycast passes/sec (CreateICPMaps + renderImage castRay, grey) over {nb} allocated voxel blocks "
+                     f"@{W}x{H}, {vox * 1000:g} mm",
+           "value": round(1000.0 / ms, 2), "unit": "passes/s", "n_gpus": 1, "steps": args.steps, "warmup": 2,
+           "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32", "data": "synthetic",
+           "config": {"workload": "C3R: k_raycast_pair over 2^21 - 1 blocks filling the frustum 0.3-2.8 m, "
+                                  "surface of a wall at 1.5 m, range 0.2-3.0 m",
+                      "cols": W, "rows": H, "voxel_m": vox, "allocated_blocks": int(nb),
+                      "blocks_read_by_rays": touched, "rays_hit_fraction": round(hit, 4), "parallelism": "replicas1"},
+           "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": pmc.get("bytes_per_launch"),
+                        "kernel": "k_raycast_pair", "algorithmic_bytes_per_launch": b, "avg_launch_ms": round(ms, 5),
+                        "timing": "HIP events around back-to-back launches on the context stream"}}
+    print(json.dumps(out))
+    tf.close()
+
+
+def orbit_frames(n, W, H, seed, device):
+    """C2/C3 input: n frames of the synthetic orbit (room + sphere, 0.25 deg per frame
+    around a pivot 1.2 m ahead, 1 mm noise), rendered on the GPU in batches straight into HBM
+    (synth.render_depth_torch -- the host renderer's geometry, torch's noise generator)."""
+    import torch
+    from topfusion_amd import synth
+    R = np.empty((n, 3, 3))
+    t = np.empty((n, 3))
+    for k in range(n):
+        R[k], t[k] = synth.orbit_pose(k)
+    dev = torch.empty((n, H, W), dtype=torch.int16, device=device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    for b0 in range(0, n, 128):
+        b1 = min(n, b0 + 128)
+        dev[b0:b1] = synth.render_depth_torch(R[b0:b1], t[b0:b1], W, H, noise_mm=1.0, generator=gen, device=device)
+    return dev
+
+
+def walk_frames(n, W, H, seed, device):
+    """C5 input: the seed-13 random walk (<= 1 cm / 0.5 deg per frame), rendered on the GPU."""
+    import torch
+    from topfusion_amd import synth
+    R, t = synth.random_walk_poses(n, seed=seed)
+    dev = torch.empty((n, H, W), dtype=torch.int16, device=device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    for b0 in range(0, n, 128):
+        b1 = min(n, b0 + 128)
+        dev[b0:b1] = synth.render_depth_torch(R[b0:b1], t[b0:b1], W, H, noise_mm=1.0, generator=gen, device=device)
+    return dev
+
+
+def per_call_rate(tf, base, frame_bytes, n):
+    """TopFu::operator() semantics (demo.cpp:102-105): one tf_process_frame call per frame, each
+    synchronous (a host round trip per frame, no lookahead), wall clock over n frames."""
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(n):
+        tf(base + k * frame_bytes)
+    torch.cuda.synchronize()
+    return n / (time.perf_counter() - t0)
+
+
+def icp_occupancy():
+    """The ICP kernel's occupancy / wait / LDS figures from the committed rocprofv3 PMC pass
+    (profiles/icp_occupancy.json, tools/icp_occupancy.py), if present."""
+    path = os.path.join(ROOT, "profiles", "icp_occupancy.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path))
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
     if args.config == "C3I":
         if args.steps is None:
             args.steps = 20
         return c3_integrate(args)
+    if args.config == "C3R":
+        if args.steps is None:
+            args.steps = 20
+        return c3_raycast(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -251,40 +390,33 @@ def main():
     cfg = CONFIGS[args.config]
     if args.steps is None:
         args.steps = cfg["steps"]
+    if args.warmup is None:
+        args.warmup = 2
     W = args.cols or cfg["cols"]
     H = args.rows or cfg["rows"]
     if args.voxel is None:
         args.voxel = cfg["voxel"]
+    F = args.frames_per_step
     fx, fy, cx, cy = synth.intrinsics(W, H)
     pkw = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=args.voxel, **cfg["capacity"])
-    n_breakdown = 0 if args.no_profile else min(args.breakdown_frames, args.steps)
-    n_frames = args.warmup + args.steps
-    if cfg["walk"]:
-        # C5: poses on the host, depth rendered on the GPU in batches; the CPU baseline's bounded
-        # sample is the same frames, downloaded
-        R, t = synth.random_walk_poses(n_frames, seed=13 + rank)
-        dev = torch.empty((n_frames, H, W), dtype=torch.int16, device=f"cuda:{local_rank}")
-        gen = torch.Generator(device=f"cuda:{local_rank}")
-        gen.manual_seed(13 + rank)
-        for b0 in range(0, n_frames, 128):
-            b1 = min(n_frames, b0 + 128)
-            dev[b0:b1] = synth.render_depth_torch(R[b0:b1], t[b0:b1], W, H, noise_mm=1.0, generator=gen,
-                                                  device=f"cuda:{local_rank}")
-        frames = dev[:min(n_frames, 64)].cpu().numpy().view(np.uint16)
-    else:
-        frames = synth.orbit_sequence(n_frames, W, H, seed=7 + rank)
-        dev = torch.from_numpy(frames.view(np.int16)).to(f"cuda:{local_rank}")
+    n_breakdown = 0 if args.no_profile else min(args.breakdown_frames, args.steps * F)
+    n_frames = (args.warmup + args.steps) * F
+    device = f"cuda:{local_rank}"
+    seed = (13 if cfg["walk"] else 7) + rank
+    dev = (walk_frames if cfg["walk"] else orbit_frames)(n_frames, W, H, seed, device)
     frame_bytes = W * H * 2
     base = dev.data_ptr()
 
     tf = TopFu(default_params(**pkw), device=local_rank)
     single = [k for k in SINGLE_KERNEL_STAGES if k != "icp" or tf.icp_persistent()]
     torch.cuda.synchronize()
-    # warm-up, every stage timed: picks the dominant single-kernel stage
+    # warm-up (whole steps: full enqueue groups), every stage timed: picks the dominant
+    # single-kernel stage
     dominant = "icp" if tf.icp_persistent() else "raycast_icp"
     if args.warmup > 0:
         tf.profile(not args.no_profile)
-        tf.process_frames(base, args.warmup)
+        for w in range(args.warmup):
+            tf.process_frames(base + w * F * frame_bytes, F)
         if not args.no_profile:
             pw = tf.profile_read()
             avg = {k: pw[k][0] / pw[k][1] for k in single if pw[k][1]}
@@ -294,31 +426,44 @@ def main():
     # --profile-every-th frame (an event pair costs a few us of dispatch gap; the full per-stage
     # breakdown comes from a separate pass below)
     tf.profile(not args.no_profile, stages=[dominant], every=args.profile_every)
-    resets_before = tf.stats()["n_resets"]
+    tf.reset_totals()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    ok = tf.process_frames(base + args.warmup * frame_bytes, args.steps)
+    oks = []
+    for k in range(args.steps):
+        oks.append(tf.process_frames(base + (args.warmup + k) * F * frame_bytes, F))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ok = np.concatenate(oks)
     prof_timed = tf.profile_read() if not args.no_profile else {}
+    tot = tf.totals()
     st = tf.stats()
     prof = {}
     if n_breakdown:
         # per-stage breakdown: a fresh context replays the warm-up and the first frames of the
         # timed region with every stage timed (outside the timed region)
         tb = TopFu(default_params(**pkw), device=local_rank)
-        tb.process_frames(base, args.warmup)
+        tb.process_frames(base, args.warmup * F)
         tb.profile(True)
-        tb.process_frames(base + args.warmup * frame_bytes, n_breakdown)
+        tb.process_frames(base + args.warmup * F * frame_bytes, n_breakdown)
         prof = tb.profile_read()
         tb.close()
         torch.cuda.synchronize()
+    # TopFu::operator() per call (one host round trip per frame, no lookahead), beside the
+    # batched rate; a fresh context on the same frames, outside the timed region
+    per_call = None
+    if args.per_call_frames > 0:
+        tc = TopFu(default_params(**pkw), device=local_rank)
+        nc = min(args.per_call_frames, n_frames)
+        per_call = per_call_rate(tc, base, frame_bytes, nc)
+        tc.close()
 
-    elapsed_max, total_frames = combine_ranks(elapsed, args.steps, f"cuda:{local_rank}", world)
+    total_steps_frames = args.steps * F
+    elapsed_max, total_frames = combine_ranks(elapsed, total_steps_frames, device, world)
 
     if rank == 0:
         value = total_frames / elapsed_max
@@ -330,8 +475,11 @@ def main():
         icp_integ = None
         if prof and prof["icp"][1]:
             icp_integ = per_stage["icp"] + per_stage["alloc"] + per_stage["integrate"]
+        integrated = max(1, tot["frames"] - tot["resets"])
+        nvis_mean = tot["visible_sum"] / integrated
         # roofline of the dominant single-kernel stage (by measured time); every single-kernel
-        # stage is also reported under roofline_stages
+        # stage is also reported under roofline_stages, with the mean visible-block count of the
+        # timed frames
         roof, roof_all = None, {}
         if prof or prof_timed:
             pmc = {}
@@ -341,37 +489,34 @@ def main():
                     pmc = json.load(open(pmc_path)).get(args.config, {})
                 except Exception:
                     pmc = {}
-            nvis = st["noVisibleEntries"]
             for k in single:
                 ms = timed_ms if (k == dominant and timed_ms) else per_stage.get(k)
                 if not ms:
                     continue
-                b = stage_bytes(k, tf.params(), nvis, W, H)
+                b = stage_bytes(k, tf.params(), nvis_mean, W, H)
                 ach = b / (ms * 1e-3) / 1e9
                 roof_all[k] = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                "frac": round(ach / PEAK_HBM_GBS, 5),
                                "traffic": (pmc.get(k) or {}).get("bytes_per_launch"),
-                               "kernel": KERNEL_OF_STAGE[k], "algorithmic_bytes_per_launch": b,
+                               "kernel": KERNEL_OF_STAGE[k], "algorithmic_bytes_per_launch": int(b),
                                "avg_launch_ms": round(ms, 5),
                                "timing": (f"HIP events around every {args.profile_every}-th launch of the timed region "
                                           f"({prof_timed[k][1]} launches)") if (k == dominant and timed_ms)
                                          else "HIP events in the breakdown pass"}
             if dominant in roof_all:
                 roof = roof_all[dominant]
-        stream_gbs = round(hbm_stream_copy(f"cuda:{local_rank}"), 1)
+            occ = icp_occupancy()
+            if occ and "icp" in roof_all:
+                roof_all["icp"]["occupancy"] = (occ.get(args.config) or occ.get("C2"))
+        stream_gbs = round(hbm_stream_copy(device), 1)
         cpu = None
         if not args.no_cpu_baseline:
-            # all cores: the OpenMP build of the oracle; 1 thread: the serial build (reported beside)
+            # all cores: the OpenMP build of the oracle; 1 thread: the serial build (reported
+            # beside); BASELINE.md protocol: one warm-up frame, then the median of 5 repeats of a
+            # bounded sample of the same stream
+            frames = dev[:min(n_frames, 64)].cpu().numpy().view(np.uint16)
             nt = omp_threads()
-            v, n, dt = cpu_baseline(frames, pkw, args.cpu_seconds, omp=True)
-            v1, n1, dt1 = cpu_baseline(frames, pkw, args.cpu_seconds, omp=False)
-            cpu = {"value": round(v, 4), "unit": "frames/s", "cores": nt, "kind": "port",
-                   "sample": f"oracle (C restatement, OpenMP build: per-pixel / per-CTA / per-block loops on {nt} "
-                             f"threads, allocation serial) on frames 0..{n - 1} of the same {args.config} stream, "
-                             f"{W}x{H}, {dt:.1f} s, host CPU of the GPU box",
-                   "single_thread": {"value": round(v1, 4), "cores": 1,
-                                     "sample": f"serial oracle on frames 0..{n1 - 1}, {dt1:.1f} s"},
-                   "cpu_model": cpu_model()[0], "nproc": cpu_model()[1]}
+            cpu = cpu_baseline_protocol(frames, pkw, args.cpu_seconds, nt)
         out = {
             "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame",
             "value": round(value, 2),
@@ -389,16 +534,27 @@ def main():
                                    f"{args.voxel * 1000:g} mm voxels, 8^3 blocks, "
                                    "3-level ICP (10/5/4) + alloc + integrate + renderImage + expected depths + "
                                    "ICP-map raycast; one independent stream per GPU",
+                       "step": f"one tf_process_frames batch of {F} consecutive frames (one enqueue group), "
+                               f"frames resident in HBM",
+                       "frames_per_step": F,
                        "cols": W, "rows": H, "voxel_m": args.voxel, "parallelism": f"replicas{world}",
                        "capacity": cfg["capacity"] or "reference defaults"},
+            "ms_per_frame": round(elapsed_max / total_steps_frames * 1000.0, 5),
+            "per_call_frames_per_sec": None if per_call is None else round(per_call, 2),
+            "per_call": (f"TopFu::operator() per call: tf_process_frame on {min(args.per_call_frames, n_frames)} frames, "
+                         "one host round trip per frame, no lookahead (demo.cpp:102-105 semantics), rank 0 only")
+                        if per_call is not None else None,
             "icp_integrate_ms_per_frame": None if icp_integ is None else round(icp_integ, 4),
             "stage_ms_per_frame": {k: (None if v is None else round(v, 4)) for k, v in per_stage.items()},
             "stage_breakdown": (f"separate replay of the timed region's first {n_breakdown} frames in a fresh context, "
                                 f"every stage timed (HIP events; averages per executed launch)") if n_breakdown else None,
-            "frames_ok": int(ok.sum()), "resets": int(st["n_resets"] - resets_before),
-            "ok_frames_per_sec": round(int(ok.sum()) * (total_frames / args.steps) / elapsed_max, 2),
+            "frames_ok": int(ok.sum()), "resets": int(tot["resets"]),
+            "ok_frames_per_sec": round(int(ok.sum()) * (total_frames / total_steps_frames) / elapsed_max, 2),
+            "visible_blocks_mean": round(nvis_mean, 1),
+            "render_tiles_mean": round(tot["tiles_sum"] / max(1, tot["frames_tracked"]), 1),
             "visible_blocks_last": st["noVisibleEntries"],
             "allocated_blocks_last": int(tf.params().n_blocks - 1 - st["lastFreeBlockId"]),
+            "last_frame_ok": bool(ok[-1]),
             "roofline": roof,
             "hbm_stream_copy_GBs": stream_gbs,
             "roofline_stages": roof_all,

@@ -190,10 +190,10 @@ typedef enum tf_stage_id {
     TF_STAGE_ICP = 1,             /* estimateTransform, all iterations */
     TF_STAGE_ALLOC = 2,           /* AllocateSceneFromDepth */
     TF_STAGE_INTEGRATE = 3,       /* IntegrateIntoScene (k_integrate only) */
-    TF_STAGE_RAYCAST_RENDER = 4,  /* renderImage raycast (k_raycast) */
-    TF_STAGE_GREY = 5,            /* renderGrey */
+    TF_STAGE_RAYCAST_RENDER = 4,  /* renderImage raycast (fused into TF_STAGE_RAYCAST_ICP in the frame) */
+    TF_STAGE_GREY = 5,            /* renderGrey (fused likewise) */
     TF_STAGE_EXPECTED_DEPTHS = 6, /* CreateExpectedDepths */
-    TF_STAGE_RAYCAST_ICP = 7,     /* CreateICPMaps raycast<true> (k_raycast) */
+    TF_STAGE_RAYCAST_ICP = 7,     /* CreateICPMaps raycast<true> + renderImage (k_raycast_pair) */
     TF_STAGE_ICP_MAPS = 8         /* renderICP + resizePointsNormals */
 } tf_stage_id;
 tf_status tf_profile_enable(tf_ctx* ctx, int enable);
@@ -209,10 +209,24 @@ tf_status tf_profile_reset(tf_ctx* ctx);
 /* ms[i] = accumulated milliseconds, counts[i] = frames measured, for i < n (n <= 9) */
 tf_status tf_profile_read(tf_ctx* ctx, double* ms, long long* counts, int n);
 tf_status tf_set_counters(tf_ctx* ctx, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries);
+/* Frame totals accumulated on the device by every frame's end since tf_create or the last
+ * tf_reset_totals (measurement; no reference counterpart -- the reference's only metric is the
+ * SampledScopeTime average, tfusion/src/core.cpp:202-216). */
+typedef struct tf_totals {
+    long long frames;               /* TopFu::operator() calls completed */
+    long long frames_tracked;       /* tracking path with ICP ok (alloc + integrate + both raycasts) */
+    long long resets;               /* ICP failures -> reset (topfu.cpp:263-264) */
+    long long visible_sum;          /* noVisibleEntries summed over the frames that integrated */
+    long long tiles_sum;            /* noTotalBlocks summed over the tracked frames */
+} tf_totals;
+tf_status tf_get_totals(tf_ctx* ctx, tf_totals* totals);
+tf_status tf_reset_totals(tf_ctx* ctx);
 /* Measurement: `iters` back-to-back launches of one stage's kernels on the context stream
- * with the pose/matrices of tf_stage_* (stage = TF_STAGE_INTEGRATE or TF_STAGE_RAYCAST_ICP),
- * timed by HIP events on that stream; *ms_per_iter = elapsed / iters.  The scene is updated
- * by every launch exactly as by tf_stage_integrate / tf_stage_raycast. */
+ * with the pose/matrices of tf_stage_* (stage = TF_STAGE_INTEGRATE: k_integrate;
+ * TF_STAGE_RAYCAST_ICP: castRay<true> into raycastResult; TF_STAGE_RAYCAST_RENDER: the frame's
+ * k_raycast_pair -- castRay<true> + renderImage's castRay and grey, over the current range
+ * image), timed by HIP events on that stream; *ms_per_iter = elapsed / iters.  The scene is
+ * updated by every launch exactly as by tf_stage_integrate / tf_stage_raycast. */
 tf_status tf_time_stage(tf_ctx* ctx, int stage, const float pose_rt[12], int iters, float* ms_per_iter);
 
 #ifdef __cplusplus

@@ -141,17 +141,12 @@ def test_icp_stage(oracle_mod, icp_schedule):
     assert_bit_exact("icp affine", aff.reshape(12), affine)
 
 
-ICP_SCHED = {"persistent_hier_allgather": "3", "persistent_hier": "2", "persistent_flat": "0", "persistent_allgather": "1", "per_iteration": "2"}
-
-
-@pytest.fixture(params=list(ICP_SCHED))
+@pytest.fixture(params=["persistent", "per_iteration"])
 def icp_schedule(request, monkeypatch):
-    """Run a test under every ICP schedule (tf_create reads TFUSION_ICP_PERSISTENT and
-    TFUSION_ICP_SCHED: 3 hierarchical gather + allgather of the partials (default),
-    2 hierarchical gather + broadcast, 0 flat gather, 1 allgather)."""
+    """Run a test under both ICP schedules: the persistent one-launch-per-frame kernel (the
+    default) and the per-iteration fallback tf_create picks when the persistent grid cannot be
+    co-resident (forced with TFUSION_ICP_PERSISTENT=0)."""
     monkeypatch.setenv("TFUSION_ICP_PERSISTENT", "0" if request.param == "per_iteration" else "1")
-    monkeypatch.setenv("TFUSION_ICP_SCHED", ICP_SCHED[request.param])
-    monkeypatch.delenv("TFUSION_ICP_ALLGATHER", raising=False)
     return request.param
 
 
@@ -251,33 +246,22 @@ def test_capacity_exhaustion(oracle_mod):
     compare_scene(g, o, "exhausted")
 
 
-@pytest.mark.parametrize("render_mode", ["0", "1", "2", "3", "3-lookahead1", "3-no-lookahead", "3-unfused-ed", "3-unfused-end", "3-vis-scan", "3-unfolded-t3"])
-def test_batched_frames_overlap(oracle_mod, monkeypatch, render_mode):
+def test_batched_frames_overlap(oracle_mod, icp_schedule):
     """The device-driven batch path (tf_process_frames): frames enqueued back to back with no
-    host sync, renderImage on the render stream overlapping the frame's tail and the next
-    frame's ICP, inline, or fused with CreateICPMaps' raycast (TFUSION_RENDER_MODE 0-3); with
-    the fused render, later frames' preprocessing runs in this frame's grid tails
-    (TFUSION_LOOKAHEAD: 2 = two-frame with ping-pong level-0 depth, the default; 1 = next
-    frame; 0 = off; across the 32-frame group boundary and the ICP-failure resets too), and
-    CreateExpectedDepths' projection pass inside k_integrate's grid (TFUSION_FUSE_ED=1, the
-    default) or as its own launch (0), and the frame end (ResetScene on ICP failure) inside
-    k_icp_maps' grid (TFUSION_FUSE_END=1, the default for modes 2-3) or as its own launch, and
-    the visible-list compaction as count + apply launches (the default) or as one look-back
-    scan (TFUSION_VIS_SCAN=1), and setToType3 + the renderImage snapshot in the persistent
-    ICP grid's tail (TFUSION_FOLD_T3=1, the default for modes 2-3) or as their own launch.  Per-frame results, the last frame's grey image, the final pose and the whole
-    scene match the oracle run frame by frame."""
+    host sync, CreateICPMaps' raycast and renderImage in one launch, later frames'
+    preprocessing in this frame's grid tails (two-frame lookahead with ping-pong level-0 depth,
+    across the 32-frame group boundary and the ICP-failure resets too), CreateExpectedDepths'
+    projection inside k_integrate's grid, the frame end (ResetScene on ICP failure) inside
+    k_icp_maps' grid and setToType3 + the renderImage snapshot in the persistent ICP grid's
+    tail.  Per-frame results, the last frame's grey image, the final pose and the whole scene
+    match the oracle run frame by frame."""
     from parity_util import DeviceFrames
     from topfusion_amd import TopFu, default_params
-    monkeypatch.setenv("TFUSION_RENDER_MODE", render_mode[0])
-    monkeypatch.setenv("TFUSION_LOOKAHEAD", {"3-no-lookahead": "0", "3-lookahead1": "1"}.get(render_mode, "2"))
-    monkeypatch.setenv("TFUSION_FUSE_ED", "0" if render_mode == "3-unfused-ed" else "1")
-    monkeypatch.setenv("TFUSION_FUSE_END", "0" if render_mode == "3-unfused-end" else "1")
-    monkeypatch.setenv("TFUSION_VIS_SCAN", "1" if render_mode == "3-vis-scan" else "0")
-    monkeypatch.setenv("TFUSION_FOLD_T3", "0" if render_mode == "3-unfolded-t3" else "1")
     cols, rows, n = 320, 240, 40          # 40 frames > one 32-frame enqueue group
     fx, fy, cx, cy = synth.intrinsics(cols, rows)
     args = dict(cols=cols, rows=rows, fx=fx, fy=fy, cx=cx, cy=cy)
     g = TopFu(default_params(**args))
+    _check_schedule(g, icp_schedule)
     o = oracle_mod.Oracle(oracle_mod.default_params(**args))
     seq = synth.orbit_sequence(n, cols, rows, seed=7)
     dev = DeviceFrames(seq)
@@ -295,6 +279,114 @@ def test_batched_frames_overlap(oracle_mod, monkeypatch, render_mode):
     assert_bit_exact("batched final raycast", g.raycast_result(), o.raycast_result())
     g.close()
     dev.free()
+
+
+def _compare_frame_state(g, o, tag, grey=True):
+    sg, so = g.stats(), o.counters()
+    for key in ("frame_counter", "n_resets", "icp_iterations", "lastFreeBlockId", "lastFreeExcessListId",
+                "noVisibleEntries"):
+        assert sg[key] == so[key], f"{tag} {key}: gpu {sg[key]} oracle {so[key]}"
+    assert_bit_exact(f"{tag} pose", g.getCameraPose()[:3, :4], o.pose())
+    if grey:
+        assert_bit_exact(f"{tag} renderImage grey", g.frame_grey(), o.frame_grey())
+    assert_bit_exact(f"{tag} raycast", g.raycast_result(), o.raycast_result())
+    for l in range(3):
+        gp, gn = g.prev_maps(l)
+        op, on = o.prev_maps(l)
+        assert_bit_exact(f"{tag} prev points L{l}", gp, op)
+        assert_bit_exact(f"{tag} prev normals L{l}", gn, on)
+
+
+def test_bench_shape_batched(oracle_mod):
+    """The exact path bench.py times: 640x480, 5 mm, the default schedule,
+    frames handed to tf_process_frames in device memory with the two-frame lookahead -- 36
+    frames as three calls of 12, the state compared with the oracle run frame by frame after
+    every call: counters, pose, the last frame's renderImage, the raycast, all ICP-map levels,
+    and the whole scene at the end."""
+    from parity_util import DeviceFrames
+    g, o = make_pair(oracle_mod)
+    n, chunk = 36, 12
+    seq = synth.orbit_sequence(n, 640, 480, seed=7)
+    dev = DeviceFrames(seq)
+    fb = 640 * 480 * 2
+    for c0 in range(0, n, chunk):
+        okg = g.process_frames(dev.ptr + c0 * fb, chunk)
+        oko = np.array([o(seq[k]) for k in range(c0, c0 + chunk)])
+        assert np.array_equal(okg, oko), (c0, okg, oko)
+        _compare_frame_state(g, o, f"frames {c0}..{c0 + chunk - 1}", grey=bool(oko[-1]))
+    compare_scene(g, o, "bench-shape final")
+    g.close()
+    dev.free()
+
+
+def test_bench_shape_one_batch(oracle_mod):
+    """As test_bench_shape_batched, but 40 frames in ONE tf_process_frames call (two enqueue
+    groups: the lookahead crosses the 32-frame group boundary), final state bit-exact."""
+    from parity_util import DeviceFrames
+    g, o = make_pair(oracle_mod)
+    n = 40
+    seq = synth.orbit_sequence(n, 640, 480, seed=7)
+    dev = DeviceFrames(seq)
+    okg = g.process_frames(dev.ptr, n)
+    oko = np.array([o(seq[k]) for k in range(n)])
+    assert np.array_equal(okg, oko), (okg, oko)
+    _compare_frame_state(g, o, "one batch of 40", grey=bool(oko[-1]))
+    compare_scene(g, o, "one batch final")
+    g.close()
+    dev.free()
+
+
+def test_two_contexts_one_device(oracle_mod):
+    """Two TopFu contexts in one process on one device (contexts share nothing; C4
+    runs one per GPU, but nothing stops several per GPU): streams seeded 7 and 8, frames
+    interleaved context by context, each context bit-exact with its own oracle after every
+    frame."""
+    g1, o1 = make_pair(oracle_mod, 320, 240)
+    g2, o2 = make_pair(oracle_mod, 320, 240)
+    s1 = synth.orbit_sequence(8, 320, 240, seed=7)
+    s2 = synth.orbit_sequence(8, 320, 240, seed=8)
+    for k in range(8):
+        for g, o, s, name in ((g1, o1, s1, "ctx seed 7"), (g2, o2, s2, "ctx seed 8")):
+            okg, oko = g(s[k]), o(s[k])
+            assert okg == oko, f"{name} frame {k}: gpu {okg} oracle {oko}"
+            sg, so = g.last_stats, o.counters()
+            for key in ("lastFreeBlockId", "noVisibleEntries", "icp_iterations", "frame_counter", "n_resets"):
+                assert sg[key] == so[key], f"{name} frame {k} {key}: gpu {sg[key]} oracle {so[key]}"
+            assert_bit_exact(f"{name} frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
+    compare_scene(g1, o1, "ctx seed 7")
+    compare_scene(g2, o2, "ctx seed 8")
+    g1.close()
+    g2.close()
+
+
+def test_c3_capacity_top_block(oracle_mod):
+    """The C3 bench capacity (2^21 - 1 voxel blocks = 4 GiB, 2^22 buckets, 2^20 excess) at C3
+    geometry (1280x960, 2 mm): allocation hands out blocks from the top of the free list, so the
+    first block of every scene is VBA block 2^21 - 2, the one whose voxels sit at the very end of
+    the 32-bit byte-offset range the raycasts use (tf_render.hip vox_at).  Three tracked frames;
+    raycast, grey image, ICP maps, poses and the whole scene bit-exact, with the top block
+    allocated and in the last frame's visible set."""
+    cols, rows = 1280, 960
+    cap = dict(n_buckets=1 << 22, n_excess=1 << 20, n_blocks=(1 << 21) - 1, vis_capacity=1 << 21,
+               max_render_blocks=1 << 20)
+    g, o = make_pair(oracle_mod, cols, rows, voxelSize=0.002, **cap)
+    seq = synth.orbit_sequence(3, cols, rows, seed=7)
+    for k in range(3):
+        okg, oko = g(seq[k]), o(seq[k])
+        assert okg == oko, f"frame {k}: ok gpu {okg} oracle {oko}"
+        sg, so = g.last_stats, o.counters()
+        for key in ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries", "icp_iterations"):
+            assert sg[key] == so[key], f"frame {k} {key}: gpu {sg[key]} oracle {so[key]}"
+        assert_bit_exact(f"frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
+        if k > 0 and oko:
+            assert_bit_exact(f"frame {k} renderImage grey", g.frame_grey(), o.frame_grey())
+    _compare_frame_state(g, o, "C3 capacity", grey=False)
+    h = g.hash()
+    top = np.nonzero(h["ptr"] == cap["n_blocks"] - 1)[0]
+    assert len(top) == 1, "the top VBA block is allocated"
+    assert g.visible_type()[top[0]] > 0, "the top VBA block is in the visible state"
+    compare_scene(g, o, "C3 capacity final")
+    g.close()
 
 
 def test_c5_random_walk_10mm(oracle_mod):

@@ -43,6 +43,13 @@ class TfStats(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class TfTotals(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_longlong) for n in ("frames", "frames_tracked", "resets", "visible_sum", "tiles_sum")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 class TfError(RuntimeError):
     def __init__(self, status, where):
         self.status = status
@@ -103,6 +110,8 @@ def load():
         "tf_upload": ([P, I, I, P, S], I),
         "tf_set_pose": ([P, P], I),
         "tf_set_counters": ([P, I, I, I], I),
+        "tf_get_totals": ([P, ctypes.POINTER(TfTotals)], I),
+        "tf_reset_totals": ([P], I),
         "tf_render_image_type": ([P, I, P, S], I),
         "tf_time_stage": ([P, I, P, I, ctypes.POINTER(ctypes.c_float)], I),
         "tf_profile_enable": ([P, I], I),

@@ -77,7 +77,10 @@ static bool params_valid(const tf_params* p)
     if (p->cols <= 0 || p->rows <= 0 || (p->cols % 4) || (p->rows % 4)) return false;
     if (p->n_buckets <= 0 || (p->n_buckets & (p->n_buckets - 1))) return false;
     if (p->n_excess <= 0 || p->n_blocks <= 0 || p->vis_capacity <= 0 || p->max_render_blocks <= 0) return false;
-    if (p->n_blocks > (1 << 21)) return false;        // VBA byte offsets are 32-bit (tf_render.hip vox_raw)
+    // The render side forms 32-bit byte offsets (voff + guard shift + lin) * 4 from the guard
+    // block before the VBA (tf_render.hip vox_at): block ptr p reads up to 4 * ((p + 2) * 512 - 1)
+    // bytes past the guard, which fits 2^32 only for p <= 2^21 - 2, i.e. n_blocks <= 2^21 - 1.
+    if (p->n_blocks > (1 << 21) - 1) return false;
     if ((p->n_buckets + p->n_excess) % 16) return false;
     if (p->bilateral_kernel_size < 1 || p->bilateral_kernel_size > 7) return false;
     if (p->voxelSize <= 0 || p->mu <= 0) return false;
@@ -91,7 +94,7 @@ static void ctx_free(tf_ctx* c)
 {
     if (!c) return;
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
-                     c->requestList, c->visCounts, c->visFlags, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
+                     c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockBox, c->blockZ, c->blockTiles, c->blockOff, c->edChunk, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->frame_ok, c->frame_mode };
     for (void* b : bufs) if (b) (void)hipFree(b);
@@ -102,9 +105,6 @@ static void ctx_free(tf_ctx* c)
     for (int k = 0; k < 2; ++k) if (c->d0_buf[k]) (void)hipFree(c->d0_buf[k]);
     if (c->st_host) (void)hipHostFree(c->st_host);
     for (int i = 0; i < 2 * TF_NUM_STAGES * TF_PROF_RING; ++i) if (c->prof_ev[i]) (void)hipEventDestroy(c->prof_ev[i]);
-    if (c->ev_integrated) (void)hipEventDestroy(c->ev_integrated);
-    if (c->ev_rendered) (void)hipEventDestroy(c->ev_rendered);
-    if (c->rstream) (void)hipStreamDestroy(c->rstream);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -115,16 +115,8 @@ static hipError_t dalloc(T** p, size_t bytes)
     return hipMalloc((void**)p, bytes < 16 ? 16 : bytes);
 }
 
-// the main stream waits for the last enqueued renderImage (render stream): every entry point
-// that reads or writes what a render may still be reading or writing joins it first
-static hipError_t join_render(tf_ctx* c)
-{
-    return hipStreamWaitEvent(c->stream, c->ev_rendered, 0);
-}
-
 static tf_status sync_state(tf_ctx* c)
 {
-    TF_CHECK(join_render(c));
     TF_CHECK(hipMemcpyAsync(c->st_host, c->st, sizeof(TfDevState), hipMemcpyDeviceToHost, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
@@ -141,7 +133,6 @@ __global__ void k_host_reset(TfDevState* st)
 
 static tf_status ctx_reset(tf_ctx* c)
 {
-    TF_CHECK(join_render(c));
     hipLaunchKernelGGL(k_host_reset, dim3(1), dim3(1), 0, c->stream, c->st);
     TF_CHECK(hipGetLastError());
     TF_CHECK(tfk_reset_scene(c));
@@ -179,11 +170,6 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     c->dist2_thres = pin->icp_dist_thres * pin->icp_dist_thres;
 #define ALLOC(ptr, bytes) do { e = dalloc(&(ptr), (bytes)); if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); } } while (0)
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_integrated, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_rendered, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(c->ev_rendered, c->rstream);
-    if (e == hipSuccess) e = hipEventRecord(c->ev_integrated, c->stream);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     ALLOC(c->hash, sizeof(TfHashEntry) * (size_t)c->n_total);
     ALLOC(c->excessList, sizeof(int) * (size_t)pin->n_excess);
@@ -196,9 +182,6 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->allocCounts, sizeof(int) * 2 * (size_t)c->alloc_chunks);
     ALLOC(c->requestList, sizeof(int) * (size_t)c->n_total);
     ALLOC(c->visCounts, sizeof(int) * (size_t)c->vis_chunks);
-    ALLOC(c->visFlags, sizeof(unsigned long long) * (size_t)c->vis_chunks);
-    e = hipMemset(c->visFlags, 0, sizeof(unsigned long long) * (size_t)c->vis_chunks);   // epoch 0: never a launch's
-    if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     ALLOC(c->visibleIds, sizeof(int) * (size_t)pin->vis_capacity);
     ALLOC(c->visType, ntot_pad);
     ALLOC(c->range, sizeof(float) * 2 * npx);
@@ -276,26 +259,10 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = tfk_check_div3(c, pin->mu, &c->mu_exact3);   // integrate: eta / mu
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
-    {   // ICP schedule: one persistent launch per frame when all its workgroups fit at once
+    {   // ICP: one persistent launch per frame when all its workgroups fit at once; otherwise (or
+        // with TFUSION_ICP_PERSISTENT=0) one k_icp_iter launch per iteration
         const char* env = getenv("TFUSION_ICP_PERSISTENT");
         c->icp_persistent = (env && env[0] == '0') ? 0 : tfk_icp_persistent_ok(c);
-        const char* ag = getenv("TFUSION_ICP_ALLGATHER");
-        const char* sc = getenv("TFUSION_ICP_SCHED");
-        c->icp_sched = 3;
-        if (ag && ag[0] == '1') c->icp_sched = 1;
-        if (sc && sc[0] >= '0' && sc[0] <= '3') c->icp_sched = sc[0] - '0';
-        const char* rm = getenv("TFUSION_RENDER_MODE");
-        c->render_mode = (rm && rm[0] >= '0' && rm[0] <= '3') ? rm[0] - '0' : 3;
-        const char* la = getenv("TFUSION_LOOKAHEAD");   // 0: every frame preprocesses itself
-        c->lookahead = (la && la[0] >= '0' && la[0] <= '2') ? la[0] - '0' : 2;
-        const char* fe = getenv("TFUSION_FUSE_ED");     // 0: k_ed_project as its own launch
-        c->fuse_ed = !(fe && fe[0] == '0');
-        const char* fn = getenv("TFUSION_FUSE_END");    // 0: the frame end as its own launch
-        c->fuse_end = !(fn && fn[0] == '0');
-        const char* vs = getenv("TFUSION_VIS_SCAN");    // 1: one look-back scan launch (A/B: no faster)
-        c->vis_scan = vs && vs[0] == '1';
-        const char* ft = getenv("TFUSION_FOLD_T3");     // 0: k_set_type3 as its own launch
-        c->fold_t3 = !(ft && ft[0] == '0');
     }
     *out = c;
     return TF_OK;
@@ -304,7 +271,6 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
 extern "C" void tf_destroy(tf_ctx* c)
 {
     if (!c) return;
-    (void)hipStreamSynchronize(c->rstream);
     (void)hipStreamSynchronize(c->stream);
     ctx_free(c);
 }
@@ -324,8 +290,6 @@ __global__ void k_stage_begin(TfDevState* st)
 
 static hipError_t clear_abort(tf_ctx* c)
 {
-    hipError_t e = join_render(c);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_stage_begin, dim3(1), dim3(1), 0, c->stream, c->st);
     return hipGetLastError();
 }
@@ -372,7 +336,7 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
         for (int i = 0; i < TF_NUM_STAGES; ++i) {
             if (!c->prof_slot_on[first + f] || !((c->prof_mask >> i) & 1u) || !stage_ran(i, mode[f], ok[f])) continue;
             if (i == TF_STAGE_PREPROCESS && !c->prof_slot_pre[first + f]) continue;   // done by the previous frame
-            if (i == TF_STAGE_RAYCAST_RENDER && c->render_mode == 3) continue;   // fused into RAYCAST_ICP
+            if (i == TF_STAGE_RAYCAST_RENDER) continue;                       // fused into RAYCAST_ICP
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, prof_event(c, first + f, 2 * i), prof_event(c, first + f, 2 * i + 1)) == hipSuccess) {
                 c->prof_ms[i] += ms;
@@ -384,20 +348,21 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
 
 // enqueue one TopFu::operator() frame into batch slot `slot` (no host synchronisation).
 // The frame's branches (frame 0 / tracking / ICP failure -> reset, topfu.cpp:161-330) are
-// decided on the device: the preprocess kernel starts the frame (tf_frame_begin sets
-// st->mode), every later kernel checks st->mode / st->abort, and the gated reset kernel ends
-// it (frame counters, per-slot ok flag).  A batch is therefore enqueued back to back.
+// decided on the device: the ICP launch starts the frame (tf_frame_begin sets st->mode), every
+// later kernel checks st->mode / st->abort, and the frame end in k_icp_maps_end's tail (frame
+// counters, per-slot ok flag, ResetScene on ICP failure) closes it.  A batch is therefore
+// enqueued back to back.  Per frame: k_icp_frame (+ setToType3 and the renderImage snapshot in
+// its tail) -> k_alloc_requests -> k_alloc_apply -> k_vis_count -> k_vis_apply -> k_integrate
+// (+ CreateExpectedDepths' projection) -> k_ed_fill -> k_raycast_pair (CreateICPMaps' castRay
+// and renderImage's castRay + grey in one grid) -> k_icp_maps_end.
 //
-// Lookahead (batches, fused render): later frames' preprocessing runs in this frame's grid
-// tails and their enqueues skip it.  Two-frame (TFUSION_LOOKAHEAD=2, default): k_raycast_pair
-// of frame j runs frame j+1's computeDists + pyramids + normals and frame j+2's bilateral
-// pass, whose level-0 depth goes to the buffer of j's parity (d0_buf, ping-pong); the batch's
-// first frame also runs frame 1's bilateral pass in k_alloc_requests.  One-frame (1): frame
-// j+1's bilateral pass in k_alloc_requests, the rest in k_raycast_pair.  Preprocessing is a
-// pure function of the raw frame; what it writes is past its last reader of this frame by
-// then (level-0 depth: this frame's pyramid pass; dists and the current maps: this frame's
-// allocation, integration and ICP).  (Measured before: preprocessing on a stream of its own
-// costs more in cross-stream waits than the overlap saves.)
+// Lookahead (batches): later frames' preprocessing runs in this frame's grid tails and their
+// enqueues skip it.  k_raycast_pair of frame j runs frame j+1's computeDists + pyramids +
+// normals and frame j+2's bilateral pass, whose level-0 depth goes to the buffer of j's parity
+// (d0_buf, ping-pong); the batch's first frame also runs frame 1's bilateral pass in
+// k_alloc_requests.  Preprocessing is a pure function of the raw frame; what it writes is past
+// its last reader of this frame by then (level-0 depth: this frame's pyramid pass; dists and
+// the current maps: this frame's allocation, integration and ICP).
 struct TfFramePlan {
     int pre_done;            // this frame's preprocessing ran in earlier launches
     uint16_t* d0;            // this frame's level-0 depth buffer
@@ -408,51 +373,25 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
                                const TfFramePlan* plan = nullptr)
 {
     static const TfFramePlan none = { 0, nullptr, {}, {}, {} };
-    if (!plan || c->render_mode != 3) plan = &none;
+    if (!plan) plan = &none;
     uint16_t* d0 = plan->d0 ? plan->d0 : c->d0_buf[0];
     c->prof_slot_on[slot] = c->prof_enabled && (c->prof_seq++ % c->prof_period) == 0;
     c->prof_slot_pre[slot] = !plan->pre_done;
     // preprocessing (topfu.cpp:166-197)
     if (!plan->pre_done) STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, c->stream, d0));
     c->depth_pyr[0] = d0;
-    // (+ setToType3 / the renderImage snapshot in the ICP grid's tail: persistent SCHED-3 ICP,
-    // render inline -- no render stream reads the snapshot)
-    const bool t3_fold = c->fold_t3 && c->icp_persistent && c->icp_sched == 3 && c->render_mode >= 2;
-    STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1, t3_fold));                  // frame begin + topfu.cpp:242-243 (tracking only)
-    // the previous frame's renderImage (render stream) must be done before the scene changes
-    // (modes 2 and 3 render on the main stream: no wait -- an event wait is a barrier packet,
-    // a few microseconds of dispatch gap even when the event has long completed)
-    if (c->render_mode <= 1) TF_CHECK(join_render(c));
-    STAGE(TF_STAGE_ALLOC, tfk_alloc(c, t3_fold ? 2 : 1, plan->alloc_bil, pitch));                        // topfu.cpp:202 / 281 (+ renderImage snapshot)
-    // (+ CreateExpectedDepths' projection pass in the same grid when fuse_ed)
-    STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1, c->fuse_ed));     // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
-    // renderImage (raycast + grey, topfu.cpp:284-285) on the render stream, behind integration;
-    // it overlaps CreateExpectedDepths / CreateICPMaps and the next frame's preprocessing + ICP,
-    // none of which writes what it reads (the scene, the range snapshot, M_render)
-    if (c->render_mode == 2) {   // inline on the main stream (A/B reference)
-        STAGE(TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c, c->stream));
-    } else if (c->render_mode == 0) {
-        TF_CHECK(hipEventRecord(c->ev_integrated, c->stream));
-        TF_CHECK(hipStreamWaitEvent(c->rstream, c->ev_integrated, 0));
-        STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c, c->rstream));
-        TF_CHECK(hipEventRecord(c->ev_rendered, c->rstream));
-    }
-    STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c, c->fuse_ed));   // topfu.cpp:306
-    if (c->render_mode == 3)    // CreateICPMaps raycast + renderImage in one launch (snapshot range)
-        STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch));        // topfu.cpp:284-285 + 307
-    else
-        STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast(c, 1));              // CreateICPMaps, topfu.cpp:307
-    // (+ the frame end in the same grid when fuse_end, render modes 2-3: no render stream reads
-    // the scene behind it)
-    const bool end_fused = c->fuse_end && c->render_mode >= 2;
-    STAGE(TF_STAGE_ICP_MAPS, end_fused ? tfk_icp_maps_end(c, slot) : tfk_icp_maps(c));   // + resizePointsNormals :308-309
-    if (c->render_mode == 1) {   // render behind the frame's tail: it overlaps the next frame's ICP
-        TF_CHECK(hipEventRecord(c->ev_integrated, c->stream));
-        TF_CHECK(hipStreamWaitEvent(c->rstream, c->ev_integrated, 0));
-        STAGE_ON(c->rstream, TF_STAGE_RAYCAST_RENDER, tfk_raycast_grey(c, c->rstream));
-        TF_CHECK(hipEventRecord(c->ev_rendered, c->rstream));
-    }
-    if (!end_fused) TF_CHECK(tfk_reset_scene_on_failure(c, slot));  // frame end; topfu.cpp:263-264
+    // frame begin + estimateTransform + poses_.push_back (topfu.cpp:200, 242-243); with the
+    // persistent ICP, setToType3 / the renderImage snapshot run in its tail
+    const bool t3_fold = c->icp_persistent != 0;
+    STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1, t3_fold));
+    STAGE(TF_STAGE_ALLOC, tfk_alloc(c, t3_fold ? 2 : 1, plan->alloc_bil, pitch));   // topfu.cpp:202 / 281
+    // (+ CreateExpectedDepths' projection pass in the same grid)
+    STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1, 1));              // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
+    STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c, 1));     // topfu.cpp:306
+    // CreateICPMaps' raycast + renderImage (topfu.cpp:284-285 + 307) in one launch (snapshot range)
+    STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch));
+    // renderICP + resizePointsNormals (topfu.cpp:308-309) + the frame end (topfu.cpp:263-264)
+    STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps_end(c, slot));
     return TF_OK;
 }
 
@@ -566,18 +505,19 @@ extern "C" tf_status tf_process_frame_host(tf_ctx* c, const uint16_t* host_depth
 extern "C" tf_status tf_process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t stride, int n, int* ok_out)
 {
     if (!c || !dev_frames || n < 0) return TF_INVALID_ARG;
-    const int la = c->render_mode == 3 ? c->lookahead : 0;
     auto frame = [&](int j) { return (const uint16_t*)((const char*)dev_frames + (size_t)j * stride); };
     for (int first = 0; first < n; first += TF_PROF_RING) {
         const int m = n - first < TF_PROF_RING ? n - first : TF_PROF_RING;
         for (int i = 0; i < m; ++i) {
             const int j = first + i;
-            TfFramePlan p = { la != 0 && j > 0, c->d0_buf[la ? j & 1 : 0], {}, {}, {} };
-            if (la && j + 1 < n) {
+            // two-frame lookahead (enqueue_frame): frame j+1's pyramid pass and frame j+2's
+            // bilateral pass run in frame j's grid tails
+            TfFramePlan p = { j > 0, c->d0_buf[j & 1], {}, {}, {} };
+            if (j + 1 < n) {
                 TfAhead next = { frame(j + 1), c->d0_buf[(j + 1) & 1] };
                 p.pair_pyr = next;
-                if (la == 1 || j == 0) p.alloc_bil = next;
-                if (la == 2 && j + 2 < n) p.pair_bil = TfAhead{ frame(j + 2), c->d0_buf[j & 1] };
+                if (j == 0) p.alloc_bil = next;
+                if (j + 2 < n) p.pair_bil = TfAhead{ frame(j + 2), c->d0_buf[j & 1] };
             }
             tf_status s = enqueue_frame(c, frame(j), (size_t)c->W * 2, i, &p);
             if (s != TF_OK) return s;
@@ -757,16 +697,20 @@ extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
 extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12], int iters, float* ms_per_iter)
 {
     if (!c || !pose_rt || iters <= 0 || !ms_per_iter) return TF_INVALID_ARG;
-    if (stage != TF_STAGE_INTEGRATE && stage != TF_STAGE_RAYCAST_ICP) return TF_INVALID_ARG;
+    if (stage != TF_STAGE_INTEGRATE && stage != TF_STAGE_RAYCAST_ICP && stage != TF_STAGE_RAYCAST_RENDER)
+        return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, pose_rt, stage == TF_STAGE_INTEGRATE ? TF_POSE_ALLOC_NOINV : 0);
     if (s != TF_OK) return s;
+    // the pair's renderImage half reads the snapshot of the raycast matrix / range region
+    if (stage == TF_STAGE_RAYCAST_RENDER) TF_CHECK(tfk_render_snapshot(c));
     hipEvent_t e0, e1;
     TF_CHECK(hipEventCreate(&e0));
     TF_CHECK(hipEventCreate(&e1));
     hipError_t e = hipEventRecord(e0, c->stream);
     for (int i = 0; i < iters && e == hipSuccess; ++i)
-        e = stage == TF_STAGE_INTEGRATE ? tfk_integrate(c) : tfk_raycast(c, 1);
+        e = stage == TF_STAGE_INTEGRATE ? tfk_integrate(c)
+          : stage == TF_STAGE_RAYCAST_ICP ? tfk_raycast(c, 1) : tfk_raycast_pair(c);
     if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
     if (e == hipSuccess) e = hipEventSynchronize(e1);
     float ms = 0.f;
@@ -781,7 +725,6 @@ extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12]
 extern "C" tf_status tf_stage_reset_scene(tf_ctx* c)
 {
     if (!c) return TF_INVALID_ARG;
-    TF_CHECK(join_render(c));
     TF_CHECK(tfk_reset_scene(c));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
@@ -828,7 +771,6 @@ extern "C" tf_status tf_buffer_bytes(tf_ctx* c, int which, int level, size_t* by
 extern "C" tf_status tf_download(tf_ctx* c, int which, int level, void* host, size_t bytes)
 {
     if (!c || !host) return TF_INVALID_ARG;
-    TF_CHECK(join_render(c));
     size_t n;
     void* p = buffer_ptr(c, which, level, &n);
     if (!p || n != bytes) return TF_INVALID_ARG;
@@ -840,17 +782,16 @@ extern "C" tf_status tf_download(tf_ctx* c, int which, int level, void* host, si
 extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host, size_t bytes)
 {
     if (!c || !host) return TF_INVALID_ARG;
-    TF_CHECK(join_render(c));
     size_t n;
     void* p = buffer_ptr(c, which, level, &n);
     if (!p || n != bytes) return TF_INVALID_ARG;
     TF_CHECK(hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
     if (which == TF_BUF_HASH) TF_CHECK(tfk_grid_rebuild(c));       // keep the block grid exact
-    if (which == TF_BUF_HASH || which == TF_BUF_VBA) c->scene_external = 1;   // next reset: full clear
-    if (which == TF_BUF_RANGE) {        // next CreateExpectedDepths initialises the whole buffer again
-        static const int one = 1;
+    static const int one = 1;
+    if (which == TF_BUF_HASH || which == TF_BUF_VBA)    // next reset (in-frame ones too): full clear
+        TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, scene_external), &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (which == TF_BUF_RANGE)          // next CreateExpectedDepths initialises the whole buffer again
         TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, range_full), &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
-    }
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }
@@ -858,7 +799,6 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
 extern "C" tf_status tf_set_pose(tf_ctx* c, const float rt[12])
 {
     if (!c || !rt) return TF_INVALID_ARG;
-    TF_CHECK(join_render(c));
     TF_CHECK(hipMemcpyAsync(c->st->pose, rt, sizeof(float) * 12, hipMemcpyHostToDevice, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
@@ -872,8 +812,28 @@ extern "C" tf_status tf_set_counters(tf_ctx* c, int lastFreeBlockId, int lastFre
     c->st_host->lastFreeBlockId = lastFreeBlockId;
     c->st_host->lastFreeExcessListId = lastFreeExcessListId;
     c->st_host->noVisibleEntries = noVisibleEntries;
-    c->scene_external = 1;                                          // next reset: full clear
+    c->st_host->scene_external = 1;                                 // next reset: full clear
     TF_CHECK(hipMemcpyAsync(c->st, c->st_host, sizeof(TfDevState), hipMemcpyHostToDevice, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)
+{
+    if (!c || !t) return TF_INVALID_ARG;
+    tf_status s = sync_state(c);
+    if (s != TF_OK) return s;
+    const TfDevState* d = c->st_host;
+    t->frames = d->tot_frames; t->frames_tracked = d->tot_tracked; t->resets = d->tot_resets;
+    t->visible_sum = d->tot_visible; t->tiles_sum = d->tot_tiles;
+    return TF_OK;
+}
+
+extern "C" tf_status tf_reset_totals(tf_ctx* c)
+{
+    if (!c) return TF_INVALID_ARG;
+    const long long zero[5] = { 0, 0, 0, 0, 0 };
+    TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, tot_frames), zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }

@@ -430,19 +430,18 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 // maps) instead of a launch plus four dependent loads.  Cross-workgroup exchange uses 64-bit
 // TAGGED slots: each value is stored as (generation << 32 | float bits) with one agent-scope
 // (sc1) 8-byte atomic store, so a reader that sees the current generation also sees the data
-// -- no ticket counter, no fence.  Workgroup 0 polls the 256 column sums, runs the final tree,
-// det (wave 1) and solve/Rodrigues/compose (wave 0) concurrently, and broadcasts the new affine
-// as 13 tagged slots that the other workgroups poll.  Every spin is bounded (status 2 -> the
-// host reports a HIP error) so no wave can outlive a missing peer.
+// -- no ticket counter, no fence.  The exchange of an iteration is the hierarchical gather
+// described above k_icp_frame.  Every spin is bounded (status 2 -> the host reports a HIP
+// error) so no wave can outlive a missing peer.
 // =========================================================================================
 #define IP_WAVES 8
 #define IP_SREG 1                       // CTA slots kept in registers per wave (8 per WG; larger images use k_icp_iter)
 #define IP_SPIN_LIMIT (1u << 21)
-#define IP_BCAST (2 * ICP_NWG * ICP_T_STRIDE)   // column slots are double-buffered by generation parity
-#define IP_PART (IP_BCAST + 16)                  // SCHED 2: 8 residue-class partials, double-buffered
+#define IP_PART (2 * ICP_NWG * ICP_T_STRIDE + 16)   // column slots (double-buffered by generation parity), then
+                                                 // the 8 residue-class partials, double-buffered
 #define IP_NPART 8                               // residue classes of the final tree's first five steps
 #define IP_LDS_PAD (56 * 1024)
-#define IP_DETW (IP_WAVES - 1)                   // SCHED 3: the wave that runs the det check off the critical path
+#define IP_DETW (IP_WAVES - 1)                   // the wave that runs the det check off the critical path
 
 struct IcpFrameArgs {
     IcpLevel lv[TF_LEVELS];             // in processing order (coarse -> fine)
@@ -455,7 +454,7 @@ struct IcpFrameArgs {
     TfDevState* st;
     unsigned long long* tag;            // [256][28] column sums, then [16] broadcast
     // fold_t3: the frame's setToType3 + visibility test and renderImage snapshot (k_set_type3)
-    // run in this grid's tail, once the pose is known (frame path, SCHED 3, inline render)
+    // run in this grid's tail, once the pose is known (frame path)
     int fold_t3;
     VisArgs vis;
     const TfHashEntry* hash;
@@ -638,25 +637,24 @@ __device__ __forceinline__ float ip_residue_tree(const float* c)
     return b[0] + b[1];
 }
 
-// SCHED 0: workgroup 0 gathers the 256 column sums, solves and broadcasts the new affine (two
-// hops per iteration).  SCHED 1: every workgroup gathers the 256 column sums and runs the
-// (deterministic, bit-identical) tail itself -- one hop per iteration, no broadcast.
-// SCHED 2 (hierarchical): workgroup x < 8 gathers the 32 columns of residue class x (the
-// workgroups dispatched round-robin onto its own XCD), runs the first five tree steps on them
-// (ip_residue_tree) and publishes 27 partials; workgroup 0 gathers the 8 x 27 partials, runs
-// the last three steps and the tail, and broadcasts.  Two small gathers instead of one 55 KB
-// one, and the serial tree in the tail shrinks to 3 steps.  SCHED 3: as 2, but every
-// workgroup gathers the partials and runs the tail itself (no broadcast hop).
-template <int SCHED>
+// Per iteration (hierarchical gather, no broadcast): every workgroup publishes its 27 column
+// sums; workgroup x < 8 gathers the 32 columns of residue class x (the workgroups dispatched
+// round-robin onto its own XCD), runs the first five steps of the final tree on them
+// (ip_residue_tree) and publishes 27 partials; every workgroup then gathers the 8 x 27
+// partials, runs the last three tree steps and the solve / Rodrigues / compose itself,
+// redundantly and bit-identically -- two small hops per iteration, no broadcast.  The det check
+// of iteration k (cv::determinant, projective_icp.cpp:197-203) runs on wave IP_DETW while
+// iteration k+1 computes its rows and is settled before anything of k+1 is published: on
+// failure the affine of k-1 is restored and the loop ends exactly where the serial order ends
+// it.  The solve (wave 0) is the only serial work between two iterations.
 __global__ void __launch_bounds__(64 * IP_WAVES)
 k_icp_frame(IcpFrameArgs a)
 {
-    constexpr bool ALLGATHER = SCHED == 1;
     __shared__ float red[ICP_MAX_SLOTS][ICP_T_STRIDE];
-    __shared__ float tl[27][33];                // SCHED 2: a residue class's 32 columns (+1 pad)
-    __shared__ float tv[27][ICP_NWG + 1];   // +1: the gather's (col, q) stores hit distinct banks
+    __shared__ float tl[27][33];                // a residue class's 32 columns (+1 pad)
+    __shared__ float tv[27][IP_NPART + 1];      // the 8 residue-class partials per sum
     __shared__ float aff_s[12];
-    __shared__ int status_s, det_ok_s;
+    __shared__ int det_ok_s;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, wg = blockIdx.x;
     TfDevState* st = a.st;
     unsigned long long* tag = a.tag;
@@ -686,10 +684,6 @@ k_icp_frame(IcpFrameArgs a)
     for (int i = 0; i < 12; ++i) aff[i] = (i % 5 == 0) ? 1.0f : 0.0f;     // affine = Identity
     int status = 1, done = 0;
     float last_sums = 0.f;
-    // SCHED 3 runs the det check (projective_icp.cpp:197-203) of iteration k on wave IP_DETW
-    // while iteration k+1 computes its rows, and settles it before anything of k+1 is
-    // published: on failure the affine of k-1 is restored and the loop ends exactly where the
-    // serial order ends it.  The solve (wave 0) is the only serial work between two iterations.
     float aff_prev[12], det_sm[27];
     bool det_pending = false;
 
@@ -727,7 +721,7 @@ k_icp_frame(IcpFrameArgs a)
         for (int it = 0; it < iters; ++it) {
             ++gen;
             IPT_REC(done, wg);
-            if (SCHED == 3 && det_pending && wave == IP_DETW) {
+            if (det_pending && wave == IP_DETW) {
                 float Am[6][6], bv[6];
                 ip_unpack(det_sm, Am, bv);
                 const double det = icp_det6_reg(Am);
@@ -770,7 +764,7 @@ k_icp_frame(IcpFrameArgs a)
                 if (!(lane & 1) && (lane >> 1) < 27) red[sl][lane >> 1] = tot;
             }
             __syncthreads();
-            if (SCHED == 3 && det_pending) {                      // settle iteration k's det check
+            if (det_pending) {                                    // settle iteration k's det check
                 det_pending = false;
                 if (!det_ok_s) {
                     status = 0;
@@ -788,7 +782,7 @@ k_icp_frame(IcpFrameArgs a)
                 ip_store(&tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE + wg * ICP_T_STRIDE + tid], ip_pack(gen, sum));
             }
             IPT_REC(done, ICP_NWG + wg);
-            if (SCHED >= 2 && wg < IP_NPART) {
+            if (wg < IP_NPART) {
                 // ---- residue-class leader: gather columns wg + 8k, partial tree, publish
                 constexpr int PER = (32 * 27 + 64 * IP_WAVES - 1) / (64 * IP_WAVES);
                 const unsigned long long* cols = &tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE];
@@ -826,9 +820,9 @@ k_icp_frame(IcpFrameArgs a)
                     ip_store(&tag[IP_PART + (gen & 1) * IP_NPART * ICP_T_STRIDE + wg * ICP_T_STRIDE + tid],
                              ip_pack(gen, ip_residue_tree(tl[tid])));
             }
-            if ((SCHED == 2 && wg == 0) || SCHED == 3) {
+            {
                 // ---- gather the 8 x 27 partials, last three tree steps, det / solve / compose
-                // (SCHED 3: every workgroup, redundantly and bit-identically -- no broadcast hop)
+                // (every workgroup, redundantly and bit-identically -- no broadcast hop)
                 const unsigned long long* parts = &tag[IP_PART + (gen & 1) * IP_NPART * ICP_T_STRIDE];
                 bool timeout = false;
                 if (tid < IP_NPART * 27) {
@@ -841,10 +835,9 @@ k_icp_frame(IcpFrameArgs a)
                     }
                     tv[q][x] = __uint_as_float((unsigned)v);
                 }
-                if (SCHED == 2 && tid == 0) det_ok_s = 1;
                 const int any_timeout = __syncthreads_or(timeout);
                 IPT_REC(done, 2 * ICP_NWG + 0);
-                if (!any_timeout && (SCHED == 3 ? (wave == 0 || wave == IP_DETW) : wave < 2)) {
+                if (!any_timeout && (wave == 0 || wave == IP_DETW)) {
                     // steps 4, 2, 1: ((P0+P4) + (P2+P6)) + ((P1+P5) + (P3+P7)); lane q holds sum q
                     float tot = 0.f;
                     if (lane < 27) {
@@ -857,13 +850,9 @@ k_icp_frame(IcpFrameArgs a)
                         sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), q));
                     ip_unpack(sm, Am, bv);
                     IPT_REC(done, 2 * ICP_NWG + 2);
-                    if (SCHED == 3 && wave == IP_DETW) {               // det after the barrier
+                    if (wave == IP_DETW) {                             // det after the barrier
 #pragma unroll
                         for (int q = 0; q < 27; ++q) det_sm[q] = sm[q];
-                    } else if (SCHED == 2 && wave == 1) {              // det on its own wave
-                        const double det = icp_det6_reg(Am);           // projective_icp.cpp:197-203
-                        if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
-                        IPT_REC_T(done, 2 * ICP_NWG + 5, 64);
                     } else {                                           // solve -> Rodrigues -> compose
                         float rv[6], R[9], tinc[12];
                         icp_solve6_ldl(Am, bv, rv);                     // projective_icp.cpp:206-209
@@ -885,123 +874,10 @@ k_icp_frame(IcpFrameArgs a)
                 }
                 __syncthreads();
                 IPT_REC(done, 2 * ICP_NWG + 1);
-                if (SCHED == 3) {
-                    status = any_timeout ? 2 : 1;
-                    det_pending = !any_timeout;
+                status = any_timeout ? 2 : 1;
+                det_pending = !any_timeout;
 #pragma unroll
-                    for (int i = 0; i < 12; ++i) aff_prev[i] = aff[i];
-                } else {
-                    status = any_timeout ? 2 : (det_ok_s ? 1 : 0);
-                }
-                if (SCHED == 2 && wave == 0 && lane <= 12) {           // broadcast affine + status
-                    const float v = lane < 12 ? aff_s[lane] : (float)status;
-                    ip_store(&tag[IP_BCAST + lane], ip_pack(gen, v));
-                }
-                if (status == 1) {
-#pragma unroll
-                    for (int i = 0; i < 12; ++i) aff[i] = aff_s[i];
-                }
-            } else if (SCHED < 2 && (ALLGATHER || wg == 0)) {
-                // ---- gather the 256 column sums (tagged polling; all loads in flight at once)
-                constexpr int PER = (ICP_NWG * 27 + 64 * IP_WAVES - 1) / (64 * IP_WAVES);
-                unsigned long long v[PER];
-#pragma unroll
-                for (int k = 0; k < PER; ++k) {
-                    const int e = tid + 64 * IP_WAVES * k;
-                    const int col = e / 27, q = e - col * 27;
-                    v[k] = e < ICP_NWG * 27 ? ip_load(&tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE + col * ICP_T_STRIDE + q]) : ((unsigned long long)gen << 32);
-                }
-                bool timeout = false;
-                for (unsigned spins = 0;; ++spins) {
-                    bool ready = true;
-#pragma unroll
-                    for (int k = 0; k < PER; ++k) {
-                        if ((unsigned)(v[k] >> 32) != gen) {
-                            ready = false;
-                            const int e = tid + 64 * IP_WAVES * k;
-                            const int col = e / 27, q = e - col * 27;
-                            v[k] = ip_load(&tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE + col * ICP_T_STRIDE + q]);
-                        }
-                    }
-                    if (ready) break;
-                    if (spins > IP_SPIN_LIMIT) { timeout = true; break; }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-#pragma unroll
-                for (int k = 0; k < PER; ++k) {
-                    const int e = tid + 64 * IP_WAVES * k;
-                    const int col = e / 27, q = e - col * 27;
-                    if (e < ICP_NWG * 27) tv[q][col] = __uint_as_float((unsigned)v[k]);
-                }
-                if (tid == 0) det_ok_s = 1;
-                const int any_timeout = __syncthreads_or(timeout);
-                IPT_REC(done, 2 * ICP_NWG + 0);
-                if (!any_timeout) {
-                    if (wave == 1) {                                   // det on its own wave
-                        float sm[27], Am[6][6], bv[6];
-                        ip_final_tree(tv, lane, sm);
-                        ip_unpack(sm, Am, bv);
-                        const double det = icp_det6_reg(Am);           // projective_icp.cpp:197-203
-                        if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
-                        IPT_REC_T(done, 2 * ICP_NWG + 5, 64);
-                    } else if (wave == 0) {                            // solve -> Rodrigues -> compose
-                        float sm[27], Am[6][6], bv[6], rv[6], R[9], tinc[12];
-                        ip_final_tree(tv, lane, sm);
-                        ip_unpack(sm, Am, bv);
-                        IPT_REC(done, 2 * ICP_NWG + 2);
-                        icp_solve6_ldl(Am, bv, rv);                     // projective_icp.cpp:206-209
-                        IPT_REC(done, 2 * ICP_NWG + 3);
-                        icp_rodrigues(rv, R);
-#pragma unroll
-                        for (int j = 0; j < 3; ++j) {
-                            tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1];
-                            tinc[j * 4 + 2] = R[j * 3 + 2]; tinc[j * 4 + 3] = rv[3 + j];
-                        }
-                        float A[12];
-#pragma unroll
-                        for (int i = 0; i < 12; ++i) A[i] = aff[i];
-                        tf_rigid_mul(tinc, A, A);
-                        if (lane < 12) aff_s[lane] = A[lane];
-                        IPT_REC(done, 2 * ICP_NWG + 4);
-                        float mine = 0.f;
-#pragma unroll
-                        for (int q = 0; q < 27; ++q) if (lane == q) mine = sm[q];
-                        last_sums = mine;
-                    }
-                    __syncthreads();
-                }
-                IPT_REC(done, 2 * ICP_NWG + 1);
-                status = any_timeout ? 2 : (det_ok_s ? 1 : 0);
-                if (!ALLGATHER && wave == 0 && lane <= 12) {            // broadcast affine + status
-                    const float v = lane < 12 ? aff_s[lane] : (float)status;
-                    ip_store(&tag[IP_BCAST + lane], ip_pack(gen, v));
-                }
-                if (status == 1) {
-#pragma unroll
-                    for (int i = 0; i < 12; ++i) aff[i] = aff_s[i];
-                }
-            } else {
-                // ---- wait for workgroup 0's broadcast
-                if (wave == 0) {
-                    unsigned long long v = 0;
-                    bool mine_ok = true;
-                    if (lane <= 12) {
-                        unsigned spins = 0;
-                        v = ip_load(&tag[IP_BCAST + lane]);
-                        while ((unsigned)(v >> 32) != gen) {
-                            if (++spins > IP_SPIN_LIMIT) { mine_ok = false; break; }
-                            __builtin_amdgcn_s_sleep(1);
-                            v = ip_load(&tag[IP_BCAST + lane]);
-                        }
-                        if (lane < 12) aff_s[lane] = __uint_as_float((unsigned)v);
-                        if (lane == 12) status_s = mine_ok ? (int)__uint_as_float((unsigned)v) : 2;
-                    }
-                    const bool all_ok = __all(mine_ok);
-                    if (lane == 0 && !all_ok) status_s = 2;
-                }
-                __syncthreads();
-
-                status = status_s;
+                for (int i = 0; i < 12; ++i) aff_prev[i] = aff[i];
                 if (status == 1) {
 #pragma unroll
                     for (int i = 0; i < 12; ++i) aff[i] = aff_s[i];
@@ -1012,7 +888,7 @@ k_icp_frame(IcpFrameArgs a)
             __syncthreads();                       // red[] / aff_s reuse in the next iteration
         }
     }
-    if (SCHED == 3 && det_pending) {                              // the last iteration's det check
+    if (det_pending) {                                            // the last iteration's det check
         if (wave == IP_DETW) {
             float Am[6][6], bv[6];
             ip_unpack(det_sm, Am, bv);
@@ -1117,7 +993,7 @@ static int icp_used_levels(const tf_params& p)
 int tfk_icp_persistent_ok(tf_ctx* c)
 {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame<2>, 64 * IP_WAVES, IP_LDS_PAD) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame, 64 * IP_WAVES, IP_LDS_PAD) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) return 0;
     if (per_cu * cus < ICP_NWG) return 0;
     for (int l = 0; l < TF_LEVELS; ++l) {
@@ -1148,7 +1024,7 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
         a.frame_begin = frame_begin;
         a.st = c->st;
         a.tag = c->icp_tagged;
-        if (fold_t3 && c->icp_sched == 3 && pose_update && frame_begin) {
+        if (fold_t3 && pose_update && frame_begin) {
             a.fold_t3 = 1;
             a.vis.fx = c->p.fx; a.vis.fy = c->p.fy; a.vis.cx = c->p.cx; a.vis.cy = c->p.cy;
             a.vis.factor = (float)TF_BLK * c->p.voxelSize;
@@ -1158,14 +1034,7 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
         }
         // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
         // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up
-        if (c->icp_sched == 3)
-            hipLaunchKernelGGL(k_icp_frame<3>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
-        else if (c->icp_sched == 1)
-            hipLaunchKernelGGL(k_icp_frame<1>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
-        else if (c->icp_sched == 0)
-            hipLaunchKernelGGL(k_icp_frame<0>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
-        else
-            hipLaunchKernelGGL(k_icp_frame<2>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
+        hipLaunchKernelGGL(k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, c->stream, c->st, frame_begin);

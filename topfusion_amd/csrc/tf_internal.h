@@ -19,8 +19,8 @@
 #define TF_RB_SIZE 16           // renderingBlockSizeX/Y (VisualisationEngine_Shared.hpp:25-26)
 #define TF_LEVELS 3
 #define TF_NUM_STAGES 9     // tf_stage_id in include/tfusion_hip.h
-#define TF_PROF_RING 32
-#define TF_ICP_TAG_WORDS (2 * 256 * 28 + 16 + 2 * 8 * 28)   // persistent ICP tagged granules (tf_icp.hip)     // frames enqueued between host syncs (and timing-event ring slots)
+#define TF_PROF_RING 32     // frames enqueued between host syncs (and timing-event ring slots)
+#define TF_ICP_TAG_WORDS (2 * 256 * 28 + 16 + 2 * 8 * 28)   // persistent ICP tagged granules (tf_icp.hip)
 
 // HashEntry, VoxelBlockHash.hpp:32-44 (16 B; one dwordx4 probe)
 struct __attribute__((aligned(16))) TfHashEntry {
@@ -64,13 +64,17 @@ struct TfDevState {
     unsigned reset_ticket;   // k_reset_scene: workgroups done (the last one resets the counters)
     int range_full;          // CreateExpectedDepths must initialise the whole range buffer (creation, upload)
     unsigned alloc_ticket;   // k_alloc_apply under exhaustion: workgroups done (the last one allocates)
-    int pad2_[2];
-    // renderImage of the frame runs on the context's render stream, overlapping the rest of
-    // the frame and the next frame's preprocessing/ICP; it reads only this snapshot (taken on
-    // the main stream once the previous render has finished: render_snapshot)
+    int scene_external;      // scene buffers / counters set from the host since the last full reset:
+                             // the next reset (in-frame ones too) clears everything, then drops it
+    int pad2_;
+    // the frame's renderImage runs in k_raycast_pair after CreateExpectedDepths has rewritten the
+    // range image; it reads the raycast matrix, go flag and range region snapshotted before
+    // (render_snapshot / icp_fold_t3)
     float M_render[16];      // M_ray of the frame being rendered
     int render_go;           // the frame took the tracking path (mode 1, ICP ok)
     int pad3_[3];
+    // totals since creation / tf_reset_totals, accumulated by the frame end (tf_totals)
+    long long tot_frames, tot_tracked, tot_resets, tot_visible, tot_tiles, tot_pad_;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -214,8 +218,8 @@ __device__ __forceinline__ float tf_wave_tree64(float b)
     return b;
 }
 
-// Main stream, after the previous frame's renderImage has finished and this frame's ICP has
-// set the pose (folded into the allocation pass's first kernel): snapshot what the frame's
+// After this frame's ICP has set the pose (k_set_type3, or the persistent ICP's tail):
+// snapshot what the frame's
 // renderImage reads and later stages of this frame or the next overwrite -- the raycast
 // matrix, the go flag, and the /8 region castRay reads of the range image
 // (range[x/8 + (y/8)*W], VisualisationEngine_Shared.hpp:104-106) that CreateExpectedDepths
@@ -239,11 +243,6 @@ struct tf_ctx {
     tf_params p;
     int device;
     hipStream_t stream;
-    hipStream_t rstream;     // renderImage stream (tf_capi.hip: enqueue_frame)
-    hipEvent_t ev_integrated, ev_rendered;
-    int render_mode;         // renderImage: 0 render stream behind integration, 1 render stream
-                             // behind the frame's tail (overlaps the next ICP), 2 inline on the main
-                             // stream, 3 fused with CreateICPMaps' raycast in one launch (default)
     int n_total;
     int W, H;
     int lw[TF_LEVELS], lh[TF_LEVELS];
@@ -251,8 +250,7 @@ struct tf_ctx {
     TfHashEntry* hash;
     int* excessList;
     TfVoxel* vba;
-    int scene_external;      // scene buffers / counters set from the host since the last full reset
-    int mu_exact3;           // eta / mu by tf_div_exact3 (checked on the device at tf_create)
+    int mu_exact3;          // eta / mu by tf_div_exact3 (checked on the device at tf_create)
     TfVoxel* vba_guard;      // allocation: one guard block of Voxel_s() (TF_VOFF_NONE reads), then vba
     int* allocList;
     int2* bgrid;             // block grid (TF_GRID_*), mirrors the hash
@@ -262,7 +260,6 @@ struct tf_ctx {
     int* allocCounts;        // per-chunk counts (2 ints per chunk)
     int* requestList;        // ordered request indices
     int* visCounts;
-    unsigned long long* visFlags;   // k_vis_scan look-back words (epoch | flag | prefix), one per chunk
     // RenderState_VH
     int* visibleIds;
     unsigned char* visType;
@@ -290,7 +287,6 @@ struct tf_ctx {
     unsigned* icp_ticket;    // last-workgroup ticket (zero between launches)
     unsigned long long* icp_tagged;   // persistent ICP: [256][28] tagged column sums + [16] broadcast
     int icp_persistent;      // 1: one launch per frame (k_icp_frame), 0: one launch per iteration
-    int icp_sched;           // persistent ICP: 0 WG0 gathers 256 columns, 1 allgather, 2 hierarchical, 3 hierarchical allgather (default)
     int icp_max_cta;
     float min_cosine, dist2_thres;
     // device state
@@ -300,12 +296,6 @@ struct tf_ctx {
     int n_resets;            // host mirror of st->n_resets
     int* frame_ok;           // per enqueued frame of a batch: 1 ok, 0 ICP failure (reset), -1 error
     int* frame_mode;         // per enqueued frame of a batch: st->mode it ran with
-    int vis_scan;            // visible-list compaction as one look-back scan launch (TFUSION_VIS_SCAN, 0)
-    unsigned vis_epoch;      // k_vis_scan launches enqueued (the look-back words' tag)
-    int fold_t3;             // setToType3 + renderImage snapshot in the ICP grid's tail (TFUSION_FOLD_T3, 1)
-    int fuse_end;            // frame end in k_icp_maps' grid, render modes 2-3 (TFUSION_FUSE_END, 1)
-    int fuse_ed;             // CreateExpectedDepths' projection pass inside k_integrate's grid (TFUSION_FUSE_ED, 1)
-    int lookahead;           // batches: later frames' preprocessing in this frame's grid tails (0 off, 1 next frame, 2 two frames)
     int alloc_chunks;        // N_tot / 4096
     int vis_chunks;
     // per-stage HIP-event timing on the context stream (tf_profile_*)
@@ -324,8 +314,8 @@ struct tf_ctx {
 // launchers (one per kernel family); all enqueue on ctx->stream
 // ---------------------------------------------------------------------------------------
 hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStream_t strm, uint16_t* d0);   // no st access
-// fold_t3: k_set_type3's work in the persistent SCHED-3 ICP grid's tail (frame path; the
-// caller then passes snapshot = 2 to tfk_alloc)
+// fold_t3: k_set_type3's work in the persistent ICP grid's tail (frame path; the caller then
+// passes snapshot = 2 to tfk_alloc)
 hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin = 0, int fold_t3 = 0);   // frame_begin: frame path (tf_frame_begin)
 int tfk_icp_persistent_ok(tf_ctx* c);      // k_icp_frame fits (co-residency, slot count)
 hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / raycast matrices
@@ -346,11 +336,11 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0,       // snapshot: + the frame
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0, int with_ed = 0);
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_type(tf_ctx* c, int type);   // RenderImage pixel stage (tf_render_type) on raycast
-hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm);
 // CreateICPMaps raycast + renderImage, one launch (frame path); next: + that frame's dists/pyramid/normals
 hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = TfAhead{}, size_t pitch = 0);   // + dists/pyramid/normals of pyr, bilateral of bil
 hipError_t tfk_icp_maps(tf_ctx* c);
-// CreateICPMaps + the frame end (tfk_reset_scene_on_failure) in one grid (tf_ctx::fuse_end)
+hipError_t tfk_render_snapshot(tf_ctx* c);   // render_snapshot as its own launch
+// CreateICPMaps + the frame end (tfk_reset_scene_on_failure) in one grid (the frame path)
 hipError_t tfk_icp_maps_end(tf_ctx* c, int slot);
 #define TF_END_BLOCKS 256        // workgroups of the frame-end / in-frame reset pass
 hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0);

@@ -105,8 +105,9 @@ __device__ __forceinline__ void blk_find8(const SceneView& s, const int (&X)[2],
 
 // raw Voxel_s word (sdf = low 16 bits, w = bits 16-23) of voxel `lin` of the block at VBA offset
 // voff, read relative to the guard block before the VBA (SceneView::vba): a missing block
-// (voff = TF_VOFF_NONE) reads the guard's Voxel_s() = (32767, 0).  Byte offsets fit 32 bits
-// (<= 2^21 blocks x 2 KiB).
+// (voff = TF_VOFF_NONE) reads the guard's Voxel_s() = (32767, 0).  Byte offsets fit 32 bits:
+// the largest is 4 * (ptr*512 + 512 + 511) for ptr = n_blocks - 1, below 2^32 because tf_create
+// accepts at most 2^21 - 1 blocks (the guard block is the 2^21-th 2 KiB block of the range).
 __device__ __forceinline__ unsigned vox_at(const SceneView& s, int voff, int lin_g)
 {
     return ld_off<unsigned>(s.vba, (unsigned)(voff + lin_g) * 4u);
@@ -542,13 +543,12 @@ static void ray_args(tf_ctx* c, RayArgs& a)
     a.oneOverVoxelSize = 1.0f / c->p.voxelSize; a.mu = c->p.mu;
 }
 
-static hipError_t launch_ray(tf_ctx* c, const RayArgs& a, int mode, hipStream_t strm = nullptr)
+static hipError_t launch_ray(tf_ctx* c, const RayArgs& a, int mode)
 {
     const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty;
     const dim3 grid((n + 7) / 8 * 8);
     if (mode == 0) hipLaunchKernelGGL(k_raycast<0>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
-    else if (mode == 1) hipLaunchKernelGGL(k_raycast<1>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
-    else hipLaunchKernelGGL(k_raycast<2>, grid, dim3(256), 0, strm, a, c->st, tx, n);
+    else hipLaunchKernelGGL(k_raycast<1>, grid, dim3(256), 0, c->stream, a, c->st, tx, n);
     return hipGetLastError();
 }
 
@@ -560,11 +560,21 @@ hipError_t tfk_raycast(tf_ctx* c, int update_visible)
     return launch_ray(c, a, update_visible ? 1 : 0);
 }
 
-// renderImage in the frame path: castRay<false> + renderGrey fused (the intermediate point
-// image is overwritten by CreateICPMaps before anything can observe it).  It is enqueued on
-// the render stream behind the frame's integration and reads the range-image snapshot.
-// CreateICPMaps' raycast + the frame's renderImage in one launch (main stream, after
-// CreateExpectedDepths)
+// the renderImage snapshot outside a frame (measurement: tf_time_stage of the raycast pair)
+__global__ void k_render_snapshot(TfDevState* st, const float2* range, float2* snap, int W, int H)
+{
+    render_snapshot(st, range, snap, W, H);
+}
+
+hipError_t tfk_render_snapshot(tf_ctx* c)
+{
+    hipLaunchKernelGGL(k_render_snapshot, dim3(64), dim3(256), 0, c->stream, c->st, (const float2*)c->range,
+                       (float2*)c->range_render, c->W, c->H);
+    return hipGetLastError();
+}
+
+// CreateICPMaps' raycast + the frame's renderImage in one launch (after CreateExpectedDepths):
+// the renderImage half reads the range-image snapshot (render_snapshot)
 hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch)
 {
     RayArgs ai, ar;
@@ -593,16 +603,6 @@ hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch)
                        pp, n_pyr, pyr_gx, bb, bil_gx);
     return hipGetLastError();
 }
-
-hipError_t tfk_raycast_grey(tf_ctx* c, hipStream_t strm)
-{
-    RayArgs a;
-    ray_args(c, a);
-    a.range = (const float2*)c->range_render;
-    a.grey = c->grey;
-    return launch_ray(c, a, 2, strm);
-}
-
 
 
 // ---------------------------------------------------------------------------------------
@@ -973,7 +973,7 @@ void tf_ed_args(tf_ctx* c, EdArgs* out)
     a.cap = (unsigned)c->p.max_render_blocks;
 }
 
-// project_done: k_ed_project's pass already ran in the frame's k_integrate grid (tf_ctx::fuse_ed)
+// project_done: k_ed_project's pass already ran in the frame's k_integrate grid (frame path)
 hipError_t tfk_expected_depths(tf_ctx* c, int project_done)
 {
     EdArgs a;

@@ -22,7 +22,9 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
     TfVoxel* vba = r.vba; const size_t n_vox = r.n_vox; int* allocList = r.allocList; const int n_blocks = r.n_blocks;
     TfHashEntry* hash = r.hash; const int n_total = r.n_total; int* excessList = r.excessList;
     const int n_excess = r.n_excess; TfDevState* st = r.st; int2* grid = r.grid; const int on_failure = r.on_failure;
-    const int full = r.full;
+    // a full clear when forced (ResetScene entry point) or when the host wrote scene state since
+    // the last full reset (tf_upload / tf_set_counters); the last workgroup drops that flag
+    const int full = r.full || st->scene_external;
     if (on_failure && bid == 0 && threadIdx.x == 0) {
         // end of the device-driven frame (return values of topfu.cpp:209 / 264 / 329); only
         // frame_counter / n_resets / pose change here, never the mode / icp_ok read below
@@ -36,6 +38,10 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
             for (int i = 0; i < 12; ++i) st->pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
             ok = 0;
         } else { st->frame_counter++; ok = 1; }
+        st->tot_frames++;
+        if (ok == 0) st->tot_resets++;
+        if (ok == 1) st->tot_visible += st->noVisibleEntries;      // the list this frame integrated
+        if (ok == 1 && mode == 1) { st->tot_tracked++; st->tot_tiles += st->noTotalBlocks; }
         r.frame_ok[r.slot] = ok;
         r.frame_mode[r.slot] = mode;
     }
@@ -96,6 +102,7 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
     __syncthreads();
     if (last_s && threadIdx.x == 0) {
         st->reset_ticket = 0;
+        st->scene_external = 0;
         st->lastFreeBlockId = n_blocks - 1;
         st->lastFreeExcessListId = n_excess - 1;
     }

@@ -49,7 +49,7 @@ void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot)
     r->on_failure = on_failure;
     r->frame_ok = on_failure ? c->frame_ok : nullptr; r->frame_mode = on_failure ? c->frame_mode : nullptr;
     r->slot = on_failure ? slot : 0;
-    r->full = on_failure ? c->scene_external : 1;
+    r->full = on_failure ? 0 : 1;       // (+ st->scene_external, read on the device)
 }
 
 hipError_t tfk_reset_scene(tf_ctx* c)
@@ -57,9 +57,7 @@ hipError_t tfk_reset_scene(tf_ctx* c)
     ResetArgs r;
     tf_reset_args(c, &r, 0, 0);
     hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, r);
-    const hipError_t e = hipGetLastError();
-    if (e == hipSuccess) c->scene_external = 0;
-    return e;
+    return hipGetLastError();
 }
 
 // the frame's end (every frame; the reset part only when ICP failed): one workgroup per CU, so
@@ -539,106 +537,6 @@ k_vis_apply(VisArgs v, TfDevState* __restrict__ st, int n_chunks, const int* __r
     }
 }
 
-// buildVisibleList's compaction in ONE launch (k_vis_count + k_vis_apply's work): a
-// decoupled look-back scan over the 4096-entry chunks.  Chunk b publishes its count (flag 1)
-// and, once its exclusive prefix is known, its inclusive prefix (flag 2) in a 64-bit word
-// tagged with the launch's epoch (no per-frame clearing); wave 0 of each workgroup reads 64
-// predecessors at a time, newest first, and stops at the nearest inclusive one.  Workgroups
-// are dispatched in index order, so every predecessor a workgroup waits on is resident; the
-// spins are bounded (a timeout reports a lost peer: icp_ok = -1 -> TF_HIP_ERROR).
-#define VIS_SPIN_LIMIT (1u << 21)
-__device__ __forceinline__ unsigned long long vis_pack(unsigned epoch, unsigned flag, unsigned v)
-{
-    return ((unsigned long long)epoch << 32) | ((unsigned long long)flag << 30) | v;
-}
-
-__global__ void __launch_bounds__(256)
-k_vis_scan(VisArgs v, TfDevState* __restrict__ st, int n_chunks, unsigned char* __restrict__ visType,
-           int* __restrict__ allocCounts, unsigned long long* __restrict__ flags, unsigned epoch,
-           int* __restrict__ visibleIds)
-{
-    if (st->abort) return;
-    const int b = blockIdx.x;
-    if (threadIdx.x == 0) {   // (k_vis_count) the allocation counters of this frame
-        allocCounts[2 * b] = 0;
-        allocCounts[2 * b + 1] = 0;
-        if (b == 0 && !st->alloc_exhausted) {
-            st->lastFreeBlockId -= st->pad_[0];
-            st->lastFreeExcessListId -= st->pad_[1];
-        }
-    }
-    const int base = b * CHUNK + threadIdx.x * 16;
-    unsigned long long lo = 0, hi = 0;
-    int cnt = 0;
-    if (base < v.n_total) {
-        load16(visType + base, &lo, &hi);
-        bool dirty = false;
-        for (int i = 0; i < 16; ++i) {
-            unsigned t = byte16(lo, hi, i);
-            if (t == 4) {              // type 3 that failed checkBlockVisibility (k_set_type3)
-                if (i < 8) lo &= ~(0xffull << (8 * i)); else hi &= ~(0xffull << (8 * (i - 8)));
-                t = 0;
-                dirty = true;
-            }
-            cnt += t > 0;
-        }
-        if (dirty) *(uint4*)(visType + base) = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
-    }
-    int tot;
-    const int lex = block_excl_scan(cnt, &tot);
-    __shared__ int excl_s;
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        int excl = 0;
-        if (b == 0) {
-            if (lane == 0) __hip_atomic_store(&flags[0], vis_pack(epoch, 2, (unsigned)tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(&flags[b], vis_pack(epoch, 1, (unsigned)tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int j0 = b - 1;
-            bool timeout = false;
-            for (unsigned spins = 0;;) {
-                const int j = j0 - lane;
-                const unsigned long long w = j >= 0 ? __hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                    : vis_pack(epoch, 2, 0);
-                const unsigned flag = (unsigned)(w >> 30) & 3u;
-                const bool ready = (unsigned)(w >> 32) == epoch && flag != 0;
-                const unsigned long long incl = __ballot(ready && flag == 2);
-                const unsigned long long notready = __ballot(!ready);
-                const int p = incl ? __ffsll((long long)incl) - 1 : 63;     // nearest inclusive predecessor
-                const unsigned long long need = p == 63 ? ~0ull : ((2ull << p) - 1);
-                if (!(notready & need)) {
-                    int val = lane <= p ? (int)(w & 0x3fffffffull) : 0;
-#pragma unroll
-                    for (int o = 32; o > 0; o >>= 1) val += __shfl_xor(val, o, 64);
-                    excl += val;
-                    if (incl) break;
-                    j0 -= 64;
-                    continue;
-                }
-                if (++spins > VIS_SPIN_LIMIT) { timeout = true; break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (lane == 0) {
-                if (timeout) st->icp_ok = -1;
-                __hip_atomic_store(&flags[b], vis_pack(epoch, 2, (unsigned)(excl + tot)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (lane == 0) {
-            excl_s = excl;
-            if (b == n_chunks - 1) st->noVisibleEntries = excl + tot < v.cap ? excl + tot : v.cap;
-        }
-    }
-    __syncthreads();
-    if (!cnt) return;
-    int r = excl_s + lex;
-    for (int i = 0; i < 16; ++i) {
-        if (byte16(lo, hi, i) > 0) {
-            if (r < v.cap) visibleIds[r] = base + i;
-            r++;
-        }
-    }
-}
-
 static AllocArgs make_alloc_args(tf_ctx* c)
 {
     AllocArgs a;
@@ -679,11 +577,6 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch)
     hipLaunchKernelGGL(k_alloc_apply, dim3(c->alloc_chunks), dim3(256), 0, c->stream, a, c->st, c->alloc_chunks,
                        c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
                        c->requestList, c->n_total);
-    if (c->vis_scan) {
-        hipLaunchKernelGGL(k_vis_scan, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks, c->visType,
-                           c->allocCounts, c->visFlags, ++c->vis_epoch, c->visibleIds);
-        return hipGetLastError();
-    }
     hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
                        c->visCounts, c->allocCounts);
     hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,

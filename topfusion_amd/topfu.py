@@ -118,6 +118,15 @@ class TopFu:
         L.check(L.load().tf_get_stats(self._h, ctypes.byref(s)), "tf_get_stats")
         return s.as_dict()
 
+    def totals(self):
+        """Frame totals accumulated on the device since creation / reset_totals() (tf_totals)."""
+        t = L.TfTotals()
+        L.check(L.load().tf_get_totals(self._h, ctypes.byref(t)), "tf_get_totals")
+        return t.as_dict()
+
+    def reset_totals(self):
+        L.check(L.load().tf_reset_totals(self._h), "tf_reset_totals")
+
     def stream(self):
         return L.load().tf_get_stream(self._h)
 
