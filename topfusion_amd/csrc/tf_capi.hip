@@ -225,7 +225,6 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     memset(&s0, 0, sizeof(s0));
     for (int i = 0; i < 12; ++i) s0.pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
     s0.icp_ok = 1;
-    s0.range_full = 1;
     e = hipMemcpyAsync(c->st, &s0, sizeof(s0), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_ticket, 0, 64, c->stream);
     if (e == hipSuccess) e = tfk_grid_clear(c);
@@ -322,7 +321,9 @@ static hipEvent_t prof_event(tf_ctx* c, int slot, int k)
 static bool stage_ran(int stage, int mode, int ok)
 {
     if (stage == TF_STAGE_PREPROCESS) return true;
-    if (stage == TF_STAGE_ICP) return mode == 1;
+    // ICP: only frames whose estimateTransform ran all its iterations (a failed det check ends
+    // it early, and its launch would understate the per-launch time of the full 19 iterations)
+    if (stage == TF_STAGE_ICP) return mode == 1 && ok == 1;
     if (stage == TF_STAGE_ALLOC || stage == TF_STAGE_INTEGRATE) return mode == 0 || ok == 1;
     if (stage == TF_STAGE_GREY) return false;                      // fused into RAYCAST_RENDER
     return mode == 1 && ok == 1;
@@ -790,8 +791,6 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
     static const int one = 1;
     if (which == TF_BUF_HASH || which == TF_BUF_VBA)    // next reset (in-frame ones too): full clear
         TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, scene_external), &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
-    if (which == TF_BUF_RANGE)          // next CreateExpectedDepths initialises the whole buffer again
-        TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, range_full), &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }

@@ -27,19 +27,15 @@ __device__ __forceinline__ void ed_project_block(const EdArgs& a, const TfDevSta
 {
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int tid = bid * 256 + threadIdx.x, stride = nblk * 256;
-    if (st->range_full) {   // range image init, two pixels per 16-byte store
+    // memsetKernel(FAR_AWAY, VERY_CLOSE) over the whole buffer (VisualisationEngine_CUDA.cu:133),
+    // two pixels per 16-byte store.  The fill writes outside the /8 region castRay reads too
+    // (boxes are clamped to the full-resolution W-1 / H-1, VisualisationEngine_Shared.hpp:67-70),
+    // so anything less than the whole buffer leaves stale min/max values there.
+    {
         const int npx = a.W * a.H;
         float4* r4 = (float4*)a.range;
         for (int i = tid; i < (npx >> 1); i += stride) r4[i] = make_float4(TF_FAR_AWAY, TF_VERY_CLOSE, TF_FAR_AWAY, TF_VERY_CLOSE);
         if ((npx & 1) && tid == 0) a.range[npx - 1] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
-    } else {
-        // Only the /8 region (row stride W, the reference's indexing) is ever filled or read; the
-        // rest of the buffer keeps the constants its last full initialisation wrote
-        const int rc = (a.W - 1) / TF_SUBSAMPLE + 1, rr = (a.H - 1) / TF_SUBSAMPLE + 1;
-        for (int i = tid; i < rc * rr; i += stride) {
-            const int y = i / rc, x = i - y * rc;
-            a.range[x + y * a.W] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
-        }
     }
     __shared__ int wsum[4];
     const int n = st->noVisibleEntries;

@@ -62,7 +62,7 @@ struct TfDevState {
     int frame_counter;       // TopFu::frame_counter_
     int n_resets;            // resets taken after ICP failures
     unsigned reset_ticket;   // k_reset_scene: workgroups done (the last one resets the counters)
-    int range_full;          // CreateExpectedDepths must initialise the whole range buffer (creation, upload)
+    int pad4_;
     unsigned alloc_ticket;   // k_alloc_apply under exhaustion: workgroups done (the last one allocates)
     int scene_external;      // scene buffers / counters set from the host since the last full reset:
                              // the next reset (in-frame ones too) clears everything, then drops it

@@ -936,10 +936,7 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
     }
     const unsigned total = red[0];
     const bool capped = total > a.cap;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->noTotalBlocks = (int)(capped ? a.cap : total);
-        st->range_full = 0;                  // (k_ed_project has read it: the previous launch)
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->noTotalBlocks = (int)(capped ? a.cap : total);
     unsigned cprefix = 0;                    // tiles of chunks [0, cdone)
     int cdone = 0;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
