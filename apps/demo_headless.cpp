@@ -10,6 +10,8 @@
 #include <tfusion/io.hpp>
 #include <tfusion/topfu.hpp>
 
+#include "synth_depth.hpp"
+
 #include <cstring>
 #include <string>
 
@@ -20,40 +22,6 @@
 #include <vector>
 
 using namespace tfusion;
-
-// analytic room (+ sphere) seen from camera->world pose (R, t); uint16 millimetres
-static void render_depth(const double R[9], const double t[3], int cols, int rows, const Intr& in,
-                         std::vector<unsigned short>& out)
-{
-    out.assign((size_t)cols * rows, 0);
-    const int axes[6] = { 2, 1, 0, 0, 1, 2 };
-    const double offs[6] = { 1.8, 0.6, -0.8, 1.1, -0.9, -0.6 };
-    const double c[3] = { 0.15, 0.25, 1.3 }, r = 0.3;
-    for (int v = 0; v < rows; ++v)
-        for (int u = 0; u < cols; ++u) {
-            const double dc[3] = { (u - in.cx) / in.fx, (v - in.cy) / in.fy, 1.0 };
-            double dw[3];
-            for (int i = 0; i < 3; ++i) dw[i] = R[i * 3 + 0] * dc[0] + R[i * 3 + 1] * dc[1] + R[i * 3 + 2] * dc[2];
-            double best = std::numeric_limits<double>::infinity();
-            for (int p = 0; p < 6; ++p) {
-                const double tt = (offs[p] - t[axes[p]]) / dw[axes[p]];
-                if (tt > 1e-6 && tt < best) best = tt;
-            }
-            double oc[3] = { t[0] - c[0], t[1] - c[1], t[2] - c[2] };
-            const double b = dw[0] * oc[0] + dw[1] * oc[1] + dw[2] * oc[2];
-            const double a = dw[0] * dw[0] + dw[1] * dw[1] + dw[2] * dw[2];
-            const double cc = oc[0] * oc[0] + oc[1] * oc[1] + oc[2] * oc[2] - r * r;
-            const double disc = b * b - a * cc;
-            if (disc >= 0) {
-                const double t0 = (-b - std::sqrt(disc)) / a;
-                if (t0 > 1e-6 && t0 < best) best = t0;
-            }
-            if (std::isfinite(best)) {
-                const double mm = std::nearbyint(best * 1000.0);
-                out[(size_t)v * cols + u] = (unsigned short)(mm > 65535 ? 65535 : mm);
-            }
-        }
-}
 
 int main(int argc, char** argv)
 {
@@ -100,10 +68,9 @@ int main(int argc, char** argv)
             have_first = false;
             if (source.cols() != cols || source.rows() != rows) { std::fprintf(stderr, "frame size changed\n"); return 1; }
         } else {
-            const double ang = 0.25 * i * M_PI / 180.0, ca = std::cos(ang), sa = std::sin(ang);
-            const double R[9] = { ca, 0, sa, 0, 1, 0, -sa, 0, ca };
-            const double t[3] = { -sa * 1.2, 0.0, 1.2 - ca * 1.2 };     // orbit about a pivot 1.2 m ahead
-            render_depth(R, t, cols, rows, params.intr, depth);
+            double R[9], t[3];
+            tfusion_apps::orbit_pose(i, R, t);
+            tfusion_apps::render_depth(R, t, cols, rows, params.intr, depth);
         }
         ++n;
         depth_device.upload(depth.data(), (size_t)cols * 2, rows, cols);

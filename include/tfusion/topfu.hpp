@@ -3,7 +3,7 @@
 //
 // Drop-in for tfusion/include/tfusion/topfu.hpp:17-110 as used by apps/demo.cpp:27-38,100-115,
 // 141-168: TopFuParams::default_params, TopFu(params), operator()(Depth), renderImage(image4u&),
-// getCameraPose(time), reset(), params(); cuda::{setDevice, getCudaEnabledDeviceCount,
+// getCameraPose(time), reset(), params(), icp(); cuda::{setDevice, getCudaEnabledDeviceCount,
 // getDeviceName, checkIfPreFermiGPU, printShortCudaDeviceInfo, printCudaDeviceInfo}.
 // Behaviour mirrored from topfu.cpp: frame 0 integrates only; later frames track and return
 // false after an ICP failure, which resets the pipeline (poses_ back to {Identity},
@@ -12,6 +12,7 @@
 #pragma once
 #include "../tfusion_hip.h"
 #include "types.hpp"
+#include "cuda/projective_icp.hpp"
 
 #include <memory>
 
@@ -139,6 +140,11 @@ namespace tfusion
         {
             const tf_params c = params_.to_c();
             check(tf_create(&c, &ctx_), "tf_create");
+            // topfu.cpp:77-80: the tracker takes the TopFu's thresholds and iterations
+            icp_.bind(ctx_);
+            icp_.setDistThreshold(params_.icp_dist_thres);
+            icp_.setAngleThreshold(params_.icp_angle_thres);
+            icp_.setIterationsNum(params_.icp_iter_num);
             poses_.reserve(30000);
             poses_.push_back(Affine3f::Identity());
         }
@@ -148,6 +154,12 @@ namespace tfusion
 
         const TopFuParams& params() const { return params_; }
         TopFuParams& params() { return params_; }
+
+        // topfu.hpp:75-76: the frame tracker; its setters change the parameters the following
+        // frames use, and estimateTransform runs it on caller pyramids (through this context,
+        // whose current / previous maps it overwrites)
+        const cuda::ProjectiveICP& icp() const { return icp_; }
+        cuda::ProjectiveICP& icp() { return icp_; }
 
         void reset()                                  // topfu.cpp:141-152
         {
@@ -214,6 +226,7 @@ namespace tfusion
         }
         TopFuParams params_;
         tf_ctx* ctx_ = nullptr;
+        cuda::ProjectiveICP icp_;
         int frame_counter_ = 0;
         std::vector<Affine3f> poses_;
     };

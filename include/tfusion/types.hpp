@@ -43,14 +43,23 @@ namespace tfusion
         float& operator()(int r, int c) { return val[r * 3 + c]; }
     };
 
-    // cv::Affine3f subset: 4x4 row-major matrix of a rigid transform (camera -> world for poses)
+    // cv::Matx44f subset: row-major 4x4, element (r, c) = val[4r + c]
+    struct Matx44f {
+        float val[16];
+        float operator()(int r, int c) const { return val[r * 4 + c]; }
+        float& operator()(int r, int c) { return val[r * 4 + c]; }
+    };
+
+    // cv::Affine3f subset: the 4x4 matrix of a rigid transform (camera -> world for poses), with
+    // the member names the reference's callers use: matrix(r, c) (topfu.cpp:246-249),
+    // rotation(), translation(), inv(), operator*, Identity(), translate()
     struct Affine3f {
-        float matrix[16];
+        Matx44f matrix;
         Affine3f() { *this = Identity(); }
         static Affine3f Identity()
         {
             Affine3f a(0);
-            for (int i = 0; i < 4; ++i) a.matrix[i * 5] = 1.f;
+            for (int i = 0; i < 4; ++i) a.matrix.val[i * 5] = 1.f;
             return a;
         }
         // from the C-ABI's row-major 3x4 [R|t]
@@ -58,27 +67,27 @@ namespace tfusion
         {
             Affine3f a(0);
             for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 4; ++c) a.matrix[r * 4 + c] = rt[r * 4 + c];
-            a.matrix[15] = 1.f;
+                for (int c = 0; c < 4; ++c) a.matrix(r, c) = rt[r * 4 + c];
+            a.matrix(3, 3) = 1.f;
             return a;
         }
         void toRt(float rt[12]) const
         {
             for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 4; ++c) rt[r * 4 + c] = matrix[r * 4 + c];
+                for (int c = 0; c < 4; ++c) rt[r * 4 + c] = matrix(r, c);
         }
         Mat3f rotation() const
         {
             Mat3f R;
             for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) R(r, c) = matrix[r * 4 + c];
+                for (int c = 0; c < 3; ++c) R(r, c) = matrix(r, c);
             return R;
         }
-        Vec3f translation() const { return Vec3f(matrix[3], matrix[7], matrix[11]); }
+        Vec3f translation() const { return Vec3f(matrix(0, 3), matrix(1, 3), matrix(2, 3)); }
         Affine3f translate(const Vec3f& t) const
         {
             Affine3f a = *this;
-            a.matrix[3] += t[0]; a.matrix[7] += t[1]; a.matrix[11] += t[2];
+            a.matrix(0, 3) += t[0]; a.matrix(1, 3) += t[1]; a.matrix(2, 3) += t[2];
             return a;
         }
         Affine3f operator*(const Affine3f& b) const   // rigid composition in float
@@ -86,27 +95,50 @@ namespace tfusion
             Affine3f o(0);
             for (int r = 0; r < 3; ++r) {
                 for (int c = 0; c < 3; ++c)
-                    o.matrix[r * 4 + c] = matrix[r * 4 + 0] * b.matrix[0 * 4 + c] + matrix[r * 4 + 1] * b.matrix[1 * 4 + c] +
-                                          matrix[r * 4 + 2] * b.matrix[2 * 4 + c];
-                o.matrix[r * 4 + 3] = matrix[r * 4 + 0] * b.matrix[3] + matrix[r * 4 + 1] * b.matrix[7] +
-                                      matrix[r * 4 + 2] * b.matrix[11] + matrix[r * 4 + 3];
+                    o.matrix(r, c) = matrix(r, 0) * b.matrix(0, c) + matrix(r, 1) * b.matrix(1, c) + matrix(r, 2) * b.matrix(2, c);
+                o.matrix(r, 3) = matrix(r, 0) * b.matrix(0, 3) + matrix(r, 1) * b.matrix(1, 3) + matrix(r, 2) * b.matrix(2, 3) +
+                                 matrix(r, 3);
             }
-            o.matrix[15] = 1.f;
+            o.matrix(3, 3) = 1.f;
             return o;
         }
         Affine3f inv() const                            // rigid inverse [R^T | -R^T t]
         {
             Affine3f o(0);
             for (int r = 0; r < 3; ++r) {
-                for (int c = 0; c < 3; ++c) o.matrix[r * 4 + c] = matrix[c * 4 + r];
-                o.matrix[r * 4 + 3] = -(matrix[0 * 4 + r] * matrix[3] + matrix[1 * 4 + r] * matrix[7] +
-                                        matrix[2 * 4 + r] * matrix[11]);
+                for (int c = 0; c < 3; ++c) o.matrix(r, c) = matrix(c, r);
+                o.matrix(r, 3) = -(matrix(0, r) * matrix(0, 3) + matrix(1, r) * matrix(1, 3) + matrix(2, r) * matrix(2, 3));
             }
-            o.matrix[15] = 1.f;
+            o.matrix(3, 3) = 1.f;
             return o;
         }
     private:
         explicit Affine3f(int) : matrix{} {}
+    };
+
+    // Matrix4f (tfusion/include/Matrix.hpp:22-66, 126-133): column-major, m[4c + r]; the 16-value
+    // constructor fills m in argument order, so Matrix4f(P(0,0), P(1,0), P(2,0), P(3,0), P(0,1), ...)
+    // holds P (the reference's conversion, topfu.cpp:246-249); operator()(x, y) is column x, row y
+    struct Matrix4f {
+        float m[16];
+        Matrix4f() : m{} { for (int i = 0; i < 4; ++i) m[i * 5] = 1.f; }
+        Matrix4f(float a00, float a01, float a02, float a03, float a10, float a11, float a12, float a13,
+                 float a20, float a21, float a22, float a23, float a30, float a31, float a32, float a33)
+            : m{ a00, a01, a02, a03, a10, a11, a12, a13, a20, a21, a22, a23, a30, a31, a32, a33 } {}
+        float& operator()(int x, int y) { return m[y | (x << 2)]; }
+        float operator()(int x, int y) const { return m[y | (x << 2)]; }
+        // the rigid transform it holds as a row-major 3x4 [R|t] (the C-ABI's pose layout)
+        void toRt(float rt[12]) const
+        {
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 4; ++c) rt[r * 4 + c] = m[4 * c + r];
+        }
+        static Matrix4f fromAffine(const Affine3f& a)
+        {
+            const Matx44f& P = a.matrix;
+            return Matrix4f(P(0, 0), P(1, 0), P(2, 0), P(3, 0), P(0, 1), P(1, 1), P(2, 1), P(3, 1),
+                            P(0, 2), P(1, 2), P(2, 2), P(3, 2), P(0, 3), P(1, 3), P(2, 3), P(3, 3));
+        }
     };
 
     struct Intr {
@@ -123,7 +155,16 @@ namespace tfusion
     struct Point { union { float data[4]; struct { float x, y, z; }; }; };
     typedef Point Normal;
     struct Vector4u { unsigned char x, y, z, w; };
-    struct Vector4f { float x, y, z, w; };
+    struct Vector4f {
+        float x, y, z, w;
+        Vector4f() : x(0), y(0), z(0), w(0) {}
+        Vector4f(float x_, float y_, float z_, float w_) : x(x_), y(y_), z(z_), w(w_) {}
+    };
+    struct Vector2i {
+        int x, y;
+        Vector2i() : x(0), y(0) {}
+        Vector2i(int x_, int y_) : x(x_), y(y_) {}
+    };
 
     inline float deg2rad(float alpha) { return alpha * 0.017453293f; }
 
@@ -206,11 +247,21 @@ namespace tfusion
         typedef DeviceArray2D<Normal> Normals;
         struct RGB { union { struct { unsigned char b, g, r; }; int bgra; }; };
         typedef DeviceArray2D<RGB> Image;
+        typedef DeviceArray2D<int> imageInt;
+
+        // cuda::Frame (types.hpp:73-79): one frame's pyramids
+        struct Frame {
+            bool use_points = true;
+            std::vector<Depth> depth_pyr;
+            std::vector<Cloud> points_pyr;
+            std::vector<Normals> normals_pyr;
+        };
     }
 
-    // ScopeTime / SampledScopeTime (types.hpp:86-108; core.cpp:180-216): wall-clock timers.
-    // SampledScopeTime averages over EACH = 33 scopes per instance (the reference keeps the
-    // counter in a function static; here it lives in the object so several streams can time).
+    // ScopeTime / SampledScopeTime (types.hpp:83-104; core.cpp:202-231): wall-clock timers with the
+    // reference's output.  SampledScopeTime keeps the reference's function-static call counter
+    // (core.cpp:208): one counter for the whole program, so a loop that constructs one per frame
+    // (demo.cpp:102-105) prints the average after 33 more frames each time, starting at the 34th.
     struct ScopeTime {
         const char* name;
         std::chrono::steady_clock::time_point start;
@@ -218,29 +269,32 @@ namespace tfusion
         ~ScopeTime()
         {
             double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - start).count();
-            std::printf("Time(%s) = %.3f ms\n", name, ms);
+            std::printf("Time(%s) = %gms\n", name, ms);
         }
     };
 
     struct SampledScopeTime {
         enum { EACH = 33 };
-        explicit SampledScopeTime(double& time_ms, int* counter = nullptr)
-            : time_ms_(time_ms), counter_(counter), start_(std::chrono::steady_clock::now()) {}
+        explicit SampledScopeTime(double& time_ms) : time_ms_(time_ms), start_(std::chrono::steady_clock::now()) {}
         ~SampledScopeTime()
         {
-            time_ms_ += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - start_).count();
-            int& c = counter_ ? *counter_ : local_;
-            if (++c == EACH) {
-                std::printf("Average frame time = %.3f ms ( %.1f fps )\n", time_ms_ / EACH, 1000.0 * EACH / time_ms_);
-                time_ms_ = 0; c = 0;
+            static int i_ = 0;                  // function-static, as core.cpp:208 (inline: one per program)
+            time_ms_ += getTime();
+            if (i_ % EACH == 0 && i_) {
+                std::printf("Average frame time = %gms ( %gfps )\n", time_ms_ / EACH, 1000.f * EACH / time_ms_);
+                std::fflush(stdout);
+                time_ms_ = 0.0;
             }
+            ++i_;
         }
     private:
+        double getTime() const
+        {
+            return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - start_).count();
+        }
         SampledScopeTime(const SampledScopeTime&) = delete;
         SampledScopeTime& operator=(const SampledScopeTime&) = delete;
         double& time_ms_;
-        int* counter_;
-        int local_ = 0;
         std::chrono::steady_clock::time_point start_;
     };
 }

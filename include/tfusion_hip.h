@@ -174,6 +174,72 @@ tf_status tf_stage_reset_scene(tf_ctx* ctx);
 /* swap curr <-> prev points/normals pyramids (topfu.cpp:205-207) */
 tf_status tf_stage_swap_pyramids(tf_ctx* ctx);
 
+/* ---- engine entry points over caller buffers (the L4 C++ API, include/tfusion/engines.hpp) --
+ * Poses are row-major 3x4 [R|t]; intr = {fx, fy, cx, cy} (Intr, types.hpp:20-26) and overrides the
+ * context's intrinsics for the call; dists / maps are caller device buffers with a row step in
+ * bytes, rows x cols of the context's image size.  All synchronous. */
+/* cuda::ProjectiveICP::setDistThreshold / setAngleThreshold / setIterationsNum
+ * (projective_icp.cpp:81-101): the tracker parameters the context's frames use from now on */
+tf_status tf_icp_set_params(tf_ctx* ctx, float dist_thres, float angle_thres, const int iters[4]);
+tf_status tf_icp_get_params(tf_ctx* ctx, float* dist_thres, float* angle_thres, int iters[4]);
+/* one level of a point/normal pyramid: float4 maps, row steps in bytes */
+typedef struct tf_map_level {
+    const void* points; size_t points_step;
+    const void* normals; size_t normals_step;
+} tf_map_level;
+/* cuda::ProjectiveICP::estimateTransform(affine, intr, vcurr, ncurr, vprev, nprev)
+ * (projective_icp.cpp:169-213) on caller pyramids (level l is (cols >> l) x (rows >> l)); the
+ * maps are copied into the context's current/previous pyramids first.  affine_rt receives the
+ * estimate (the last successful composition when *ok == 0, as the reference leaves it). */
+tf_status tf_icp_estimate(tf_ctx* ctx, const float intr[4], const tf_map_level* curr, const tf_map_level* prev,
+                          int levels, float affine_rt[12], int* ok, int* iterations);
+/* SceneReconstructionEngine_CUDA::AllocateSceneFromDepth(scene, intr, pose, dists, renderState,
+ * onlyUpdateVisibleList, resetVisibleList) (SceneReconstructionEngine_host.cu:75-195); pose is
+ * world -> camera (TopFu passes poses_.back().inv(), topfu.cpp:281) */
+tf_status tf_scene_alloc(tf_ctx* ctx, const float intr[4], const float pose_rt[12], const float* dists,
+                         size_t dists_step, int only_update_visible_list, int reset_visible_list);
+/* ::IntegrateIntoScene(scene, intr, pose, dists, renderState) (SceneReconstructionEngine_host.cu:197-251) */
+tf_status tf_scene_integrate(tf_ctx* ctx, const float intr[4], const float pose_rt[12], const float* dists,
+                             size_t dists_step);
+/* VisualisationEngine_CUDA::CreateExpectedDepths(scene, pose, intr, renderState)
+ * (VisualisationEngine_CUDA.cu:119-173); pose is world -> camera */
+tf_status tf_vis_expected_depths(tf_ctx* ctx, const float intr[4], const float pose_rt[12]);
+/* ::RenderImage(scene, pose, intr, renderState, image, type, raycastType)
+ * (VisualisationEngine_CUDA.cu:220-291, 423-429); pose is camera -> world (Matrix4f(poses_.back()),
+ * topfu.cpp:346-352); new_raycast = 1: RENDER_FROM_NEW_RAYCAST, 0: RENDER_FROM_OLD_RAYCAST (the
+ * pixel stage on the current raycast result) */
+tf_status tf_vis_render_image(tf_ctx* ctx, const float intr[4], const float pose_rt[12], int type, int new_raycast,
+                              uint8_t* dev_rgba, size_t step);
+/* ::CreateICPMaps(scene, pose, intr, points, normals, renderState) (VisualisationEngine_CUDA.cu:
+ * 323-360, 473-493): castRay<true> + renderICP into the caller's level-0 maps; pose is camera -> world */
+tf_status tf_vis_icp_maps(tf_ctx* ctx, const float intr[4], const float pose_rt[12], void* points, size_t points_step,
+                          void* normals, size_t normals_step);
+
+/* ---- cuda:: image processing over caller buffers (imgproc.hpp:9-31, imgproc.cu) --------
+ * Stateless; stream = hipStream_t (NULL: the legacy default stream); all asynchronous on it.
+ * Depth is uint16 millimetres, dists float, points / normals float4; steps in bytes. */
+/* cuda::computeDists (imgproc.cu:263-290) */
+tf_status tf_imgproc_compute_dists(const uint16_t* depth, size_t depth_step, float* dists, size_t dists_step,
+                                   int cols, int rows, void* stream);
+/* cuda::depthBilateralFilter (imgproc.cu:10-61); sigma_depth in metres as the reference takes it */
+tf_status tf_imgproc_bilateral(const uint16_t* in, size_t in_step, uint16_t* out, size_t out_step, int cols, int rows,
+                               int ksz, float sigma_spatial, float sigma_depth, void* stream);
+/* cuda::depthTruncation (imgproc.cu:70-89), in place; threshold in metres */
+tf_status tf_imgproc_truncate(uint16_t* depth, size_t step, int cols, int rows, float threshold, void* stream);
+/* cuda::depthBuildPyramid (imgproc.cu:98-140): out is (cols/2) x (rows/2) */
+tf_status tf_imgproc_pyr_down(const uint16_t* in, size_t in_step, int cols, int rows, uint16_t* out, size_t out_step,
+                              float sigma_depth, void* stream);
+/* cuda::computePointNormals (imgproc.cu:214-254) with intr = {fx, fy, cx, cy} of this level */
+tf_status tf_imgproc_point_normals(const float intr[4], const uint16_t* depth, size_t depth_step, int cols, int rows,
+                                   void* points, size_t points_step, void* normals, size_t normals_step, void* stream);
+/* cuda::resizePointsNormals (imgproc.cu:355-401): outputs are (cols/2) x (rows/2) */
+tf_status tf_imgproc_resize_points_normals(const void* points, size_t points_step, const void* normals,
+                                           size_t normals_step, int cols, int rows, void* points_out,
+                                           size_t points_out_step, void* normals_out, size_t normals_out_step,
+                                           void* stream);
+/* cuda::waitAllDefaultStream (imgproc.cpp:18-19) */
+tf_status tf_imgproc_sync(void* stream);
+
 /* ---- state transfer --------------------------------------------------------- */
 /* host <-> context buffer copies; level selects the pyramid level for TF_BUF_DEPTH..
  * TF_BUF_PREV_NORMALS.  bytes must equal the buffer size (tf_buffer_bytes). */

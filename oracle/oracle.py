@@ -83,6 +83,7 @@ def lib(omp=False):
         L.tfo_get_counters.argtypes = [P, ctypes.POINTER(Counters)]
         L.tfo_get_pose.argtypes = [P, P]
         L.tfo_alloc.argtypes = [P, P, P]
+        L.tfo_alloc_ex.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int]
         L.tfo_integrate.argtypes = [P, P, P]
         L.tfo_expected_depths.argtypes = [P, P]
         L.tfo_raycast.argtypes = [P, P, ctypes.c_int]
@@ -290,9 +291,9 @@ class Oracle:
         return self._view(self.L.tfo_curr_depth(self.ctx, l), np.uint16, h * w, (h, w)).copy()
 
     # stage-level
-    def alloc(self, pose_rt, dists):
-        self.L.tfo_alloc(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
-                        ptr(np.ascontiguousarray(dists, np.float32)))
+    def alloc(self, pose_rt, dists, only_update_visible=False, reset_visible=False):
+        self.L.tfo_alloc_ex(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
+                            ptr(np.ascontiguousarray(dists, np.float32)), int(only_update_visible), int(reset_visible))
 
     def integrate(self, pose_rt, dists):
         self.L.tfo_integrate(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),

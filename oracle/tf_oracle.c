@@ -719,8 +719,9 @@ static int check_block_visibility(int16_t px, int16_t py, int16_t pz, const floa
     return 0;
 }
 
-/* AllocateSceneFromDepth, SceneReconstructionEngine_host.cu:75-195 (+ kernels :331-479) */
-void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists)
+/* AllocateSceneFromDepth, SceneReconstructionEngine_host.cu:75-195 (+ kernels :331-479), with the
+   onlyUpdateVisibleList (:160-168: no allocation pass) and resetVisibleList (:88) arguments */
+void tfo_alloc_ex(tfo_ctx* c, const float pose_rt[12], const float* dists, int only_update_visible, int reset_visible)
 {
     int W = c->p.cols, H = c->p.rows;
     float M[16], invM[16];
@@ -733,6 +734,7 @@ void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists)
     int noAllocatedVoxelEntries = c->lastFreeBlockId;
     int noAllocatedExcessEntries = c->lastFreeExcessListId;
     int noVisibleEntries = 0;
+    if (reset_visible) c->noVisibleEntries = 0;
     memset(c->allocType, 0, (size_t)c->n_total);
     /* setToType3, :343-348 */
     for (int i = 0; i < c->noVisibleEntries; ++i) c->visType[c->visibleIds[i]] = 3;
@@ -741,7 +743,7 @@ void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists)
         for (int x = 0; x < W; ++x)
             build_hash_alloc_pixel(c, x, y, dists, invM, invProj, mu, oneOverVoxelSize);
     /* allocateVoxelBlocksList_device, :350-415, serial in index order */
-    for (int t = 0; t < c->n_total; ++t) {
+    for (int t = 0; t < c->n_total && !only_update_visible; ++t) {
         int vbaIdx, exlIdx;
         switch (c->allocType[t]) {
         case 1:
@@ -794,6 +796,11 @@ void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists)
     c->noVisibleEntries = noVisibleEntries;
     c->lastFreeBlockId = noAllocatedVoxelEntries;
     c->lastFreeExcessListId = noAllocatedExcessEntries;
+}
+
+void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists)
+{
+    tfo_alloc_ex(c, pose_rt, dists, 0, 0);
 }
 
 /* computeUpdatedVoxelDepthInfo, SceneReconstructionEngine.hpp:23-71 */

@@ -126,6 +126,7 @@ void tfo_get_counters(const tfo_ctx* c, tfo_counters* out);
 void tfo_get_pose(const tfo_ctx* c, float rt[12]);            /* getCameraPose(): [R|t] row-major */
 /* stage-level entry points on the context */
 void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists);      /* AllocateSceneFromDepth */
+void tfo_alloc_ex(tfo_ctx* c, const float pose_rt[12], const float* dists, int only_update_visible, int reset_visible);
 void tfo_integrate(tfo_ctx* c, const float pose_rt[12], const float* dists);  /* IntegrateIntoScene */
 void tfo_expected_depths(tfo_ctx* c, const float pose_rt[12]);                 /* CreateExpectedDepths */
 void tfo_raycast(tfo_ctx* c, const float invM_rt[12], int update_visible);    /* GenericRaycast */

@@ -59,3 +59,32 @@ class DeviceFrames:
         if self.ptr:
             self._hip.hipFree(ctypes.c_void_p(self.ptr))
             self.ptr = None
+
+
+class DeviceBuffer(DeviceFrames):
+    """A device allocation of `nbytes` (zero-filled), with host <-> device copies; 2-D copies
+    with a row step (bytes) for pitched layouts."""
+
+    def __init__(self, nbytes):
+        super().__init__(np.zeros(int(nbytes), np.uint8))
+
+    def upload2d(self, arr, step):
+        import ctypes
+        a = np.ascontiguousarray(arr)
+        rows = a.shape[0]
+        row_bytes = a.nbytes // rows
+        assert step * rows <= self.nbytes and row_bytes <= step
+        assert self._hip.hipMemcpy2D(ctypes.c_void_p(self.ptr), ctypes.c_size_t(step), a.ctypes.data_as(ctypes.c_void_p),
+                                     ctypes.c_size_t(row_bytes), ctypes.c_size_t(row_bytes), ctypes.c_size_t(rows), 1) == 0
+
+    def download2d(self, shape, dtype, step):
+        import ctypes
+        out = np.empty(shape, dtype)
+        rows = shape[0]
+        row_bytes = out.nbytes // rows
+        assert self._hip.hipMemcpy2D(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(row_bytes), ctypes.c_void_p(self.ptr),
+                                     ctypes.c_size_t(step), ctypes.c_size_t(row_bytes), ctypes.c_size_t(rows), 2) == 0
+        return out
+
+    def sync(self):
+        assert self._hip.hipDeviceSynchronize() == 0

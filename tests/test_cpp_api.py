@@ -10,9 +10,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 APPS = os.path.join(ROOT, "apps")
 
 
-def _build():
+def _build(app="demo_headless"):
     subprocess.run(["make", "-s", "-C", APPS], check=True)
-    return os.path.join(APPS, "demo_headless")
+    return os.path.join(APPS, app)
 
 
 def test_cpp_api_builds_and_links():
@@ -31,6 +31,30 @@ def test_demo_headless_runs():
     m = re.search(r"frames (\d+) ok (\d+) resets (\d+)", r.stdout)
     assert m and int(m.group(1)) == 40 and int(m.group(2)) >= 30, r.stdout
     assert "rendered pixels lit" in r.stdout
+    # SampledScopeTime's function-static counter (core.cpp:206-216): one scope per frame prints
+    # the average once, at the 34th
+    assert r.stdout.count("Average frame time = ") == 1, r.stdout
+
+
+def test_engine_api_builds_and_links():
+    exe = _build("engine_check")
+    syms = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True, check=True).stdout
+    for fn in ("tf_scene_alloc", "tf_scene_integrate", "tf_vis_render_image", "tf_vis_icp_maps", "tf_icp_estimate",
+               "tf_imgproc_bilateral", "tf_icp_set_params"):
+        assert fn in syms, fn
+
+
+@pytest.mark.gpu
+def test_engine_api_matches_topfu():
+    """apps/engine_check: TopFu::operator() against the same frames spelled out over the L4
+    engine API (imgproc functions, a stand-alone ProjectiveICP, the reconstruction and
+    visualisation engines) -- bool, pose, counters and renderImage bit-exact every frame, ICP
+    maps at the end; 40 frames include ICP-failure resets."""
+    exe = _build("engine_check")
+    r = subprocess.run([exe, "40", "320", "240"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = re.search(r"engine_check frames (\d+) ok (\d+) resets (\d+): MATCH", r.stdout)
+    assert m and int(m.group(1)) == 40 and int(m.group(3)) >= 1, r.stdout
 
 
 @pytest.mark.gpu

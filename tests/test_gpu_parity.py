@@ -168,6 +168,7 @@ def test_sequence(oracle_mod, cols, rows, nframes, icp_schedule):
     g, o = make_pair(oracle_mod, cols, rows)
     _check_schedule(g, icp_schedule)
     seq = synth.orbit_sequence(nframes, cols, rows, seed=7)
+    spilled = 0
     for k in range(nframes):
         okg = g(seq[k])
         oko = o(seq[k])
@@ -180,6 +181,15 @@ def test_sequence(oracle_mod, cols, rows, nframes, icp_schedule):
         assert_bit_exact(f"frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
         if k > 0 and oko:
             assert_bit_exact(f"frame {k} renderImage grey", g.frame_grey(), o.frame_grey())
+            # the whole range image, including the pixels outside the /8 region that boxes
+            # clamped to the full-resolution W-1 / H-1 spill into
+            rg = g.range_image()
+            assert_bit_exact(f"frame {k} range image", rg, o.range_image())
+            rc, rr = (cols - 1) // 8 + 1, (rows - 1) // 8 + 1
+            spill = rg.copy()
+            spill[:rr, :rc] = 0
+            spilled += int((spill[..., 1] > np.float32(0.05)).sum())
+    assert spilled > 0, "no frame filled the range image outside its /8 region"
     compare_scene(g, o, "final")
     assert_bit_exact("final raycast", g.raycast_result(), o.raycast_result())
     for l in range(3):
@@ -282,6 +292,7 @@ def test_batched_frames_overlap(oracle_mod, icp_schedule):
 
 
 def _compare_frame_state(g, o, tag, grey=True):
+    assert_bit_exact(f"{tag} range image", g.range_image(), o.range_image())
     sg, so = g.stats(), o.counters()
     for key in ("frame_counter", "n_resets", "icp_iterations", "lastFreeBlockId", "lastFreeExcessListId",
                 "noVisibleEntries"):

@@ -50,6 +50,12 @@ class TfTotals(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class TfMapLevel(ctypes.Structure):
+    """tf_map_level: one level of a float4 point / normal pyramid (device pointers, row steps)."""
+    _fields_ = [("points", ctypes.c_void_p), ("points_step", ctypes.c_size_t),
+                ("normals", ctypes.c_void_p), ("normals_step", ctypes.c_size_t)]
+
+
 class TfError(RuntimeError):
     def __init__(self, status, where):
         self.status = status
@@ -111,6 +117,22 @@ def load():
         "tf_set_pose": ([P, P], I),
         "tf_set_counters": ([P, I, I, I], I),
         "tf_get_totals": ([P, ctypes.POINTER(TfTotals)], I),
+        "tf_icp_set_params": ([P, F, F, P], I),
+        "tf_icp_get_params": ([P, ctypes.POINTER(F), ctypes.POINTER(F), P], I),
+        "tf_icp_estimate": ([P, P, ctypes.POINTER(TfMapLevel), ctypes.POINTER(TfMapLevel), I, P,
+                             ctypes.POINTER(I), ctypes.POINTER(I)], I),
+        "tf_scene_alloc": ([P, P, P, P, S, I, I], I),
+        "tf_scene_integrate": ([P, P, P, P, S], I),
+        "tf_vis_expected_depths": ([P, P, P], I),
+        "tf_vis_render_image": ([P, P, P, I, I, P, S], I),
+        "tf_vis_icp_maps": ([P, P, P, P, S, P, S], I),
+        "tf_imgproc_compute_dists": ([P, S, P, S, I, I, P], I),
+        "tf_imgproc_bilateral": ([P, S, P, S, I, I, I, F, F, P], I),
+        "tf_imgproc_truncate": ([P, S, I, I, F, P], I),
+        "tf_imgproc_pyr_down": ([P, S, I, I, P, S, F, P], I),
+        "tf_imgproc_point_normals": ([P, P, S, I, I, P, S, P, S, P], I),
+        "tf_imgproc_resize_points_normals": ([P, S, P, S, I, I, P, S, P, S, P], I),
+        "tf_imgproc_sync": ([P], I),
         "tf_reset_totals": ([P], I),
         "tf_render_image_type": ([P, I, P, S], I),
         "tf_time_stage": ([P, I, P, I, ctypes.POINTER(ctypes.c_float)], I),

@@ -738,6 +738,151 @@ extern "C" tf_status tf_stage_swap_pyramids(tf_ctx* c)
     return TF_OK;
 }
 
+// ---- engine entry points over caller buffers (include/tfusion/engines.hpp) -------------
+// the call's intrinsics (the reference engines take Intr per call) in place of the context's
+// for as long as the scope lives; every launcher reads c->p when it builds its arguments
+struct IntrScope {
+    tf_ctx* c;
+    float saved[4];
+    IntrScope(tf_ctx* ctx, const float* intr) : c(ctx)
+    {
+        saved[0] = c->p.fx; saved[1] = c->p.fy; saved[2] = c->p.cx; saved[3] = c->p.cy;
+        if (intr) { c->p.fx = intr[0]; c->p.fy = intr[1]; c->p.cx = intr[2]; c->p.cy = intr[3]; }
+    }
+    ~IntrScope() { c->p.fx = saved[0]; c->p.fy = saved[1]; c->p.cx = saved[2]; c->p.cy = saved[3]; }
+};
+
+extern "C" tf_status tf_icp_set_params(tf_ctx* c, float dist_thres, float angle_thres, const int iters[4])
+{
+    if (!c || !iters || !(dist_thres >= 0) || !(angle_thres >= 0)) return TF_INVALID_ARG;
+    if (iters[3] != 0) return TF_INVALID_ARG;            // three pyramid levels (TF_LEVELS)
+    for (int l = 0; l < 4; ++l) if (iters[l] < 0) return TF_INVALID_ARG;
+    c->p.icp_dist_thres = dist_thres;
+    c->p.icp_angle_thres = angle_thres;
+    for (int l = 0; l < 4; ++l) c->p.icp_iter_num[l] = iters[l];
+    // ComputeIcpHelper ctor (projective_icp.cpp:11-15)
+    c->min_cosine = cosf(angle_thres);
+    c->dist2_thres = dist_thres * dist_thres;
+    return TF_OK;
+}
+
+extern "C" tf_status tf_icp_get_params(tf_ctx* c, float* dist_thres, float* angle_thres, int iters[4])
+{
+    if (!c) return TF_INVALID_ARG;
+    if (dist_thres) *dist_thres = c->p.icp_dist_thres;
+    if (angle_thres) *angle_thres = c->p.icp_angle_thres;
+    if (iters) for (int l = 0; l < 4; ++l) iters[l] = c->p.icp_iter_num[l];
+    return TF_OK;
+}
+
+// caller pitched float4 map -> the context's packed level buffer
+static hipError_t copy_map_in(tf_ctx* c, float4* dst, int l, const void* src, size_t step)
+{
+    const size_t row = sizeof(float4) * (size_t)c->lw[l];
+    return hipMemcpy2DAsync(dst, row, src, step ? step : row, row, c->lh[l], hipMemcpyDeviceToDevice, c->stream);
+}
+
+extern "C" tf_status tf_icp_estimate(tf_ctx* c, const float intr[4], const tf_map_level* curr, const tf_map_level* prev,
+                                     int levels, float affine_rt[12], int* ok, int* iterations)
+{
+    if (!c || !curr || !prev || levels < 1 || levels > TF_LEVELS) return TF_INVALID_ARG;
+    int used = 4;                                         // getUsedLevelsNum (projective_icp.cpp:103-108)
+    while (used > 0 && c->p.icp_iter_num[used - 1] == 0) --used;
+    if (used > levels) return TF_INVALID_ARG;
+    for (int l = 0; l < levels; ++l)
+        if (!curr[l].points || !curr[l].normals || !prev[l].points || !prev[l].normals) return TF_INVALID_ARG;
+    for (int l = 0; l < levels; ++l) {
+        TF_CHECK(copy_map_in(c, c->curr_pts[l], l, curr[l].points, curr[l].points_step));
+        TF_CHECK(copy_map_in(c, c->curr_nrm[l], l, curr[l].normals, curr[l].normals_step));
+        TF_CHECK(copy_map_in(c, c->prev_pts[l], l, prev[l].points, prev[l].points_step));
+        TF_CHECK(copy_map_in(c, c->prev_nrm[l], l, prev[l].normals, prev[l].normals_step));
+    }
+    IntrScope is(c, intr);
+    return tf_stage_icp(c, affine_rt, ok, iterations);
+}
+
+// caller dists (pitched) -> the context's dists buffer
+static hipError_t copy_dists_in(tf_ctx* c, const float* dists, size_t step)
+{
+    const size_t row = sizeof(float) * (size_t)c->W;
+    return hipMemcpy2DAsync(c->dists, row, dists, step ? step : row, row, c->H, hipMemcpyDeviceToDevice, c->stream);
+}
+
+extern "C" tf_status tf_scene_alloc(tf_ctx* c, const float intr[4], const float pose_rt[12], const float* dists,
+                                   size_t dists_step, int only_update_visible_list, int reset_visible_list)
+{
+    if (!c || !pose_rt || !dists) return TF_INVALID_ARG;
+    TF_CHECK(copy_dists_in(c, dists, dists_step));
+    IntrScope is(c, intr);
+    tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
+    if (s != TF_OK) return s;
+    if (reset_visible_list) {          // renderState_vh->noVisibleEntries = 0 (SceneReconstructionEngine_host.cu:88)
+        static const int zero = 0;
+        TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, noVisibleEntries), &zero, sizeof(int),
+                                hipMemcpyHostToDevice, c->stream));
+    }
+    TF_CHECK(tfk_alloc(c, 0, TfAhead{}, 0, only_update_visible_list ? 1 : 0));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_scene_integrate(tf_ctx* c, const float intr[4], const float pose_rt[12], const float* dists,
+                                       size_t dists_step)
+{
+    if (!c || !pose_rt || !dists) return TF_INVALID_ARG;
+    TF_CHECK(copy_dists_in(c, dists, dists_step));
+    IntrScope is(c, intr);
+    tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
+    if (s != TF_OK) return s;
+    TF_CHECK(tfk_integrate(c));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_vis_expected_depths(tf_ctx* c, const float intr[4], const float pose_rt[12])
+{
+    if (!c || !pose_rt) return TF_INVALID_ARG;
+    IntrScope is(c, intr);
+    return tf_stage_expected_depths(c, pose_rt);
+}
+
+extern "C" tf_status tf_vis_render_image(tf_ctx* c, const float intr[4], const float pose_rt[12], int type, int new_raycast,
+                                        uint8_t* dev_rgba, size_t step)
+{
+    if (!c || !pose_rt || type < TF_RENDER_SHADED_GREYSCALE || type > TF_RENDER_COLOUR_FROM_CONFIDENCE) return TF_INVALID_ARG;
+    IntrScope is(c, intr);
+    tf_status s = set_pose_in(c, pose_rt, 0);
+    if (s != TF_OK) return s;
+    if (new_raycast) TF_CHECK(tfk_raycast(c, 0));        // RENDER_FROM_NEW_RAYCAST (VisualisationEngine_CUDA.cu:227-240)
+    TF_CHECK(tfk_render_type(c, type));
+    if (dev_rgba) {
+        const size_t row = (size_t)c->W * 4;
+        TF_CHECK(hipMemcpy2DAsync(dev_rgba, step ? step : row, c->grey, row, row, c->H, hipMemcpyDeviceToDevice, c->stream));
+    }
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_vis_icp_maps(tf_ctx* c, const float intr[4], const float pose_rt[12], void* points,
+                                    size_t points_step, void* normals, size_t normals_step)
+{
+    if (!c || !pose_rt) return TF_INVALID_ARG;
+    IntrScope is(c, intr);
+    tf_status s = set_pose_in(c, pose_rt, 0);
+    if (s != TF_OK) return s;
+    TF_CHECK(tfk_raycast(c, 1));                          // castRay<true> (VisualisationEngine_CUDA.cu:340-345)
+    TF_CHECK(tfk_icp_maps(c));                            // renderICP (:347-359) + the context's resized levels
+    const size_t row = sizeof(float4) * (size_t)c->W;
+    if (points)
+        TF_CHECK(hipMemcpy2DAsync(points, points_step ? points_step : row, c->prev_pts[0], row, row, c->H,
+                                  hipMemcpyDeviceToDevice, c->stream));
+    if (normals)
+        TF_CHECK(hipMemcpy2DAsync(normals, normals_step ? normals_step : row, c->prev_nrm[0], row, row, c->H,
+                                  hipMemcpyDeviceToDevice, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
 // ---- state transfer -------------------------------------------------------------------
 static void* buffer_ptr(tf_ctx* c, int which, int level, size_t* bytes)
 {

@@ -330,7 +330,8 @@ struct TfAhead {
     uint16_t* d0;            // its level-0 depth buffer (d0_buf)
 };
 hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0,       // snapshot: + the frame's renderImage snapshot
-                     TfAhead bil = TfAhead{}, size_t pitch = 0);   // bil: + that frame's bilateral pass
+                     TfAhead bil = TfAhead{}, size_t pitch = 0,    // bil: + that frame's bilateral pass
+                     int only_update = 0);    // onlyUpdateVisibleList: requests are discarded, not allocated
 // frame_path: + frame-0 map copy; with_ed: CreateExpectedDepths' projection pass in the
 // grid's first TF_ED_BLOCKS workgroups (then tfk_expected_depths(c, 1) runs only the fill)
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0, int with_ed = 0);

@@ -466,6 +466,22 @@ k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int*
 }
 
 
+// AllocateSceneFromDepth(..., onlyUpdateVisibleList = true): the requests of this frame are
+// dropped unapplied -- request state back to empty, counters unchanged (the reference memsets
+// allocType every frame, SceneReconstructionEngine_host.cu:146); the visible types the request
+// pass set stay, as in the reference
+__global__ void __launch_bounds__(256)
+k_alloc_discard(TfDevState* __restrict__ st, const int* __restrict__ counts, unsigned char* __restrict__ allocType,
+                int* __restrict__ winnerKey, int n_total)
+{
+    if (st->abort) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { st->alloc_exhausted = 0; st->pad_[0] = 0; st->pad_[1] = 0; }
+    if (counts[2 * blockIdx.x] == 0) return;             // no request in this chunk
+    for (int i = blockIdx.x * CHUNK + threadIdx.x; i < (int)(blockIdx.x + 1) * CHUNK && i < n_total; i += 256) {
+        if (allocType[i]) { allocType[i] = 0; winnerKey[i] = -1; }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // buildVisibleList_device<false> (SceneReconstructionEngine_host.cu:434-479) with
 // checkBlockVisibility<false> (SceneReconstructionEngine.hpp:300-375), ordered compaction
@@ -553,7 +569,7 @@ static AllocArgs make_alloc_args(tf_ctx* c)
 
 // AllocateSceneFromDepth (SceneReconstructionEngine_host.cu:75-195) with the matrices
 // already in st->M_alloc / st->invM_alloc
-hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch)
+hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch, int only_update)
 {
     AllocArgs a = make_alloc_args(c);
     VisArgs v;
@@ -574,9 +590,13 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch)
     } else nb = BilArgs{};
     hipLaunchKernelGGL(k_alloc_requests, dim3(n_alloc + n_next), dim3(256), 0, c->stream,
                        a, c->st, c->hash, c->allocType, c->visType, c->winnerKey, c->allocCounts, gx, n_alloc, nb, next_gx);
-    hipLaunchKernelGGL(k_alloc_apply, dim3(c->alloc_chunks), dim3(256), 0, c->stream, a, c->st, c->alloc_chunks,
-                       c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
-                       c->requestList, c->n_total);
+    if (only_update)   // allocateVoxelBlocksList_device is skipped (SceneReconstructionEngine_host.cu:162-168)
+        hipLaunchKernelGGL(k_alloc_discard, dim3(c->alloc_chunks), dim3(256), 0, c->stream, c->st, c->allocCounts,
+                           c->allocType, c->winnerKey, c->n_total);
+    else
+        hipLaunchKernelGGL(k_alloc_apply, dim3(c->alloc_chunks), dim3(256), 0, c->stream, a, c->st, c->alloc_chunks,
+                           c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
+                           c->requestList, c->n_total);
     hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
                        c->visCounts, c->allocCounts);
     hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
