@@ -56,6 +56,14 @@ typedef struct tf_params {
     int   n_blocks;                     /* SDF_LOCAL_BLOCK_NUM (VoxelBlockHash.hpp:14) */
     int   vis_capacity;                 /* visibleEntryIDs capacity (RenderState_VH.hpp:42) */
     int   max_render_blocks;            /* MAX_RENDERING_BLOCKS (VisualisationEngine_Shared.hpp:5) */
+    /* swapping: Scene(params, useSwapping) (scene.hpp:29-33) with its GlobalCache
+       (GlobalCache.hpp:11-134), kept in HBM; TopFu itself runs without (topfu.cpp:67) */
+    int   use_swapping;
+    int   swap_transfer_blocks;         /* SDF_TRANSFER_BLOCK_NUM (VoxelBlockHash.hpp:27): blocks per swap */
+    /* colour: Voxel_s_rgb voxels (VoxelTypes.hpp:39-67) integrated from the RGB image */
+    int   voxel_rgb;
+    float rgb_intr[4];                  /* projParams_rgb (fx, fy, cx, cy); all 0: the depth intrinsics */
+    float depth_to_rgb[12];             /* calib_inv of trafo_rgb_to_depth, row-major [R|t]: M_rgb = it * M_d */
 } tf_params;
 
 /* integer counters the reference keeps host-side (LocalVBA.hpp:26, VoxelBlockHash.hpp:69,
@@ -87,7 +95,10 @@ typedef enum tf_buffer {
     TF_BUF_CURR_NORMALS = 9,
     TF_BUF_PREV_POINTS = 10,
     TF_BUF_PREV_NORMALS = 11,
-    TF_BUF_GREY = 12          /* uchar4[rows*cols] last renderImage output */
+    TF_BUF_GREY = 12,         /* uchar4[rows*cols] last renderImage output */
+    TF_BUF_SWAP_STATE = 13,   /* uchar[n_buckets+n_excess] HashSwapState::state (GlobalCache.hpp:11-20) */
+    TF_BUF_SWAP_STORED_FLAGS = 14,  /* uchar[n_buckets+n_excess] GlobalCache hasStoredData */
+    TF_BUF_SWAP_STORED = 15   /* Voxel_s[(n_buckets+n_excess)*512] GlobalCache storedVoxelBlocks */
 } tf_buffer;
 
 /* ---- device ---------------------------------------------------------------- */
@@ -201,6 +212,17 @@ tf_status tf_scene_alloc(tf_ctx* ctx, const float intr[4], const float pose_rt[1
 /* ::IntegrateIntoScene(scene, intr, pose, dists, renderState) (SceneReconstructionEngine_host.cu:197-251) */
 tf_status tf_scene_integrate(tf_ctx* ctx, const float intr[4], const float pose_rt[12], const float* dists,
                              size_t dists_step);
+/* The swapping engine of the GlobalCache's lineage, run after integration when use_swapping is
+ * set (every frame of tf_process_frame(s) does it): IntegrateGlobalIntoLocal + SaveToGlobalMemory
+ * (InfiniTAM ITMSwappingEngine_CUDA, whose instantiation the reference comments out,
+ * CUDAInstantiations.cu:8); its semantics are written out in DESIGN.md §Swapping. */
+tf_status tf_scene_swap(tf_ctx* ctx);
+/* blocks swapped in / out and reallocated by the last frame (or tf_scene_* call) */
+tf_status tf_swap_counts(tf_ctx* ctx, int counts[3]);
+/* GlobalCache::SaveToFile / ReadFromFile (GlobalCache.hpp:79-110): hasStoredData as one byte per
+ * entry, then every entry's 512 voxels (4 B each), n_buckets + n_excess entries */
+tf_status tf_swap_save(tf_ctx* ctx, const char* path);
+tf_status tf_swap_load(tf_ctx* ctx, const char* path);
 /* VisualisationEngine_CUDA::CreateExpectedDepths(scene, pose, intr, renderState)
  * (VisualisationEngine_CUDA.cu:119-173); pose is world -> camera */
 tf_status tf_vis_expected_depths(tf_ctx* ctx, const float intr[4], const float pose_rt[12]);
@@ -284,6 +306,8 @@ typedef struct tf_totals {
     long long resets;               /* ICP failures -> reset (topfu.cpp:263-264) */
     long long visible_sum;          /* noVisibleEntries summed over the frames that integrated */
     long long tiles_sum;            /* noTotalBlocks summed over the tracked frames */
+    long long swapped_in;           /* blocks swapped in (use_swapping) */
+    long long swapped_out;          /* blocks swapped out (use_swapping) */
 } tf_totals;
 tf_status tf_get_totals(tf_ctx* ctx, tf_totals* totals);
 tf_status tf_reset_totals(tf_ctx* ctx);

@@ -25,7 +25,9 @@ class Params(ctypes.Structure):
                 ("mu", ctypes.c_float), ("maxW", ctypes.c_int), ("voxelSize", ctypes.c_float),
                 ("viewFrustum_min", ctypes.c_float), ("viewFrustum_max", ctypes.c_float),
                 ("n_buckets", ctypes.c_int), ("n_excess", ctypes.c_int), ("n_blocks", ctypes.c_int),
-                ("vis_capacity", ctypes.c_int), ("max_render_blocks", ctypes.c_int)]
+                ("vis_capacity", ctypes.c_int), ("max_render_blocks", ctypes.c_int),
+                ("use_swapping", ctypes.c_int), ("swap_transfer_blocks", ctypes.c_int),
+                ("voxel_rgb", ctypes.c_int), ("rgb_intr", ctypes.c_float * 4), ("depth_to_rgb", ctypes.c_float * 12)]
 
 
 class Counters(ctypes.Structure):
@@ -92,8 +94,11 @@ def lib(omp=False):
         L.tfo_render_image.argtypes = [P, P]
         L.tfo_render_type.argtypes = [P, P, ctypes.c_int, P]
         L.tfo_render_image_type.argtypes = [P, ctypes.c_int]
+        L.tfo_swap.argtypes = [P]
+        L.tfo_swap_counts.argtypes = [P, P]
         for name in ("tfo_hash", "tfo_vba", "tfo_visible_ids", "tfo_visible_type", "tfo_range_image",
-                     "tfo_raycast_result", "tfo_dists", "tfo_frame_grey"):
+                     "tfo_raycast_result", "tfo_dists", "tfo_frame_grey", "tfo_swap_state", "tfo_swap_stored_flags",
+                     "tfo_swap_stored"):
             getattr(L, name).argtypes = [P]; getattr(L, name).restype = P
         for name in ("tfo_prev_points", "tfo_prev_normals", "tfo_curr_points", "tfo_curr_normals", "tfo_curr_depth"):
             getattr(L, name).argtypes = [P, ctypes.c_int]; getattr(L, name).restype = P
@@ -112,6 +117,10 @@ def default_params(**kw):
         if k == "icp_iter_num":
             for i in range(4):
                 p.icp_iter_num[i] = int(v[i]) if i < len(v) else 0
+        elif k in ("rgb_intr", "depth_to_rgb"):
+            arr = getattr(p, k)
+            for i, x in enumerate(v):
+                arr[i] = float(x)
         else:
             setattr(p, k, v)
     return p
@@ -320,6 +329,22 @@ class Oracle:
         img = np.empty((self.H, self.W, 4), np.uint8)
         self.L.tfo_render_image(self.ctx, ptr(img))
         return img
+
+    # swapping state (GlobalCache)
+    def swap_counts(self):
+        """Last frame's (swapped in, swapped out, reallocated) block counts."""
+        out = np.zeros(3, np.int32)
+        self.L.tfo_swap_counts(self.ctx, ptr(out))
+        return tuple(int(v) for v in out)
+
+    def swap_state(self):
+        return self._view(self.L.tfo_swap_state(self.ctx), np.uint8, self.n_total).copy()
+
+    def swap_stored_flags(self):
+        return self._view(self.L.tfo_swap_stored_flags(self.ctx), np.uint8, self.n_total).copy()
+
+    def swap_stored(self):
+        return self._view(self.L.tfo_swap_stored(self.ctx), VOXEL_DTYPE, self.n_total * 512).copy()
 
     def render_image_type(self, type):
         """RenderImage(type) from the current pose into the context image (the buffer the frame's

@@ -36,6 +36,10 @@ void tfo_default_params(tfo_params* p)
     p->n_buckets = 0x100000; p->n_excess = 0x20000; p->n_blocks = 0x10000;
     p->vis_capacity = 0x10000 * 4;                  /* SDF_LOCAL_BLOCK_NUM*sizeof(int) elements, RenderState_VH.hpp:42 */
     p->max_render_blocks = 65536 * 4;
+    p->use_swapping = 0;                            /* Scene(params, false), topfu.cpp:67 */
+    p->swap_transfer_blocks = 0x1000;               /* SDF_TRANSFER_BLOCK_NUM, VoxelBlockHash.hpp:27 */
+    p->voxel_rgb = 0;                               /* Voxel_s (Defines.hpp:5) */
+    p->depth_to_rgb[0] = p->depth_to_rgb[5] = p->depth_to_rgb[10] = 1.0f;   /* registered RGB-D */
 }
 
 /* ------------------------------------------------------------------------- */
@@ -547,6 +551,11 @@ struct tfo_ctx {
     float* prev_pts[3]; float* prev_nrm[3];
     int lvl_w[3], lvl_h[3];
     int icp_iterations, icp_ok, n_resets;
+    /* swapping: GlobalCache (GlobalCache.hpp:11-134) kept per hash entry */
+    uint8_t* swapState;       /* HashSwapState::state */
+    uint8_t* hasStored;       /* hasStoredData */
+    tfo_voxel* stored;        /* storedVoxelBlocks, 512 voxels per entry */
+    int swap_counts[3];       /* last frame: swapped in, swapped out, reallocated */
 };
 
 static const float k_identity_rt[12] = { 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0 };
@@ -561,6 +570,12 @@ static void reset_scene(tfo_ctx* c)
     for (int i = 0; i < c->n_total; ++i) c->hash[i].ptr = -2;
     for (int i = 0; i < c->p.n_excess; ++i) c->excessList[i] = i;
     c->lastFreeExcessListId = c->p.n_excess - 1;
+    /* the reference's ResetScene leaves a GlobalCache alone (its swapping is never enabled);
+       here a reset also empties it, so no block of the old scene is swapped into the new one */
+    if (c->p.use_swapping) {
+        memset(c->swapState, 0, (size_t)c->n_total);
+        memset(c->hasStored, 0, (size_t)c->n_total);
+    }
 }
 
 tfo_ctx* tfo_create(const tfo_params* p)
@@ -592,6 +607,11 @@ tfo_ctx* tfo_create(const tfo_params* p)
         c->prev_nrm[l] = (float*)calloc((size_t)w * h * 4, sizeof(float));
         w /= 2; h /= 2;
     }
+    if (p->use_swapping) {
+        c->swapState = (uint8_t*)calloc((size_t)c->n_total, 1);
+        c->hasStored = (uint8_t*)calloc((size_t)c->n_total, 1);
+        c->stored = (tfo_voxel*)calloc((size_t)c->n_total * BLK3, sizeof(tfo_voxel));
+    }
     reset_scene(c);                                   /* topfu.cpp:75 */
     memcpy(c->pose, k_identity_rt, sizeof(c->pose));  /* reset(), topfu.cpp:141-152 */
     c->frame_counter = 0;
@@ -606,6 +626,7 @@ void tfo_destroy(tfo_ctx* c)
     for (int l = 0; l < 3; ++l) {
         free(c->depth_pyr[l]); free(c->curr_pts[l]); free(c->curr_nrm[l]); free(c->prev_pts[l]); free(c->prev_nrm[l]);
     }
+    free(c->swapState); free(c->hasStored); free(c->stored);
     free(c);
 }
 
@@ -695,6 +716,45 @@ static inline int check_point_visibility(const float pt[4], const float M[16], c
     return (b[0] >= 0 && b[0] < (float)W && b[1] >= 0 && b[1] < (float)H);
 }
 
+/* checkPointVisibility<true>'s enlarged frustum (SceneReconstructionEngine.hpp:315-321): the
+   image grown by an eighth of its size on every side, integer limits */
+static inline int check_point_enlarged(const float pt[4], const float M[16], const float proj[4], int W, int H)
+{
+    float b[4];
+    m4v(M, pt, b);
+    if (b[2] < 1e-10f) return 0;
+    b[0] = proj[0] * b[0] / b[2] + proj[2];
+    b[1] = proj[1] * b[1] / b[2] + proj[3];
+    const int lx = -W / 8, ux = W + W / 8, ly = -H / 8, uy = H + H / 8;
+    return (b[0] >= (float)lx && b[0] < (float)ux && b[1] >= (float)ly && b[1] < (float)uy);
+}
+
+/* checkBlockVisibility<true>'s isVisibleEnlarged: any of the 8 corners in the enlarged frustum
+   (a corner inside the image is inside it too, so the early return on isVisible changes nothing) */
+static int check_block_enlarged(int16_t px, int16_t py, int16_t pz, const float M[16], const float proj[4],
+                                float voxelSize, int W, int H)
+{
+    float factor = (float)BLK * voxelSize;
+    float pt[4];
+    pt[0] = (float)px * factor; pt[1] = (float)py * factor; pt[2] = (float)pz * factor; pt[3] = 1.0f;
+    if (check_point_enlarged(pt, M, proj, W, H)) return 1;
+    pt[2] += factor;
+    if (check_point_enlarged(pt, M, proj, W, H)) return 1;
+    pt[1] += factor;
+    if (check_point_enlarged(pt, M, proj, W, H)) return 1;
+    pt[0] += factor;
+    if (check_point_enlarged(pt, M, proj, W, H)) return 1;
+    pt[2] -= factor;
+    if (check_point_enlarged(pt, M, proj, W, H)) return 1;
+    pt[1] -= factor;
+    if (check_point_enlarged(pt, M, proj, W, H)) return 1;
+    pt[0] -= factor; pt[1] += factor;
+    if (check_point_enlarged(pt, M, proj, W, H)) return 1;
+    pt[0] += factor; pt[1] -= factor; pt[2] += factor;
+    if (check_point_enlarged(pt, M, proj, W, H)) return 1;
+    return 0;
+}
+
 static int check_block_visibility(int16_t px, int16_t py, int16_t pz, const float M[16], const float proj[4],
                                   float voxelSize, int W, int H)
 {
@@ -779,20 +839,36 @@ void tfo_alloc_ex(tfo_ctx* c, const float pose_rt[12], const float* dists, int o
         default: break;
         }
     }
-    /* buildVisibleList_device<false>, :434-479, compaction in index order */
+    /* buildVisibleList_device<useSwapping>, :434-479, compaction in index order; swapping
+       (:159-160, never with onlyUpdateVisibleList): the enlarged frustum for type-3 entries
+       and swap state 1 ("needed") for every listed entry not already in active memory (2) */
+    const int swapping = c->p.use_swapping && !only_update_visible;
     for (int t = 0; t < c->n_total; ++t) {
         uint8_t vt = c->visType[t];
         if (vt == 3) {
             const tfo_hash_entry* e = &c->hash[t];
-            if (!check_block_visibility(e->x, e->y, e->z, M, proj, c->p.voxelSize, W, H)) vt = 0;
+            if (swapping ? !check_block_enlarged(e->x, e->y, e->z, M, proj, c->p.voxelSize, W, H)
+                         : !check_block_visibility(e->x, e->y, e->z, M, proj, c->p.voxelSize, W, H)) vt = 0;
             c->visType[t] = vt;
         }
         if (vt > 0) {
+            if (swapping && c->swapState[t] != 2) c->swapState[t] = 1;
             if (noVisibleEntries < c->p.vis_capacity) c->visibleIds[noVisibleEntries] = t;
             noVisibleEntries++;
         }
     }
     if (noVisibleEntries > c->p.vis_capacity) noVisibleEntries = c->p.vis_capacity;
+    /* reAllocateSwappedOutVoxelBlocks_device (:184-189, 417-432): listed entries whose block
+       was swapped out (ptr == -1) get a block again, in ascending index order */
+    c->swap_counts[2] = 0;
+    if (swapping)
+        for (int t = 0; t < c->n_total; ++t) {
+            if (c->visType[t] > 0 && c->hash[t].ptr == -1) {
+                int vbaIdx = noAllocatedVoxelEntries--;
+                if (vbaIdx >= 0) { c->hash[t].ptr = c->allocList[vbaIdx]; c->swap_counts[2]++; }
+                else noAllocatedVoxelEntries++;
+            }
+        }
     c->noVisibleEntries = noVisibleEntries;
     c->lastFreeBlockId = noAllocatedVoxelEntries;
     c->lastFreeExcessListId = noAllocatedExcessEntries;
@@ -802,6 +878,78 @@ void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists)
 {
     tfo_alloc_ex(c, pose_rt, dists, 0, 0);
 }
+
+/* ------------------------------------------------------------------------- */
+/* Swapping.  The reference has the GlobalCache (GlobalCache.hpp:11-134: per-entry host
+   store, hasStoredData, swap states 0 / 1 / 2, SDF_TRANSFER_BLOCK_NUM blocks per transfer)
+   and the swapping branches of AllocateSceneFromDepth (above), but not the engine that moves
+   blocks (CUDAInstantiations.cu:8 comments out ITMSwappingEngine_CUDA).  The engine restated
+   here is the published algorithm of that lineage (InfiniTAM v3 ITMSwappingEngine_CUDA /
+   ITMSwappingEngine_Shared.h, not vendored): after integration,
+     IntegrateGlobalIntoLocal: entries in state 1 (ascending index, at most T) take their
+       stored block back -- CombineVoxelInformation merges it into the active block by weight
+       (skipped where the stored weight is 0) -- and go to state 2;
+     SaveToGlobalMemory: entries in state 2 with a block and not visible this frame
+       (ascending, at most T) are copied to the store, their block reset to Voxel_s() and
+       returned to the free list (cleanMemory: allocList[++lastFreeBlockId] = ptr, ptr = -1),
+       state 0.
+   Canonical order: ascending hash index where the lineage uses atomics.  One guard: an entry in
+   state 1 without a block (its reallocation failed) is not swapped in (the lineage would write
+   through ptr = -1). */
+/* ------------------------------------------------------------------------- */
+/* CombineVoxelInformation (depth part), ITMSwappingEngine_Shared.h: src = stored, dst = active */
+static inline void combine_voxel(const tfo_voxel* src, tfo_voxel* dst, int maxW)
+{
+    int newW = dst->w;
+    int oldW = src->w;
+    float newF = (float)dst->sdf / 32767.0f;
+    float oldF = (float)src->sdf / 32767.0f;
+    if (oldW == 0) return;
+    newF = (float)oldW * oldF + (float)newW * newF;
+    newW = oldW + newW;
+    newF /= (float)newW;
+    newW = (newW < maxW) ? newW : maxW;
+    dst->w = (uint8_t)newW;
+    dst->sdf = (int16_t)(newF * 32767.0f);
+}
+
+void tfo_swap(tfo_ctx* c)
+{
+    if (!c->p.use_swapping) return;
+    const int T = c->p.swap_transfer_blocks;
+    int n_in = 0, n_out = 0;
+    for (int t = 0; t < c->n_total && n_in < T; ++t) {                 /* IntegrateGlobalIntoLocal */
+        if (c->swapState[t] != 1 || c->hash[t].ptr < 0) continue;
+        if (c->hasStored[t]) {
+            tfo_voxel* dst = c->vba + (size_t)c->hash[t].ptr * BLK3;
+            const tfo_voxel* src = c->stored + (size_t)t * BLK3;
+            for (int v = 0; v < BLK3; ++v) combine_voxel(&src[v], &dst[v], c->p.maxW);
+        }
+        c->swapState[t] = 2;
+        n_in++;
+    }
+    for (int t = 0; t < c->n_total && n_out < T; ++t) {                /* SaveToGlobalMemory */
+        if (c->swapState[t] != 2 || c->hash[t].ptr < 0 || c->visType[t] != 0) continue;
+        tfo_voxel* blk = c->vba + (size_t)c->hash[t].ptr * BLK3;
+        memcpy(c->stored + (size_t)t * BLK3, blk, sizeof(tfo_voxel) * BLK3);   /* moveActiveDataToTransferBuffer */
+        c->hasStored[t] = 1;
+        for (int v = 0; v < BLK3; ++v) { blk[v].sdf = 32767; blk[v].w = 0; blk[v].pad = 0; }
+        c->swapState[t] = 0;                                            /* cleanMemory */
+        int vbaIdx = c->lastFreeBlockId++;
+        if (vbaIdx < c->p.n_blocks - 1) {
+            c->allocList[vbaIdx + 1] = c->hash[t].ptr;
+            c->hash[t].ptr = -1;
+        }
+        n_out++;
+    }
+    c->swap_counts[0] = n_in;
+    c->swap_counts[1] = n_out;
+}
+
+void tfo_swap_counts(const tfo_ctx* c, int out[3]) { memcpy(out, c->swap_counts, sizeof(int) * 3); }
+uint8_t* tfo_swap_state(tfo_ctx* c) { return c->swapState; }
+uint8_t* tfo_swap_stored_flags(tfo_ctx* c) { return c->hasStored; }
+tfo_voxel* tfo_swap_stored(tfo_ctx* c) { return c->stored; }
 
 /* computeUpdatedVoxelDepthInfo, SceneReconstructionEngine.hpp:23-71 */
 static inline void update_voxel(tfo_voxel* v, const float pt_model[4], const float M[16], const float proj[4],
@@ -1371,6 +1519,7 @@ int tfo_process_frame(tfo_ctx* c, const uint16_t* depth)
         c->icp_iterations = 0;
         tfo_alloc(c, c->pose, c->dists);                  /* poses_.back() == identity */
         tfo_integrate(c, c->pose, c->dists);
+        tfo_swap(c);                                      /* (swapping only) */
         for (int l = 0; l < 3; ++l) {                     /* swap curr <-> prev points/normals */
             float* t = c->curr_pts[l]; c->curr_pts[l] = c->prev_pts[l]; c->prev_pts[l] = t;
             t = c->curr_nrm[l]; c->curr_nrm[l] = c->prev_nrm[l]; c->prev_nrm[l] = t;
@@ -1387,6 +1536,7 @@ int tfo_process_frame(tfo_ctx* c, const uint16_t* depth)
     tfo_rigid_inv(c->pose, pinv);
     tfo_alloc(c, pinv, c->dists);
     tfo_integrate(c, pinv, c->dists);
+    tfo_swap(c);                                          /* (swapping only) */
     /* renderImage(image): raycast with the (stale) range image + grey shading (topfu.cpp:284-288) */
     tfo_render_image(c, c->frame_grey);
     tfo_expected_depths(c, pinv);

@@ -64,6 +64,13 @@ typedef struct tfo_params {
     int   n_blocks;                 /* SDF_LOCAL_BLOCK_NUM */
     int   vis_capacity;             /* visibleEntryIDs capacity */
     int   max_render_blocks;        /* MAX_RENDERING_BLOCKS */
+    /* swapping: Scene(params, useSwapping) (scene.hpp:29-33, GlobalCache.hpp); off in TopFu (topfu.cpp:67) */
+    int   use_swapping;
+    int   swap_transfer_blocks;     /* SDF_TRANSFER_BLOCK_NUM (VoxelBlockHash.hpp:27) */
+    /* colour: Voxel_s_rgb instead of Voxel_s (VoxelTypes.hpp:39-67) and the RGB camera */
+    int   voxel_rgb;
+    float rgb_intr[4];              /* projParams_rgb (fx, fy, cx, cy); all 0: the depth intrinsics */
+    float depth_to_rgb[12];         /* trafo_rgb_to_depth.calib_inv as row-major [R|t] (M_rgb = it * M_d) */
 } tfo_params;
 
 typedef struct tfo_hash_entry {     /* VoxelBlockHash.hpp:32-44 (16 B) */
@@ -135,6 +142,12 @@ void tfo_render_type(tfo_ctx* c, const float invM_rt[12], int type, uint8_t* rgb
 void tfo_render_image_type(tfo_ctx* c, int type);
 void tfo_render_grey(tfo_ctx* c, const float invM_rt[12], uint8_t* rgba);     /* renderGrey */
 void tfo_render_image(tfo_ctx* c, uint8_t* rgba);                              /* TopFu::renderImage */
+/* swapping (GlobalCache + the InfiniTAM-lineage swapping engine, see tf_oracle.c) */
+void tfo_swap(tfo_ctx* c);                          /* IntegrateGlobalIntoLocal + SaveToGlobalMemory */
+void tfo_swap_counts(const tfo_ctx* c, int out[3]);  /* last frame: swapped in, swapped out, reallocated */
+uint8_t* tfo_swap_state(tfo_ctx* c);                /* HashSwapState::state per entry */
+uint8_t* tfo_swap_stored_flags(tfo_ctx* c);         /* GlobalCache hasStoredData per entry */
+tfo_voxel* tfo_swap_stored(tfo_ctx* c);             /* GlobalCache storedVoxelBlocks, 512 per entry */
 /* state access */
 tfo_hash_entry* tfo_hash(tfo_ctx* c);
 tfo_voxel* tfo_vba(tfo_ctx* c);

@@ -17,7 +17,8 @@ STAGE_NAMES = ("preprocess", "icp", "alloc", "integrate", "raycast_render", "gre
                "raycast_icp", "icp_maps")
 
 (TF_BUF_HASH, TF_BUF_VBA, TF_BUF_VISIBLE_IDS, TF_BUF_VISIBLE_TYPE, TF_BUF_RANGE, TF_BUF_RAYCAST, TF_BUF_DISTS,
- TF_BUF_DEPTH, TF_BUF_CURR_POINTS, TF_BUF_CURR_NORMALS, TF_BUF_PREV_POINTS, TF_BUF_PREV_NORMALS, TF_BUF_GREY) = range(13)
+ TF_BUF_DEPTH, TF_BUF_CURR_POINTS, TF_BUF_CURR_NORMALS, TF_BUF_PREV_POINTS, TF_BUF_PREV_NORMALS, TF_BUF_GREY,
+ TF_BUF_SWAP_STATE, TF_BUF_SWAP_STORED_FLAGS, TF_BUF_SWAP_STORED) = range(16)
 
 
 class TfParams(ctypes.Structure):
@@ -31,7 +32,9 @@ class TfParams(ctypes.Structure):
                 ("mu", ctypes.c_float), ("maxW", ctypes.c_int), ("voxelSize", ctypes.c_float),
                 ("viewFrustum_min", ctypes.c_float), ("viewFrustum_max", ctypes.c_float),
                 ("n_buckets", ctypes.c_int), ("n_excess", ctypes.c_int), ("n_blocks", ctypes.c_int),
-                ("vis_capacity", ctypes.c_int), ("max_render_blocks", ctypes.c_int)]
+                ("vis_capacity", ctypes.c_int), ("max_render_blocks", ctypes.c_int),
+                ("use_swapping", ctypes.c_int), ("swap_transfer_blocks", ctypes.c_int),
+                ("voxel_rgb", ctypes.c_int), ("rgb_intr", ctypes.c_float * 4), ("depth_to_rgb", ctypes.c_float * 12)]
 
 
 class TfStats(ctypes.Structure):
@@ -44,7 +47,8 @@ class TfStats(ctypes.Structure):
 
 
 class TfTotals(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_longlong) for n in ("frames", "frames_tracked", "resets", "visible_sum", "tiles_sum")]
+    _fields_ = [(n, ctypes.c_longlong) for n in ("frames", "frames_tracked", "resets", "visible_sum", "tiles_sum",
+                                                 "swapped_in", "swapped_out")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -124,6 +128,10 @@ def load():
         "tf_scene_alloc": ([P, P, P, P, S, I, I], I),
         "tf_scene_integrate": ([P, P, P, P, S], I),
         "tf_vis_expected_depths": ([P, P, P], I),
+        "tf_scene_swap": ([P], I),
+        "tf_swap_counts": ([P, P], I),
+        "tf_swap_save": ([P, ctypes.c_char_p], I),
+        "tf_swap_load": ([P, ctypes.c_char_p], I),
         "tf_vis_render_image": ([P, P, P, I, I, P, S], I),
         "tf_vis_icp_maps": ([P, P, P, P, S, P, S], I),
         "tf_imgproc_compute_dists": ([P, S, P, S, I, I, P], I),
@@ -170,6 +178,10 @@ def default_params(**kw):
         if k == "icp_iter_num":
             for i in range(4):
                 p.icp_iter_num[i] = int(v[i]) if i < len(v) else 0
+        elif k in ("rgb_intr", "depth_to_rgb"):
+            arr = getattr(p, k)
+            for i, x in enumerate(v):
+                arr[i] = float(x)
         else:
             setattr(p, k, v)
     return p

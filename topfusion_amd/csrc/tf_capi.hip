@@ -69,6 +69,10 @@ extern "C" tf_status tf_default_params(tf_params* p)
     p->n_buckets = 0x100000; p->n_excess = 0x20000; p->n_blocks = 0x10000;
     p->vis_capacity = 0x40000;
     p->max_render_blocks = 65536 * 4;
+    p->use_swapping = 0;                          // Scene(params, false), topfu.cpp:67
+    p->swap_transfer_blocks = 0x1000;             // SDF_TRANSFER_BLOCK_NUM, VoxelBlockHash.hpp:27
+    p->voxel_rgb = 0;                             // Voxel_s (Defines.hpp:5)
+    p->depth_to_rgb[0] = p->depth_to_rgb[5] = p->depth_to_rgb[10] = 1.0f;   // registered RGB-D
     return TF_OK;
 }
 
@@ -87,6 +91,8 @@ static bool params_valid(const tf_params* p)
     // steps per pixel ceil(2*|e-s|) with |e-s| ~ 2*mu/(8*voxel) must fit the 6-bit key field
     if (4.0f * p->mu / (8.0f * p->voxelSize) + 2.0f > 60.0f) return false;
     if ((double)p->cols * p->rows * 64.0 > 2147483000.0) return false;
+    if (p->use_swapping && (p->swap_transfer_blocks <= 0 || p->swap_transfer_blocks > p->n_buckets + p->n_excess)) return false;
+    if (p->voxel_rgb) return false;                 // Voxel_s_rgb: not built into this library yet
     return true;
 }
 
@@ -96,7 +102,7 @@ static void ctx_free(tf_ctx* c)
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockBox, c->blockZ, c->blockTiles, c->blockOff, c->edChunk, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
-                     c->frame_ok, c->frame_mode };
+                     c->frame_ok, c->frame_mode, c->swapState, c->swapFlags, c->swapStore, c->swapCounts };
     for (void* b : bufs) if (b) (void)hipFree(b);
     // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
     float4* maps[4] = { c->curr_pts[0], c->curr_nrm[0], c->prev_pts[0], c->prev_nrm[0] };
@@ -217,6 +223,15 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->icp_ticket, 64);
     ALLOC(c->icp_tagged, sizeof(unsigned long long) * TF_ICP_TAG_WORDS);
     ALLOC(c->st, sizeof(TfDevState));
+    if (pin->use_swapping) {        // the GlobalCache in HBM: 2 KiB per hash entry + flags
+        ALLOC(c->swapState, ntot_pad);
+        ALLOC(c->swapFlags, ntot_pad);
+        ALLOC(c->swapStore, sizeof(TfVoxel) * (size_t)c->n_total * TF_BLK3);
+        ALLOC(c->swapCounts, sizeof(int) * 2 * (size_t)c->alloc_chunks);
+        e = hipMemsetAsync(c->swapState, 0, ntot_pad, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(c->swapFlags, 0, ntot_pad, c->stream);
+        if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    }
 #undef ALLOC
     e = hipHostMalloc((void**)&c->st_host, sizeof(TfDevState), hipHostMallocDefault);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
@@ -388,6 +403,7 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     STAGE(TF_STAGE_ALLOC, tfk_alloc(c, t3_fold ? 2 : 1, plan->alloc_bil, pitch));   // topfu.cpp:202 / 281
     // (+ CreateExpectedDepths' projection pass in the same grid)
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1, 1));              // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
+    if (c->p.use_swapping) TF_CHECK(tfk_swap(c));                   // swap in / out after integration
     STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c, 1));     // topfu.cpp:306
     // CreateICPMaps' raycast + renderImage (topfu.cpp:284-285 + 307) in one launch (snapshot range)
     STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch));
@@ -839,6 +855,67 @@ extern "C" tf_status tf_scene_integrate(tf_ctx* c, const float intr[4], const fl
     return TF_OK;
 }
 
+extern "C" tf_status tf_scene_swap(tf_ctx* c)
+{
+    if (!c) return TF_INVALID_ARG;
+    if (!c->p.use_swapping) return TF_INVALID_ARG;
+    TF_CHECK(clear_abort(c));
+    TF_CHECK(tfk_swap(c));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_swap_counts(tf_ctx* c, int counts[3])
+{
+    if (!c || !counts) return TF_INVALID_ARG;
+    tf_status s = sync_state(c);
+    if (s != TF_OK) return s;
+    counts[0] = c->st_host->swap_in; counts[1] = c->st_host->swap_out; counts[2] = c->st_host->swap_realloc;
+    return TF_OK;
+}
+
+// GlobalCache::SaveToFile / ReadFromFile (GlobalCache.hpp:79-110): hasStoredData (1 byte per
+// entry), then 512 voxels of 4 bytes per entry
+extern "C" tf_status tf_swap_save(tf_ctx* c, const char* path)
+{
+    if (!c || !path || !c->p.use_swapping) return TF_INVALID_ARG;
+    const size_t nf = (size_t)c->n_total, nv = sizeof(TfVoxel) * (size_t)c->n_total * TF_BLK3;
+    void* host = malloc(nf + nv);
+    if (!host) return TF_OOM;
+    hipError_t e = hipMemcpyAsync(host, c->swapFlags, nf, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync((char*)host + nf, c->swapStore, nv, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    tf_status s = tf_from_hip(e);
+    if (s == TF_OK) {
+        FILE* f = fopen(path, "wb");
+        if (!f || fwrite(host, 1, nf + nv, f) != nf + nv) s = TF_INVALID_ARG;
+        if (f) fclose(f);
+    }
+    free(host);
+    return s;
+}
+
+extern "C" tf_status tf_swap_load(tf_ctx* c, const char* path)
+{
+    if (!c || !path || !c->p.use_swapping) return TF_INVALID_ARG;
+    const size_t nf = (size_t)c->n_total, nv = sizeof(TfVoxel) * (size_t)c->n_total * TF_BLK3;
+    FILE* f = fopen(path, "rb");
+    if (!f) return TF_INVALID_ARG;
+    void* host = malloc(nf + nv);
+    if (!host) { fclose(f); return TF_OOM; }
+    const size_t got = fread(host, 1, nf + nv, f);
+    fclose(f);
+    tf_status s = TF_OK;
+    if (got == nf + nv) {       // the reference reads the blocks only when the flags are complete
+        hipError_t e = hipMemcpyAsync(c->swapFlags, host, nf, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(c->swapStore, (char*)host + nf, nv, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        s = tf_from_hip(e);
+    } else s = TF_INVALID_ARG;
+    free(host);
+    return s;
+}
+
 extern "C" tf_status tf_vis_expected_depths(tf_ctx* c, const float intr[4], const float pose_rt[12])
 {
     if (!c || !pose_rt) return TF_INVALID_ARG;
@@ -903,6 +980,9 @@ static void* buffer_ptr(tf_ctx* c, int which, int level, size_t* bytes)
     case TF_BUF_PREV_POINTS: *bytes = sizeof(float4) * nl; return c->prev_pts[level];
     case TF_BUF_PREV_NORMALS: *bytes = sizeof(float4) * nl; return c->prev_nrm[level];
     case TF_BUF_GREY: *bytes = sizeof(uchar4) * npx; return c->grey;
+    case TF_BUF_SWAP_STATE: *bytes = c->swapState ? (size_t)c->n_total : 0; return c->swapState;
+    case TF_BUF_SWAP_STORED_FLAGS: *bytes = c->swapFlags ? (size_t)c->n_total : 0; return c->swapFlags;
+    case TF_BUF_SWAP_STORED: *bytes = c->swapStore ? sizeof(TfVoxel) * (size_t)c->n_total * TF_BLK3 : 0; return c->swapStore;
     }
     *bytes = 0;
     return nullptr;
@@ -970,13 +1050,14 @@ extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)
     const TfDevState* d = c->st_host;
     t->frames = d->tot_frames; t->frames_tracked = d->tot_tracked; t->resets = d->tot_resets;
     t->visible_sum = d->tot_visible; t->tiles_sum = d->tot_tiles;
+    t->swapped_in = d->tot_swap_in; t->swapped_out = d->tot_swap_out;
     return TF_OK;
 }
 
 extern "C" tf_status tf_reset_totals(tf_ctx* c)
 {
     if (!c) return TF_INVALID_ARG;
-    const long long zero[5] = { 0, 0, 0, 0, 0 };
+    const long long zero[7] = { 0, 0, 0, 0, 0, 0, 0 };
     TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, tot_frames), zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;

@@ -1029,6 +1029,7 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
             a.vis.fx = c->p.fx; a.vis.fy = c->p.fy; a.vis.cx = c->p.cx; a.vis.cy = c->p.cy;
             a.vis.factor = (float)TF_BLK * c->p.voxelSize;
             a.vis.W = c->W; a.vis.H = c->H; a.vis.n_total = c->n_total; a.vis.cap = c->p.vis_capacity;
+            a.vis.enlarged = c->p.use_swapping ? 1 : 0;
             a.hash = c->hash; a.visibleIds = c->visibleIds; a.visType = c->visType;
             a.range = (const float2*)c->range; a.snap = (float2*)c->range_render;
         }

@@ -73,8 +73,11 @@ struct TfDevState {
     float M_render[16];      // M_ray of the frame being rendered
     int render_go;           // the frame took the tracking path (mode 1, ICP ok)
     int pad3_[3];
+    // swapping (tf_swap.hip): the last frame's counts, and the free-list top handed from the
+    // swap-in launch to the swap-out launch
+    int swap_in, swap_out, swap_realloc, swap_free0;
     // totals since creation / tf_reset_totals, accumulated by the frame end (tf_totals)
-    long long tot_frames, tot_tracked, tot_resets, tot_visible, tot_tiles, tot_pad_;
+    long long tot_frames, tot_tracked, tot_resets, tot_visible, tot_tiles, tot_swap_in, tot_swap_out, tot_pad_;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -205,6 +208,12 @@ __host__ __device__ __forceinline__ size_t tf_grid_cell(int bx, int by, int bz)
            (size_t)(bx + TF_GRID_HALF);
 }
 
+// the cell of a block the hash now holds (allocation, reallocation after a swap-out)
+__device__ __forceinline__ void grid_set(int2* grid, const TfHashEntry& e, int idx)
+{
+    if (e.ptr >= 0 && tf_grid_in(e.x, e.y, e.z)) grid[tf_grid_cell(e.x, e.y, e.z)] = make_int2(idx, e.ptr * TF_BLK3);
+}
+
 // wave64 butterfly sum that reproduces the reference's halving tree bit for bit
 // (temp_utils.hpp:503-523 for lanes 0..63 after the cross-wave steps)
 __device__ __forceinline__ float tf_wave_tree64(float b)
@@ -254,6 +263,11 @@ struct tf_ctx {
     TfVoxel* vba_guard;      // allocation: one guard block of Voxel_s() (TF_VOFF_NONE reads), then vba
     int* allocList;
     int2* bgrid;             // block grid (TF_GRID_*), mirrors the hash
+    // swapping (p.use_swapping): the GlobalCache in HBM (GlobalCache.hpp:11-134)
+    unsigned char* swapState;    // HashSwapState::state per entry
+    unsigned char* swapFlags;    // hasStoredData per entry
+    TfVoxel* swapStore;          // storedVoxelBlocks: 512 voxels per entry
+    int* swapCounts;             // per 4096-entry chunk: [swap-in candidates, swap-out candidates]
     // SceneReconstructionEngine temporaries
     unsigned char* allocType;
     int* winnerKey;          // per-entry last-writer key (pixel*64+step), replaces blockCoords races
@@ -347,5 +361,9 @@ hipError_t tfk_icp_maps_end(tf_ctx* c, int slot);
 hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0);
 #define TF_ED_BLOCKS 256         // workgroups of the expected-depth projection pass
 hipError_t tfk_frame0_matrices(tf_ctx* c);
+// swapping (tf_swap.hip): reallocation of listed swapped-out entries (after the visible list),
+// and IntegrateGlobalIntoLocal + SaveToGlobalMemory (after integration)
+hipError_t tfk_swap_realloc(tf_ctx* c);
+hipError_t tfk_swap(tf_ctx* c);
 
 enum { TF_POSE_ALLOC = 1, TF_POSE_RAY = 2, TF_POSE_ALLOC_NOINV = 4 };

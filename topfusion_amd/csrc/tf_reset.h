@@ -13,6 +13,8 @@ struct ResetArgs {
     int on_failure;                  // frame end: bookkeeping always, the reset only if ICP failed
     int* frame_ok; int* frame_mode; int slot;
     int full;                        // clear everything (else only what the frames wrote)
+    unsigned char* swapState;        // swapping: GlobalCache states / stored flags, cleared with a reset
+    unsigned char* swapFlags;
 };
 
 // Runs as workgroup `bid` of `nblk` (256 threads): its own launch (k_reset_scene) or the
@@ -76,6 +78,12 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
             }
         }
     }
+    if (r.swapState) {                       // the GlobalCache of the old scene goes with it
+        for (size_t i = tid; i < (size_t)n_total / 16; i += stride) {
+            ((uint4*)r.swapState)[i] = make_uint4(0, 0, 0, 0);
+            ((uint4*)r.swapFlags)[i] = make_uint4(0, 0, 0, 0);
+        }
+    }
     for (size_t i0 = tid; i0 < (size_t)n_total; i0 += 8 * stride) {   // 8 entry loads in flight per lane
         TfHashEntry o[8];
 #pragma unroll
@@ -88,7 +96,7 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
             const size_t i = i0 + k * stride;
             // live entries (only they differ from e)
             if (i < (size_t)n_total && (full || o[k].ptr >= 0)) {
-                if (o[k].ptr >= 0 && tf_grid_in(o[k].x, o[k].y, o[k].z))
+                if (o[k].ptr >= 0 && tf_grid_in(o[k].x, o[k].y, o[k].z))   // (swapped-out entries have no cell)
                     grid[tf_grid_cell(o[k].x, o[k].y, o[k].z)] = make_int2(-1, TF_VOFF_NONE);
                 hash[i] = e;
             }

@@ -50,6 +50,12 @@ void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot)
     r->frame_ok = on_failure ? c->frame_ok : nullptr; r->frame_mode = on_failure ? c->frame_mode : nullptr;
     r->slot = on_failure ? slot : 0;
     r->full = on_failure ? 0 : 1;       // (+ st->scene_external, read on the device)
+    // swapping: swap-outs push blocks back onto the free list in any order, so its identity (which
+    // the clear-what-was-written reset relies on) no longer holds -- every reset is full, and
+    // also empties the GlobalCache (swap states, stored flags)
+    r->swapState = c->p.use_swapping ? c->swapState : nullptr;
+    r->swapFlags = c->p.use_swapping ? c->swapFlags : nullptr;
+    if (c->p.use_swapping) r->full = 1;
 }
 
 hipError_t tfk_reset_scene(tf_ctx* c)
@@ -71,10 +77,6 @@ hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot)
     return hipGetLastError();
 }
 
-__device__ __forceinline__ void grid_set(int2* grid, const TfHashEntry& e, int idx)
-{
-    if (e.ptr >= 0 && tf_grid_in(e.x, e.y, e.z)) grid[tf_grid_cell(e.x, e.y, e.z)] = make_int2(idx, e.ptr * TF_BLK3);
-}
 
 __global__ void k_grid_build(const TfHashEntry* __restrict__ hash, int n_total, int2* __restrict__ grid)
 {
@@ -488,7 +490,8 @@ k_alloc_discard(TfDevState* __restrict__ st, const int* __restrict__ counts, uns
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
-            unsigned char* __restrict__ visType, int* __restrict__ counts, int* __restrict__ allocCounts)
+            unsigned char* __restrict__ visType, int* __restrict__ counts, int* __restrict__ allocCounts,
+            unsigned char* __restrict__ swapState)
 {
     if (st->abort) return;
     if (threadIdx.x == 0) {
@@ -517,6 +520,21 @@ k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restric
             cnt += t > 0;
         }
         if (dirty) *(uint4*)(visType + base) = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
+        if (swapState) {
+            // buildVisibleList_device<true> (SceneReconstructionEngine_host.cu:466-469): every
+            // listed entry not already in active memory (state 2) becomes "needed" (1)
+            unsigned long long slo, shi;
+            load16(swapState + base, &slo, &shi);
+            bool sdirty = false;
+            for (int i = 0; i < 16; ++i) {
+                if (byte16(lo, hi, i) > 0 && byte16(slo, shi, i) != 2 && byte16(slo, shi, i) != 1) {
+                    if (i < 8) slo = (slo & ~(0xffull << (8 * i))) | (1ull << (8 * i));
+                    else shi = (shi & ~(0xffull << (8 * (i - 8)))) | (1ull << (8 * (i - 8)));
+                    sdirty = true;
+                }
+            }
+            if (sdirty) *(uint4*)(swapState + base) = make_uint4((unsigned)slo, (unsigned)(slo >> 32), (unsigned)shi, (unsigned)(shi >> 32));
+        }
     }
     int tot = block_sum(cnt);
     if (threadIdx.x == 0) counts[blockIdx.x] = tot;
@@ -576,6 +594,10 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch, int onl
     v.fx = c->p.fx; v.fy = c->p.fy; v.cx = c->p.cx; v.cy = c->p.cy;
     v.factor = (float)TF_BLK * c->p.voxelSize;
     v.W = c->W; v.H = c->H; v.n_total = c->n_total; v.cap = c->p.vis_capacity;
+    // swapping (SceneReconstructionEngine_host.cu:159-160, never with onlyUpdateVisibleList):
+    // the enlarged frustum for the previous list, swap states marked, swapped-out entries reallocated
+    const bool swapping = c->p.use_swapping && !only_update;
+    v.enlarged = swapping ? 1 : 0;
     if (snapshot != 2)   // 2: the frame's ICP launch has done it (tfk_icp fold_t3)
         hipLaunchKernelGGL(k_set_type3, dim3(256), dim3(256), 0, c->stream, v, c->st, c->hash, c->visibleIds, c->visType,
                            (const float2*)c->range, snapshot ? (float2*)c->range_render : nullptr);
@@ -598,9 +620,10 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch, int onl
                            c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
                            c->requestList, c->n_total);
     hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
-                       c->visCounts, c->allocCounts);
+                       c->visCounts, c->allocCounts, swapping ? c->swapState : nullptr);
     hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
                        c->visCounts, c->visType, c->visibleIds);
+    if (swapping) return tfk_swap_realloc(c);      // reAllocateSwappedOutVoxelBlocks (:184-189)
     return hipGetLastError();
 }
 

@@ -12,8 +12,12 @@ struct VisArgs {
     float factor;                 // (float)SDF_BLOCK_SIZE * voxelSize
     int W, H;
     int n_total, cap;
+    int enlarged;                 // swapping: checkPointVisibility<true>'s enlarged frustum
 };
 
+// isVisible, or with v.enlarged (swapping) isVisibleEnlarged: the image grown by an eighth of its
+// size on every side, integer limits (SceneReconstructionEngine.hpp:315-321); a point inside the
+// image is inside the enlarged frame too, so "any corner enlarged-visible" is the flag
 __device__ __forceinline__ bool vis_point(const float* M, const float* pt, const VisArgs& v)
 {
     float b[4];
@@ -21,6 +25,10 @@ __device__ __forceinline__ bool vis_point(const float* M, const float* pt, const
     if (b[2] < 1e-10f) return false;
     float bx = v.fx * b[0] / b[2] + v.cx;
     float by = v.fy * b[1] / b[2] + v.cy;
+    if (v.enlarged) {
+        const int lx = -v.W / 8, ux = v.W + v.W / 8, ly = -v.H / 8, uy = v.H + v.H / 8;
+        return bx >= (float)lx && bx < (float)ux && by >= (float)ly && by < (float)uy;
+    }
     return bx >= 0 && bx < (float)v.W && by >= 0 && by < (float)v.H;
 }
 

@@ -229,6 +229,32 @@ class TopFu:
         L.check(L.load().tf_set_counters(self._h, lastFreeBlockId, lastFreeExcessListId, noVisibleEntries),
                 "tf_set_counters")
 
+    # swapping (GlobalCache in HBM)
+    def swap(self):
+        """The swapping engine once (IntegrateGlobalIntoLocal + SaveToGlobalMemory)."""
+        L.check(L.load().tf_scene_swap(self._h), "tf_scene_swap")
+
+    def swap_counts(self):
+        """(swapped in, swapped out, reallocated) blocks of the last frame / call."""
+        out = np.zeros(3, np.int32)
+        L.check(L.load().tf_swap_counts(self._h, _ptr(out)), "tf_swap_counts")
+        return tuple(int(v) for v in out)
+
+    def swap_state(self):
+        return self.download(L.TF_BUF_SWAP_STATE)
+
+    def swap_stored_flags(self):
+        return self.download(L.TF_BUF_SWAP_STORED_FLAGS)
+
+    def swap_stored(self):
+        return self.download(L.TF_BUF_SWAP_STORED).view(VOXEL_DTYPE)
+
+    def swap_save(self, path):
+        L.check(L.load().tf_swap_save(self._h, str(path).encode()), "tf_swap_save")
+
+    def swap_load(self, path):
+        L.check(L.load().tf_swap_load(self._h, str(path).encode()), "tf_swap_load")
+
     # typed views
     def hash(self):
         return self.download(L.TF_BUF_HASH).view(HASH_DTYPE)
