@@ -331,6 +331,10 @@ class Oracle:
         return img
 
     # swapping state (GlobalCache)
+    def swap(self):
+        """The swapping engine once (IntegrateGlobalIntoLocal + SaveToGlobalMemory)."""
+        self.L.tfo_swap(self.ctx)
+
     def swap_counts(self):
         """Last frame's (swapped in, swapped out, reallocated) block counts."""
         out = np.zeros(3, np.int32)

@@ -572,6 +572,7 @@ static void reset_scene(tfo_ctx* c)
     c->lastFreeExcessListId = c->p.n_excess - 1;
     /* the reference's ResetScene leaves a GlobalCache alone (its swapping is never enabled);
        here a reset also empties it, so no block of the old scene is swapped into the new one */
+    memset(c->swap_counts, 0, sizeof(c->swap_counts));   /* a reset transfers nothing */
     if (c->p.use_swapping) {
         memset(c->swapState, 0, (size_t)c->n_total);
         memset(c->hasStored, 0, (size_t)c->n_total);

@@ -111,6 +111,7 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
     if (last_s && threadIdx.x == 0) {
         st->reset_ticket = 0;
         st->scene_external = 0;
+        st->swap_in = 0; st->swap_out = 0; st->swap_realloc = 0;   // a reset frame transfers nothing
         st->lastFreeBlockId = n_blocks - 1;
         st->lastFreeExcessListId = n_excess - 1;
     }

@@ -265,7 +265,7 @@ k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEnt
         for (int j = 0; j < 8; ++j) {
             const int i = i0 + j;
             if (i >= noSteps) break;
-            if (g[j].x >= 0) { visType[g[j].x] = 1; continue; }     // found (ptr >= 0; ptr == -1 never exists)
+            if (g[j].x >= 0) { visType[g[j].x] = 1; continue; }     // found, ptr >= 0 (swapped-out entries have no cell: the probe finds them)
             alloc_probe(a, hash, allocType, visType, winnerKey, counts, sbx[j], sby[j], sbz[j], key0 + i);
         }
     }
@@ -624,6 +624,8 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch, int onl
     hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
                        c->visCounts, c->visType, c->visibleIds);
     if (swapping) return tfk_swap_realloc(c);      // reAllocateSwappedOutVoxelBlocks (:184-189)
+    if (c->p.use_swapping)                         // (an onlyUpdateVisibleList pass reallocates nothing)
+        return hipMemsetAsync(&c->st->swap_realloc, 0, sizeof(int), c->stream);
     return hipGetLastError();
 }
 

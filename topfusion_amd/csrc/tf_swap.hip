@@ -62,17 +62,22 @@ __device__ __forceinline__ int sw_excl_scan(int v, int* total)
 }
 
 // ---------------------------------------------------------------------------------------
-// reAllocateSwappedOutVoxelBlocks_device (SceneReconstructionEngine_host.cu:417-432): listed
-// entries whose block was swapped out (ptr == -1) take blocks from the free list in ascending
-// index order (the visible list is in that order); once it is empty the rest keep ptr -1.
-// One workgroup.
+// reAllocateSwappedOutVoxelBlocks_device (SceneReconstructionEngine_host.cu:417-432): entries of
+// visible type > 0 whose block was swapped out (ptr == -1) take blocks from the free list in
+// ascending index order; once it is empty the rest keep ptr -1.  One workgroup over the visible
+// list (ascending, so its serial free-list order is a block prefix sum); when the list is full
+// (noVisibleEntries == cap: entries past the capacity may be of type > 0 without being listed,
+// and the reference's pass covers every entry) it walks visType over the whole table instead.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
 k_swap_realloc(TfDevState* __restrict__ st, TfHashEntry* __restrict__ hash, const int* __restrict__ visibleIds,
-               const int* __restrict__ allocList, int2* __restrict__ grid)
+               const unsigned char* __restrict__ visType, const int* __restrict__ allocList, int2* __restrict__ grid,
+               int cap, int n_total)
 {
     if (st->abort) return;
-    const int n = st->noVisibleEntries;
+    const int nv = st->noVisibleEntries;
+    const bool full = nv >= cap;
+    const int n = full ? n_total : nv;
     int v = st->lastFreeBlockId;                // uniform: every thread reads it before any write
     int done = 0;
     for (int i0 = 0; i0 < n; i0 += 256) {
@@ -80,8 +85,8 @@ k_swap_realloc(TfDevState* __restrict__ st, TfHashEntry* __restrict__ hash, cons
         int id = -1;
         bool need = false;
         if (i < n) {
-            id = visibleIds[i];
-            need = hash[id].ptr == -1;
+            id = full ? i : visibleIds[i];
+            need = (!full || visType[id] > 0) && hash[id].ptr == -1;
         }
         int cnt;
         const int r = sw_excl_scan(need ? 1 : 0, &cnt);
@@ -267,7 +272,8 @@ k_swap_out(TfDevState* __restrict__ st, unsigned char* __restrict__ swapState, u
 
 hipError_t tfk_swap_realloc(tf_ctx* c)
 {
-    hipLaunchKernelGGL(k_swap_realloc, dim3(1), dim3(256), 0, c->stream, c->st, c->hash, c->visibleIds, c->allocList, c->bgrid);
+    hipLaunchKernelGGL(k_swap_realloc, dim3(1), dim3(256), 0, c->stream, c->st, c->hash, c->visibleIds, c->visType,
+                       c->allocList, c->bgrid, c->p.vis_capacity, c->n_total);
     return hipGetLastError();
 }
 
