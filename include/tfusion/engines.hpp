@@ -58,29 +58,81 @@ namespace tfusion
         enum RenderRaycastSelection { RENDER_FROM_NEW_RAYCAST, RENDER_FROM_OLD_RAYCAST, RENDER_FROM_OLD_FORWARDPROJ };
     };
 
+    // HashSwapState (GlobalCache.hpp:11-20): 0 data on the host side only, 1 in both (not yet
+    // combined), 2 most recent in active memory
+    struct HashSwapState { unsigned char state; };
+
+    // GlobalCache<TVoxel> (GlobalCache.hpp:22-134): a view of the scene context's cache, which
+    // lives in HBM next to the active voxel blocks, not in host memory;
+    // the accessors copy out.  The transfer buffers of the reference (synced blocks, needed ids)
+    // have no counterpart: a transfer is a device-side copy.
+    template <class TVoxel>
+    class GlobalCache
+    {
+    public:
+        int noTotalEntries;
+
+        explicit GlobalCache(tf_ctx* ctx) : noTotalEntries(0), ctx_(ctx)
+        {
+            tf_params p;
+            tf_engine_check(tf_get_params(ctx, &p), "GlobalCache: tf_get_params");
+            noTotalEntries = p.n_buckets + p.n_excess;
+        }
+        bool HasStoredData(int address) const { return byte_at(TF_BUF_SWAP_STORED_FLAGS, address) != 0; }
+        // the stored block of an entry (SDF_BLOCK_SIZE3 voxels) copied into `out`
+        void GetStoredVoxelBlock(int address, TVoxel* out) const
+        {
+            size_t n = 0;
+            tf_engine_check(tf_buffer_bytes(ctx_, TF_BUF_SWAP_STORED, 0, &n), "tf_buffer_bytes");
+            const size_t blk = sizeof(TVoxel) * 512;
+            if (address < 0 || address >= noTotalEntries) throw std::out_of_range("GetStoredVoxelBlock");
+            tf_engine_check(tf_download_range(ctx_, TF_BUF_SWAP_STORED, (size_t)address * blk, out, blk),
+                            "GetStoredVoxelBlock");
+        }
+        HashSwapState GetSwapState(int address) const { return HashSwapState{ byte_at(TF_BUF_SWAP_STATE, address) }; }
+        void SaveToFile(const char* fileName) const { tf_engine_check(tf_swap_save(ctx_, fileName), "SaveToFile"); }
+        void ReadFromFile(const char* fileName) { tf_engine_check(tf_swap_load(ctx_, fileName), "ReadFromFile"); }
+
+    private:
+        unsigned char byte_at(int which, int address) const
+        {
+            if (address < 0 || address >= noTotalEntries) throw std::out_of_range("GlobalCache entry");
+            unsigned char b = 0;
+            tf_engine_check(tf_download_range(ctx_, which, (size_t)address, &b, 1), "GlobalCache");
+            return b;
+        }
+        tf_ctx* ctx_;
+    };
+
     // Scene<TVoxel, TIndex> (scene.hpp:13-44): owns the context
     template <class TVoxel, class TIndex>
     class Scene
     {
     public:
         const SceneParams* sceneParams;
+        GlobalCache<TVoxel>* globalCache = nullptr;     // scene.hpp:27, set when useSwapping
 
         // scene.hpp:29-34; `frame` (an addition, defaulted) gives the image size, intrinsics and
-        // capacities the context is created with
+        // capacities the context is created with; useSwapping sets tf_params::use_swapping
         Scene(const SceneParams* params, bool useSwapping, const TopFuParams& frame = TopFuParams::default_params())
             : sceneParams(params)
         {
-            if (useSwapping) throw std::invalid_argument("Scene: the swapping GlobalCache is not enabled on this path");
             TopFuParams tp = frame;
             tf_params c = tp.to_c();
             if (params) {
                 c.mu = params->mu; c.maxW = params->maxW; c.voxelSize = params->voxelSize;
                 c.viewFrustum_min = params->viewFrustum_min; c.viewFrustum_max = params->viewFrustum_max;
             }
+            c.use_swapping = useSwapping ? 1 : 0;
             tf_engine_check(tf_create(&c, &ctx_), "Scene: tf_create");
             intr_ = tp.intr;
+            if (useSwapping) globalCache = new GlobalCache<TVoxel>(ctx_);
         }
-        ~Scene() { tf_destroy(ctx_); }
+        ~Scene()
+        {
+            delete globalCache;
+            tf_destroy(ctx_);
+        }
         Scene(const Scene&) = delete;
         Scene& operator=(const Scene&) = delete;
 
@@ -156,6 +208,25 @@ namespace tfusion
             detail::intr4(intr, in);
             detail::rt_of(pose, rt);
             tf_engine_check(tf_scene_integrate(scene->context(), in, rt, dist.ptr(), dist.step()), "IntegrateIntoScene");
+        }
+    };
+
+    // SwappingEngine_CUDA<TVoxel, TIndex>: the engine of the GlobalCache's lineage (InfiniTAM
+    // ITMSwappingEngine_CUDA; its instantiation is commented out in the reference,
+    // CUDAInstantiations.cu:8), called after IntegrateIntoScene on a swapping scene
+    template <class TVoxel, class TIndex>
+    class SwappingEngine_CUDA
+    {
+    public:
+        // stored blocks of the entries marked "needed" (state 1) merged into their active blocks
+        void IntegrateGlobalIntoLocal(Scene<TVoxel, TIndex>* scene, RenderState* = nullptr)
+        {
+            tf_engine_check(tf_scene_swap_in(scene->context()), "IntegrateGlobalIntoLocal");
+        }
+        // active blocks not visible this frame moved to the cache, their VBA blocks freed
+        void SaveToGlobalMemory(Scene<TVoxel, TIndex>* scene, RenderState* = nullptr)
+        {
+            tf_engine_check(tf_scene_swap_out(scene->context()), "SaveToGlobalMemory");
         }
     };
 

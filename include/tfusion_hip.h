@@ -217,6 +217,10 @@ tf_status tf_scene_integrate(tf_ctx* ctx, const float intr[4], const float pose_
  * (InfiniTAM ITMSwappingEngine_CUDA, whose instantiation the reference comments out,
  * CUDAInstantiations.cu:8); its semantics are written out in DESIGN.md §Swapping. */
 tf_status tf_scene_swap(tf_ctx* ctx);
+/* the two halves on their own: SwappingEngine::IntegrateGlobalIntoLocal(scene, renderState) and
+ * ::SaveToGlobalMemory(scene, renderState); tf_scene_swap == swap_in then swap_out */
+tf_status tf_scene_swap_in(tf_ctx* ctx);
+tf_status tf_scene_swap_out(tf_ctx* ctx);
 /* blocks swapped in / out and reallocated by the last frame (or tf_scene_* call) */
 tf_status tf_swap_counts(tf_ctx* ctx, int counts[3]);
 /* GlobalCache::SaveToFile / ReadFromFile (GlobalCache.hpp:79-110): hasStoredData as one byte per
@@ -267,6 +271,8 @@ tf_status tf_imgproc_sync(void* stream);
  * TF_BUF_PREV_NORMALS.  bytes must equal the buffer size (tf_buffer_bytes). */
 tf_status tf_buffer_bytes(tf_ctx* ctx, int which, int level, size_t* bytes);
 tf_status tf_download(tf_ctx* ctx, int which, int level, void* host, size_t bytes);
+/* bytes [offset, offset + bytes) of a level-0 buffer (one entry of a large table) */
+tf_status tf_download_range(tf_ctx* ctx, int which, size_t offset, void* host, size_t bytes);
 tf_status tf_upload(tf_ctx* ctx, int which, int level, const void* host, size_t bytes);
 tf_status tf_set_pose(tf_ctx* ctx, const float rt[12]);
 

@@ -55,8 +55,7 @@ def lib(omp=False):
     every result identical, tests/test_oracle.py)."""
     if omp not in _libs:
         path = _LIB_OMP if omp else _LIB
-        if not os.path.exists(path):
-            build(omp)
+        build(omp)                  # make: a no-op unless the sources are newer
         L = ctypes.CDLL(path)
         P = ctypes.c_void_p
         L.tfo_default_params.argtypes = [ctypes.POINTER(Params)]
@@ -95,6 +94,8 @@ def lib(omp=False):
         L.tfo_render_type.argtypes = [P, P, ctypes.c_int, P]
         L.tfo_render_image_type.argtypes = [P, ctypes.c_int]
         L.tfo_swap.argtypes = [P]
+        L.tfo_swap_in.argtypes = [P]
+        L.tfo_swap_out.argtypes = [P]
         L.tfo_swap_counts.argtypes = [P, P]
         for name in ("tfo_hash", "tfo_vba", "tfo_visible_ids", "tfo_visible_type", "tfo_range_image",
                      "tfo_raycast_result", "tfo_dists", "tfo_frame_grey", "tfo_swap_state", "tfo_swap_stored_flags",
@@ -334,6 +335,12 @@ class Oracle:
     def swap(self):
         """The swapping engine once (IntegrateGlobalIntoLocal + SaveToGlobalMemory)."""
         self.L.tfo_swap(self.ctx)
+
+    def swap_in(self):
+        self.L.tfo_swap_in(self.ctx)
+
+    def swap_out(self):
+        self.L.tfo_swap_out(self.ctx)
 
     def swap_counts(self):
         """Last frame's (swapped in, swapped out, reallocated) block counts."""

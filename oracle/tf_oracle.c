@@ -914,12 +914,12 @@ static inline void combine_voxel(const tfo_voxel* src, tfo_voxel* dst, int maxW)
     dst->sdf = (int16_t)(newF * 32767.0f);
 }
 
-void tfo_swap(tfo_ctx* c)
+void tfo_swap_in(tfo_ctx* c)                                            /* IntegrateGlobalIntoLocal */
 {
     if (!c->p.use_swapping) return;
     const int T = c->p.swap_transfer_blocks;
-    int n_in = 0, n_out = 0;
-    for (int t = 0; t < c->n_total && n_in < T; ++t) {                 /* IntegrateGlobalIntoLocal */
+    int n_in = 0;
+    for (int t = 0; t < c->n_total && n_in < T; ++t) {
         if (c->swapState[t] != 1 || c->hash[t].ptr < 0) continue;
         if (c->hasStored[t]) {
             tfo_voxel* dst = c->vba + (size_t)c->hash[t].ptr * BLK3;
@@ -929,7 +929,15 @@ void tfo_swap(tfo_ctx* c)
         c->swapState[t] = 2;
         n_in++;
     }
-    for (int t = 0; t < c->n_total && n_out < T; ++t) {                /* SaveToGlobalMemory */
+    c->swap_counts[0] = n_in;
+}
+
+void tfo_swap_out(tfo_ctx* c)                                           /* SaveToGlobalMemory */
+{
+    if (!c->p.use_swapping) return;
+    const int T = c->p.swap_transfer_blocks;
+    int n_out = 0;
+    for (int t = 0; t < c->n_total && n_out < T; ++t) {
         if (c->swapState[t] != 2 || c->hash[t].ptr < 0 || c->visType[t] != 0) continue;
         tfo_voxel* blk = c->vba + (size_t)c->hash[t].ptr * BLK3;
         memcpy(c->stored + (size_t)t * BLK3, blk, sizeof(tfo_voxel) * BLK3);   /* moveActiveDataToTransferBuffer */
@@ -943,8 +951,13 @@ void tfo_swap(tfo_ctx* c)
         }
         n_out++;
     }
-    c->swap_counts[0] = n_in;
     c->swap_counts[1] = n_out;
+}
+
+void tfo_swap(tfo_ctx* c)
+{
+    tfo_swap_in(c);
+    tfo_swap_out(c);
 }
 
 void tfo_swap_counts(const tfo_ctx* c, int out[3]) { memcpy(out, c->swap_counts, sizeof(int) * 3); }

@@ -144,6 +144,8 @@ void tfo_render_grey(tfo_ctx* c, const float invM_rt[12], uint8_t* rgba);     /*
 void tfo_render_image(tfo_ctx* c, uint8_t* rgba);                              /* TopFu::renderImage */
 /* swapping (GlobalCache + the InfiniTAM-lineage swapping engine, see tf_oracle.c) */
 void tfo_swap(tfo_ctx* c);                          /* IntegrateGlobalIntoLocal + SaveToGlobalMemory */
+void tfo_swap_in(tfo_ctx* c);                       /* IntegrateGlobalIntoLocal */
+void tfo_swap_out(tfo_ctx* c);                      /* SaveToGlobalMemory */
 void tfo_swap_counts(const tfo_ctx* c, int out[3]);  /* last frame: swapped in, swapped out, reallocated */
 uint8_t* tfo_swap_state(tfo_ctx* c);                /* HashSwapState::state per entry */
 uint8_t* tfo_swap_stored_flags(tfo_ctx* c);         /* GlobalCache hasStoredData per entry */

@@ -44,6 +44,25 @@ def test_engine_api_builds_and_links():
         assert fn in syms, fn
 
 
+def test_swap_api_builds_and_links():
+    exe = _build("swap_check")
+    syms = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True, check=True).stdout
+    for fn in ("tf_scene_swap_in", "tf_scene_swap_out", "tf_swap_save", "tf_swap_load", "tf_download_range"):
+        assert fn in syms, fn
+
+
+@pytest.mark.gpu
+def test_swap_api_runs(tmp_path):
+    """apps/swap_check: a swapping Scene over the engine API (SwappingEngine_CUDA's two calls
+    after allocation + integration), free-list bookkeeping every frame, GlobalCache
+    SaveToFile / ReadFromFile into a second scene."""
+    exe = _build("swap_check")
+    r = subprocess.run([exe, str(tmp_path / "cache.bin")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = re.search(r"swapped in (\d+) out (\d+) stored (\d+): MATCH", r.stdout)
+    assert m and int(m.group(2)) > 0 and int(m.group(3)) > 0, r.stdout
+
+
 @pytest.mark.gpu
 def test_engine_api_matches_topfu():
     """apps/engine_check: TopFu::operator() against the same frames spelled out over the L4

@@ -75,13 +75,15 @@ def _invariants(h, n_blocks, last_free, flags, state):
     assert (state[out] != 2).all(), "a swapped-out entry marked active"
 
 
-@pytest.mark.parametrize("n_blocks,transfer", [(8192, 1024), (2600, 96)])
-def test_swapping_engine_path(oracle_mod, n_blocks, transfer):
+@pytest.mark.parametrize("n_blocks,transfer,split", [(8192, 1024, False), (2600, 96, False), (2600, 96, True)])
+def test_swapping_engine_path(oracle_mod, n_blocks, transfer, split):
     """A camera turning in place through 400 deg and back (40 deg a frame, ground-truth poses)
     over SceneReconstructionEngine_CUDA::{AllocateSceneFromDepth, IntegrateIntoScene} + the
     swapping engine, with a VBA too small for the room (blocks must be evicted to make room)
     and a transfer cap below the per-frame demand (backlogs carry over).  The small case also
-    runs the free list dry, so swapped-out entries stay without a block (state 1, ptr -1)."""
+    runs the free list dry, so swapped-out entries stay without a block (state 1, ptr -1).
+    split: IntegrateGlobalIntoLocal and SaveToGlobalMemory as two calls (tf_scene_swap_in /
+    _out, as a SwappingEngine caller makes them) against the oracle's two halves."""
     import ctypes
     from topfusion_amd import _lib
     L = _lib.load()
@@ -106,8 +108,15 @@ def test_swapping_engine_path(oracle_mod, n_blocks, transfer):
         o.integrate(w2c, dd)
         flags_before = o.swap_stored_flags()
         state_before = o.swap_state()
-        g.swap()
-        o.swap()
+        if split:
+            g.swap_in()
+            o.swap_in()
+            assert g.swap_counts()[0] == o.swap_counts()[0], f"frame {k} swapped in"
+            g.swap_out()
+            o.swap_out()
+        else:
+            g.swap()
+            o.swap()
         cg, co = g.swap_counts(), o.swap_counts()
         assert cg == co, f"frame {k} ({deg} deg) swap counts (in, out, realloc): gpu {cg} oracle {co}"
         tot += co

@@ -117,6 +117,7 @@ def load():
         "tf_stage_swap_pyramids": ([P], I),
         "tf_buffer_bytes": ([P, I, I, ctypes.POINTER(S)], I),
         "tf_download": ([P, I, I, P, S], I),
+        "tf_download_range": ([P, I, S, P, S], I),
         "tf_upload": ([P, I, I, P, S], I),
         "tf_set_pose": ([P, P], I),
         "tf_set_counters": ([P, I, I, I], I),
@@ -129,6 +130,8 @@ def load():
         "tf_scene_integrate": ([P, P, P, P, S], I),
         "tf_vis_expected_depths": ([P, P, P], I),
         "tf_scene_swap": ([P], I),
+        "tf_scene_swap_in": ([P], I),
+        "tf_scene_swap_out": ([P], I),
         "tf_swap_counts": ([P, P], I),
         "tf_swap_save": ([P, ctypes.c_char_p], I),
         "tf_swap_load": ([P, ctypes.c_char_p], I),

@@ -855,15 +855,19 @@ extern "C" tf_status tf_scene_integrate(tf_ctx* c, const float intr[4], const fl
     return TF_OK;
 }
 
-extern "C" tf_status tf_scene_swap(tf_ctx* c)
+static tf_status scene_swap(tf_ctx* c, int which)
 {
     if (!c) return TF_INVALID_ARG;
     if (!c->p.use_swapping) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));
-    TF_CHECK(tfk_swap(c));
+    TF_CHECK(tfk_swap(c, which));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }
+
+extern "C" tf_status tf_scene_swap(tf_ctx* c) { return scene_swap(c, 3); }
+extern "C" tf_status tf_scene_swap_in(tf_ctx* c) { return scene_swap(c, 1); }
+extern "C" tf_status tf_scene_swap_out(tf_ctx* c) { return scene_swap(c, 2); }
 
 extern "C" tf_status tf_swap_counts(tf_ctx* c, int counts[3])
 {
@@ -1001,6 +1005,17 @@ extern "C" tf_status tf_download(tf_ctx* c, int which, int level, void* host, si
     void* p = buffer_ptr(c, which, level, &n);
     if (!p || n != bytes) return TF_INVALID_ARG;
     TF_CHECK(hipMemcpyAsync(host, p, n, hipMemcpyDeviceToHost, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
+extern "C" tf_status tf_download_range(tf_ctx* c, int which, size_t offset, void* host, size_t bytes)
+{
+    if (!c || !host) return TF_INVALID_ARG;
+    size_t n;
+    void* p = buffer_ptr(c, which, 0, &n);
+    if (!p || offset > n || bytes > n - offset) return TF_INVALID_ARG;
+    TF_CHECK(hipMemcpyAsync(host, (const char*)p + offset, bytes, hipMemcpyDeviceToHost, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }

@@ -364,6 +364,6 @@ hipError_t tfk_frame0_matrices(tf_ctx* c);
 // swapping (tf_swap.hip): reallocation of listed swapped-out entries (after the visible list),
 // and IntegrateGlobalIntoLocal + SaveToGlobalMemory (after integration)
 hipError_t tfk_swap_realloc(tf_ctx* c);
-hipError_t tfk_swap(tf_ctx* c);
+hipError_t tfk_swap(tf_ctx* c, int which = 3);   // 1 in, 2 out, 3 both
 
 enum { TF_POSE_ALLOC = 1, TF_POSE_RAY = 2, TF_POSE_ALLOC_NOINV = 4 };

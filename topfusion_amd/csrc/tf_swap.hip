@@ -158,6 +158,7 @@ k_swap_in(TfDevState* __restrict__ st, unsigned char* __restrict__ swapState, co
     sw_excl_scan(all, &all);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->swap_in = all < T ? all : T;
+        st->tot_swap_in += all < T ? all : T;
         st->swap_free0 = st->lastFreeBlockId;            // for k_swap_out (nobody writes it in between)
     }
     const int base = blockIdx.x * SW_CHUNK + threadIdx.x * 16;
@@ -204,6 +205,29 @@ k_swap_in(TfDevState* __restrict__ st, unsigned char* __restrict__ swapState, co
     (void)tmp;
 }
 
+// swap-out candidates of a chunk, for a SaveToGlobalMemory on its own (k_swap_in counts them
+// when the two run together); also records the free-list top k_swap_out starts from
+__global__ void __launch_bounds__(256)
+k_swap_count_out(TfDevState* __restrict__ st, const unsigned char* __restrict__ swapState,
+                 const unsigned char* __restrict__ visType, const TfHashEntry* __restrict__ hash,
+                 int* __restrict__ counts, int n_total)
+{
+    if (st->abort) return;
+    const int base = blockIdx.x * SW_CHUNK + threadIdx.x * 16;
+    int c = 0;
+    if (base < n_total) {
+        unsigned long long lo, hi, vlo, vhi;
+        sw_load16(swapState + base, &lo, &hi);
+        sw_load16(visType + base, &vlo, &vhi);
+        for (int i = 0; i < 16; ++i)
+            if (sw_byte(lo, hi, i) == 2 && sw_byte(vlo, vhi, i) == 0 && hash[base + i].ptr >= 0) ++c;
+    }
+    int tot;
+    sw_excl_scan(c, &tot);
+    if (threadIdx.x == 0) counts[2 * blockIdx.x + 1] = tot;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->swap_free0 = st->lastFreeBlockId;
+}
+
 // SaveToGlobalMemory for the chunk's candidates of rank < T
 __global__ void __launch_bounds__(256)
 k_swap_out(TfDevState* __restrict__ st, unsigned char* __restrict__ swapState, unsigned char* __restrict__ swapFlags,
@@ -224,10 +248,8 @@ k_swap_out(TfDevState* __restrict__ st, unsigned char* __restrict__ swapState, u
     const int free0 = st->swap_free0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const int n_out = all < T ? all : T;
-        const int n_in = st->swap_in;
         st->swap_out = n_out;
         st->lastFreeBlockId = free0 + n_out;             // cleanMemory's increments, taken or not
-        st->tot_swap_in += n_in;
         st->tot_swap_out += n_out;
     }
     const int base = blockIdx.x * SW_CHUNK + threadIdx.x * 16;
@@ -277,14 +299,23 @@ hipError_t tfk_swap_realloc(tf_ctx* c)
     return hipGetLastError();
 }
 
-hipError_t tfk_swap(tf_ctx* c)
+// which: 1 = IntegrateGlobalIntoLocal, 2 = SaveToGlobalMemory, 3 = both (the frame's order)
+hipError_t tfk_swap(tf_ctx* c, int which)
 {
     const int nch = (c->n_total + SW_CHUNK - 1) / SW_CHUNK, T = c->p.swap_transfer_blocks;
-    hipLaunchKernelGGL(k_swap_count_in, dim3(nch), dim3(256), 0, c->stream, c->st, c->swapState, c->hash, c->swapCounts,
-                       c->n_total);
-    hipLaunchKernelGGL(k_swap_in, dim3(nch), dim3(256), 0, c->stream, c->st, c->swapState, c->swapFlags, c->swapStore,
-                       c->hash, c->vba, c->visType, c->swapCounts, nch, c->n_total, T, c->p.maxW);
-    hipLaunchKernelGGL(k_swap_out, dim3(nch), dim3(256), 0, c->stream, c->st, c->swapState, c->swapFlags, c->swapStore,
-                       c->hash, c->vba, c->visType, c->allocList, c->bgrid, c->swapCounts, nch, c->n_total, T, c->p.n_blocks);
+    if (which & 1) {
+        hipLaunchKernelGGL(k_swap_count_in, dim3(nch), dim3(256), 0, c->stream, c->st, c->swapState, c->hash, c->swapCounts,
+                           c->n_total);
+        hipLaunchKernelGGL(k_swap_in, dim3(nch), dim3(256), 0, c->stream, c->st, c->swapState, c->swapFlags, c->swapStore,
+                           c->hash, c->vba, c->visType, c->swapCounts, nch, c->n_total, T, c->p.maxW);
+    }
+    if (which & 2) {
+        if (!(which & 1))
+            hipLaunchKernelGGL(k_swap_count_out, dim3(nch), dim3(256), 0, c->stream, c->st, c->swapState, c->visType, c->hash,
+                               c->swapCounts, c->n_total);
+        hipLaunchKernelGGL(k_swap_out, dim3(nch), dim3(256), 0, c->stream, c->st, c->swapState, c->swapFlags, c->swapStore,
+                           c->hash, c->vba, c->visType, c->allocList, c->bgrid, c->swapCounts, nch, c->n_total, T,
+                           c->p.n_blocks);
+    }
     return hipGetLastError();
 }

@@ -234,6 +234,14 @@ class TopFu:
         """The swapping engine once (IntegrateGlobalIntoLocal + SaveToGlobalMemory)."""
         L.check(L.load().tf_scene_swap(self._h), "tf_scene_swap")
 
+    def swap_in(self):
+        """IntegrateGlobalIntoLocal alone."""
+        L.check(L.load().tf_scene_swap_in(self._h), "tf_scene_swap_in")
+
+    def swap_out(self):
+        """SaveToGlobalMemory alone."""
+        L.check(L.load().tf_scene_swap_out(self._h), "tf_scene_swap_out")
+
     def swap_counts(self):
         """(swapped in, swapped out, reallocated) blocks of the last frame / call."""
         out = np.zeros(3, np.int32)
