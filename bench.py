@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--cols", type=int, default=None)
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--voxel", type=float, default=None)
+    ap.add_argument("--swapping", action="store_true",
+                    help="a swapping scene (Scene(params, true)): enlarged-frustum visibility, the GlobalCache in HBM, "
+                         "blocks out of view evicted / brought back every frame (SURVEY §8f-2; C5 churn)")
+    ap.add_argument("--swap-transfer-blocks", type=int, default=0x1000,
+                    help="blocks moved per direction per frame (SDF_TRANSFER_BLOCK_NUM, VoxelBlockHash.hpp:27)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample length")
     ap.add_argument("--no-profile", action="store_true", help="disable the per-stage HIP-event timing")
@@ -399,6 +404,8 @@ def main():
     F = args.frames_per_step
     fx, fy, cx, cy = synth.intrinsics(W, H)
     pkw = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=args.voxel, **cfg["capacity"])
+    if args.swapping:
+        pkw.update(use_swapping=1, swap_transfer_blocks=args.swap_transfer_blocks)
     n_breakdown = 0 if args.no_profile else min(args.breakdown_frames, args.steps * F)
     n_frames = (args.warmup + args.steps) * F
     device = f"cuda:{local_rank}"
@@ -518,7 +525,8 @@ def main():
             nt = omp_threads()
             cpu = cpu_baseline_protocol(frames, pkw, args.cpu_seconds, nt)
         out = {
-            "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame",
+            "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame"
+                      + (" (swapping scene)" if args.swapping else ""),
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -538,7 +546,9 @@ def main():
                                f"frames resident in HBM",
                        "frames_per_step": F,
                        "cols": W, "rows": H, "voxel_m": args.voxel, "parallelism": f"replicas{world}",
-                       "capacity": cfg["capacity"] or "reference defaults"},
+                       "capacity": cfg["capacity"] or "reference defaults",
+                       "swapping": (f"on: GlobalCache in HBM, <= {args.swap_transfer_blocks} blocks per direction "
+                                    "per frame") if args.swapping else "off (topfu.cpp:67)"},
             "ms_per_frame": round(elapsed_max / total_steps_frames * 1000.0, 5),
             "per_call_frames_per_sec": None if per_call is None else round(per_call, 2),
             "per_call": (f"TopFu::operator() per call: tf_process_frame on {min(args.per_call_frames, n_frames)} frames, "
@@ -555,6 +565,8 @@ def main():
             "visible_blocks_last": st["noVisibleEntries"],
             "allocated_blocks_last": int(tf.params().n_blocks - 1 - st["lastFreeBlockId"]),
             "last_frame_ok": bool(ok[-1]),
+            "swapped_out_per_frame": round(tot["swapped_out"] / max(1, tot["frames"]), 2) if args.swapping else None,
+            "swapped_in_per_frame": round(tot["swapped_in"] / max(1, tot["frames"]), 2) if args.swapping else None,
             "roofline": roof,
             "hbm_stream_copy_GBs": stream_gbs,
             "roofline_stages": roof_all,

@@ -196,3 +196,34 @@ def test_swapping_batched_and_save_load(oracle_mod):
         assert_bit_exact("loaded store", g2.swap_stored().view(np.uint32), g.swap_stored().view(np.uint32))
         g2.close()
     g.close()
+
+
+def test_swapping_c5_random_walk(oracle_mod):
+    """C5 geometry (10 mm voxels, the seed-13 random walk) on a swapping scene whose VBA runs
+    out (2048 blocks): allocation saturates, out-of-view blocks are evicted to the cache at
+    the transfer cap, and the walk's ICP-failure resets (the reference's own, as without
+    swapping) empty it; every frame's result, counters, transfer counts and pose against the
+    oracle, the whole scene + GlobalCache after an eviction frame and at the end."""
+    W, H, n = 320, 240, 24
+    g, o = _pair(oracle_mod, W, H, voxelSize=0.01, n_blocks=2048, swap_transfer_blocks=256,
+                 n_buckets=0x10000, n_excess=0x4000)
+    seq = synth.random_walk_sequence(n, W, H, seed=13)
+    outs = 0
+    for k in range(n):
+        okg, oko = g(seq[k]), o(seq[k])
+        assert okg == oko, f"frame {k}: gpu {okg} oracle {oko}"
+        sg, so = g.last_stats, o.counters()
+        for key in ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries", "icp_iterations", "frame_counter",
+                    "n_resets"):
+            assert sg[key] == so[key], f"frame {k} {key}: gpu {sg[key]} oracle {so[key]}"
+        c = o.swap_counts()
+        assert g.swap_counts() == c, f"frame {k} swap counts: gpu {g.swap_counts()} oracle {c}"
+        outs += c[1]
+        assert_bit_exact(f"frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
+        if c[1] and o.swap_stored_flags().any():
+            _compare(g, o, f"frame {k} (evicted {c[1]})", stored=True)
+    _compare(g, o, "C5 swapping final", stored=True)
+    assert outs > 0 and o.counters()["n_resets"] >= 1
+    tg = g.totals()
+    assert tg["swapped_out"] == outs, (tg, outs)
+    g.close()
