@@ -61,7 +61,7 @@ typedef struct tf_params {
     int   use_swapping;
     int   swap_transfer_blocks;         /* SDF_TRANSFER_BLOCK_NUM (VoxelBlockHash.hpp:27): blocks per swap */
     /* colour: Voxel_s_rgb voxels (VoxelTypes.hpp:39-67) integrated from the RGB image */
-    int   voxel_rgb;
+    int   voxel_rgb;                    /* 1: Voxel_s_rgb (colour integrated by the *_rgb entry points) */
     float rgb_intr[4];                  /* projParams_rgb (fx, fy, cx, cy); all 0: the depth intrinsics */
     float depth_to_rgb[12];             /* calib_inv of trafo_rgb_to_depth, row-major [R|t]: M_rgb = it * M_d */
 } tf_params;
@@ -98,7 +98,9 @@ typedef enum tf_buffer {
     TF_BUF_GREY = 12,         /* uchar4[rows*cols] last renderImage output */
     TF_BUF_SWAP_STATE = 13,   /* uchar[n_buckets+n_excess] HashSwapState::state (GlobalCache.hpp:11-20) */
     TF_BUF_SWAP_STORED_FLAGS = 14,  /* uchar[n_buckets+n_excess] GlobalCache hasStoredData */
-    TF_BUF_SWAP_STORED = 15   /* Voxel_s[(n_buckets+n_excess)*512] GlobalCache storedVoxelBlocks */
+    TF_BUF_SWAP_STORED = 15,  /* Voxel_s[(n_buckets+n_excess)*512] GlobalCache storedVoxelBlocks */
+    TF_BUF_VBA_RGB = 16       /* voxel_rgb: uint32[n_blocks*512] Voxel_s_rgb clr + w_color (VoxelTypes.hpp:39-67),
+                                 r | g << 8 | b << 16 | w_color << 24 -- the colour half of each voxel */
 } tf_buffer;
 
 /* ---- device ---------------------------------------------------------------- */
@@ -130,6 +132,19 @@ tf_status tf_process_frame_host(tf_ctx* ctx, const uint16_t* host_depth, size_t 
  * frame.  ok_out (optional, n ints) receives each frame's bool. */
 tf_status tf_process_frames(tf_ctx* ctx, const uint16_t* dev_frames, size_t frame_stride_bytes, int n,
                             int* ok_out);
+/* TopFu::operator()(depth, image) (topfu.hpp:80) with the image integrated: with voxel_rgb set,
+ * each frame's uchar4 RGB image (rows x cols, pitch bytes; registered to the depth through
+ * rgb_intr / depth_to_rgb) updates the Voxel_s_rgb colour of the voxels near the surface
+ * (computeUpdatedVoxelColorInfo, SceneReconstructionEngine.hpp:116-148, where the lineage's
+ * ComputeUpdatedVoxelInfo<true, ...> calls it, :163-176).  dev_rgb null: as the depth-only call. */
+tf_status tf_process_frame_rgb(tf_ctx* ctx, const uint16_t* dev_depth, size_t pitch_bytes, const uint8_t* dev_rgb,
+                               size_t rgb_pitch_bytes, float pose_out[12], tf_stats* stats);
+/* same, host depth and host RGB (uploaded through the context's staging buffers) */
+tf_status tf_process_frame_rgb_host(tf_ctx* ctx, const uint16_t* host_depth, size_t pitch_bytes, const uint8_t* host_rgb,
+                                    size_t rgb_pitch_bytes, float pose_out[12], tf_stats* stats);
+/* the batch form: frame i's RGB image at dev_rgb_frames + i*rgb_stride_bytes (pitch cols*4) */
+tf_status tf_process_frames_rgb(tf_ctx* ctx, const uint16_t* dev_frames, size_t frame_stride_bytes,
+                                const uint8_t* dev_rgb_frames, size_t rgb_stride_bytes, int n, int* ok_out);
 /* TopFu::renderImage (tfusion/src/topfu.cpp:332-377): raycast + grey shading of the
  * current pose into dev_rgba (uchar4, rows x cols, pitch bytes). */
 tf_status tf_render_image(tf_ctx* ctx, uint8_t* dev_rgba, size_t pitch_bytes);
@@ -137,7 +152,8 @@ tf_status tf_render_image(tf_ctx* ctx, uint8_t* dev_rgba, size_t pitch_bytes);
 typedef enum tf_render_type {
     TF_RENDER_SHADED_GREYSCALE = 0,              /* renderGrey_device (SDF-gradient normals) */
     TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS = 1, /* renderGrey_ImageNormals_device<false> (raycast-image normals) */
-    TF_RENDER_COLOUR_FROM_VOLUME = 2,            /* Voxel_s has no colour: greyscale (VisualisationEngine_CUDA.cu:251-252) */
+    TF_RENDER_COLOUR_FROM_VOLUME = 2,            /* renderColour_device with voxel_rgb; Voxel_s has no colour: greyscale
+                                                    (VisualisationEngine_CUDA.cu:251-256) */
     TF_RENDER_COLOUR_FROM_NORMAL = 3,            /* renderColourFromNormal_device (alpha left as it was) */
     TF_RENDER_COLOUR_FROM_CONFIDENCE = 4         /* renderColourFromConfidence_device */
 } tf_render_type;
@@ -212,6 +228,10 @@ tf_status tf_scene_alloc(tf_ctx* ctx, const float intr[4], const float pose_rt[1
 /* ::IntegrateIntoScene(scene, intr, pose, dists, renderState) (SceneReconstructionEngine_host.cu:197-251) */
 tf_status tf_scene_integrate(tf_ctx* ctx, const float intr[4], const float pose_rt[12], const float* dists,
                              size_t dists_step);
+/* ::IntegrateIntoScene with the view's RGB image (voxel_rgb: the Voxel_s_rgb colour update;
+ * SceneReconstructionEngine_host.cu:217 M_rgb = calib_inv * M_d, :245-247 the rgb arguments) */
+tf_status tf_scene_integrate_rgb(tf_ctx* ctx, const float intr[4], const float pose_rt[12], const float* dists,
+                                 size_t dists_step, const uint8_t* dev_rgb, size_t rgb_step);
 /* The swapping engine of the GlobalCache's lineage, run after integration when use_swapping is
  * set (every frame of tf_process_frame(s) does it): IntegrateGlobalIntoLocal + SaveToGlobalMemory
  * (InfiniTAM ITMSwappingEngine_CUDA, whose instantiation the reference comments out,

@@ -86,6 +86,8 @@ def lib(omp=False):
         L.tfo_alloc.argtypes = [P, P, P]
         L.tfo_alloc_ex.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int]
         L.tfo_integrate.argtypes = [P, P, P]
+        L.tfo_integrate_rgb.argtypes = [P, P, P, P, ctypes.c_size_t]
+        L.tfo_process_frame_rgb.argtypes = [P, P, P, ctypes.c_size_t]; L.tfo_process_frame_rgb.restype = ctypes.c_int
         L.tfo_expected_depths.argtypes = [P, P]
         L.tfo_raycast.argtypes = [P, P, ctypes.c_int]
         L.tfo_render_icp.argtypes = [P, P, P, P]
@@ -99,7 +101,7 @@ def lib(omp=False):
         L.tfo_swap_counts.argtypes = [P, P]
         for name in ("tfo_hash", "tfo_vba", "tfo_visible_ids", "tfo_visible_type", "tfo_range_image",
                      "tfo_raycast_result", "tfo_dists", "tfo_frame_grey", "tfo_swap_state", "tfo_swap_stored_flags",
-                     "tfo_swap_stored"):
+                     "tfo_swap_stored", "tfo_vba_rgb"):
             getattr(L, name).argtypes = [P]; getattr(L, name).restype = P
         for name in ("tfo_prev_points", "tfo_prev_normals", "tfo_curr_points", "tfo_curr_normals", "tfo_curr_depth"):
             getattr(L, name).argtypes = [P, ctypes.c_int]; getattr(L, name).restype = P
@@ -233,10 +235,14 @@ class Oracle:
         except Exception:
             pass
 
-    def __call__(self, depth):
+    def __call__(self, depth, rgb=None):
         d = np.ascontiguousarray(depth, np.uint16)
         assert d.shape == (self.H, self.W)
-        return bool(self.L.tfo_process_frame(self.ctx, ptr(d)))
+        if rgb is None:
+            return bool(self.L.tfo_process_frame(self.ctx, ptr(d)))
+        c = np.ascontiguousarray(rgb, np.uint8)
+        assert c.shape == (self.H, self.W, 4)
+        return bool(self.L.tfo_process_frame_rgb(self.ctx, ptr(d), ptr(c), 0))
 
     def reset(self):
         self.L.tfo_reset(self.ctx)
@@ -261,6 +267,10 @@ class Oracle:
 
     def vba(self):
         return self._view(self.L.tfo_vba(self.ctx), VOXEL_DTYPE, self.params.n_blocks * 512).copy()
+
+    def vba_rgb(self):
+        """voxel_rgb: the colour plane, uint32 per voxel (r | g << 8 | b << 16 | w_color << 24)."""
+        return self._view(self.L.tfo_vba_rgb(self.ctx), np.uint32, self.params.n_blocks * 512).copy()
 
     def visible_ids(self):
         n = self.counters()["noVisibleEntries"]
@@ -305,9 +315,15 @@ class Oracle:
         self.L.tfo_alloc_ex(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
                             ptr(np.ascontiguousarray(dists, np.float32)), int(only_update_visible), int(reset_visible))
 
-    def integrate(self, pose_rt, dists):
-        self.L.tfo_integrate(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)),
-                            ptr(np.ascontiguousarray(dists, np.float32)))
+    def integrate(self, pose_rt, dists, rgb=None):
+        pr = ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12))
+        dd = np.ascontiguousarray(dists, np.float32)
+        if rgb is None:
+            self.L.tfo_integrate(self.ctx, pr, ptr(dd))
+        else:
+            c = np.ascontiguousarray(rgb, np.uint8)
+            assert c.shape == (self.H, self.W, 4)
+            self.L.tfo_integrate_rgb(self.ctx, pr, ptr(dd), ptr(c), 0)
 
     def expected_depths(self, pose_rt):
         self.L.tfo_expected_depths(self.ctx, ptr(np.ascontiguousarray(pose_rt, np.float32).reshape(12)))

@@ -556,6 +556,11 @@ struct tfo_ctx {
     uint8_t* hasStored;       /* hasStoredData */
     tfo_voxel* stored;        /* storedVoxelBlocks, 512 voxels per entry */
     int swap_counts[3];       /* last frame: swapped in, swapped out, reallocated */
+    /* colour (voxel_rgb): Voxel_s_rgb's clr + w_color per voxel, r | g << 8 | b << 16 | w << 24,
+       beside the Voxel_s plane (VoxelTypes.hpp:39-67); the frame's RGB image while integrating */
+    uint32_t* vba_rgb;
+    const uint8_t* rgb_in;
+    size_t rgb_pitch;
 };
 
 static const float k_identity_rt[12] = { 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0 };
@@ -572,6 +577,7 @@ static void reset_scene(tfo_ctx* c)
     c->lastFreeExcessListId = c->p.n_excess - 1;
     /* the reference's ResetScene leaves a GlobalCache alone (its swapping is never enabled);
        here a reset also empties it, so no block of the old scene is swapped into the new one */
+    if (c->vba_rgb) memset(c->vba_rgb, 0, sizeof(uint32_t) * (size_t)c->p.n_blocks * BLK3);   /* Voxel_s_rgb(): clr 0, w 0 */
     memset(c->swap_counts, 0, sizeof(c->swap_counts));   /* a reset transfers nothing */
     if (c->p.use_swapping) {
         memset(c->swapState, 0, (size_t)c->n_total);
@@ -613,6 +619,7 @@ tfo_ctx* tfo_create(const tfo_params* p)
         c->hasStored = (uint8_t*)calloc((size_t)c->n_total, 1);
         c->stored = (tfo_voxel*)calloc((size_t)c->n_total * BLK3, sizeof(tfo_voxel));
     }
+    if (p->voxel_rgb) c->vba_rgb = (uint32_t*)calloc((size_t)p->n_blocks * BLK3, sizeof(uint32_t));
     reset_scene(c);                                   /* topfu.cpp:75 */
     memcpy(c->pose, k_identity_rt, sizeof(c->pose));  /* reset(), topfu.cpp:141-152 */
     c->frame_counter = 0;
@@ -627,7 +634,7 @@ void tfo_destroy(tfo_ctx* c)
     for (int l = 0; l < 3; ++l) {
         free(c->depth_pyr[l]); free(c->curr_pts[l]); free(c->curr_nrm[l]); free(c->prev_pts[l]); free(c->prev_nrm[l]);
     }
-    free(c->swapState); free(c->hasStored); free(c->stored);
+    free(c->swapState); free(c->hasStored); free(c->stored); free(c->vba_rgb);
     free(c);
 }
 
@@ -965,21 +972,91 @@ uint8_t* tfo_swap_state(tfo_ctx* c) { return c->swapState; }
 uint8_t* tfo_swap_stored_flags(tfo_ctx* c) { return c->hasStored; }
 tfo_voxel* tfo_swap_stored(tfo_ctx* c) { return c->stored; }
 
-/* computeUpdatedVoxelDepthInfo, SceneReconstructionEngine.hpp:23-71 */
-static inline void update_voxel(tfo_voxel* v, const float pt_model[4], const float M[16], const float proj[4],
-                                float mu, int maxW, const float* depth, int W, int H)
+/* computeUpdatedVoxelDepthInfo, SceneReconstructionEngine.hpp:23-71; returns eta, or -1 where the
+   voxel projects behind the camera / outside the image or onto no depth (its return values) */
+static inline float update_voxel(tfo_voxel* v, const float pt_model[4], const float M[16], const float proj[4],
+                                 float mu, int maxW, const float* depth, int W, int H)
 {
     float pc[4];
     m4v(M, pt_model, pc);
-    if (pc[2] <= 0) return;
+    if (pc[2] <= 0) return -1;
     float ix = proj[0] * pc[0] / pc[2] + proj[2];
     float iy = proj[1] * pc[1] / pc[2] + proj[3];
-    if ((ix < 1) || (ix > (float)(W - 2)) || (iy < 1) || (iy > (float)(H - 2))) return;
+    if ((ix < 1) || (ix > (float)(W - 2)) || (iy < 1) || (iy > (float)(H - 2))) return -1;
     float depth_measure = depth[(int)(ix + 0.5f) + (int)(iy + 0.5f) * W];
-    if (depth_measure <= 0.0f) return;
+    if (depth_measure <= 0.0f) return -1;
     float eta = depth_measure - pc[2];
-    if (eta < -mu) return;
+    if (eta < -mu) return eta;
     tfo_tsdf_update(&v->sdf, &v->w, eta, mu, maxW);
+    return eta;
+}
+
+/* Vector3f::toUChar: CLAMP((int)ROUND(v), 0, 255), Vector.hpp:242-244 */
+static inline uint32_t u8_round(float v)
+{
+    int i = (int)((v < 0) ? (v - 0.5f) : (v + 0.5f));
+    return (uint32_t)(i < 0 ? 0 : (i > 255 ? 255 : i));
+}
+
+/* computeUpdatedVoxelColorInfo, SceneReconstructionEngine.hpp:116-148, with interpolateBilinear
+   (PixelUtils.hpp:8-32) of the uchar4 RGB image; called where ComputeUpdatedVoxelInfo<true, ...>
+   (:163-176, the lineage's colour path) does: after the depth update, unless
+   (eta > mu) || (fabs(eta / mu) > 0.25f).  One guard: a projection with pc.z == 0 (a NaN image
+   position, undefined behaviour in the reference) is skipped. */
+static inline void update_voxel_colour(uint32_t* clr, const float pt_model[4], const float Mr[16], const float proj[4],
+                                       int maxW, const uint8_t* rgb, size_t pitch, int W, int H)
+{
+    float oldW = (float)(*clr >> 24);
+    float oldC[3], newC[3];
+    for (int k = 0; k < 3; ++k) oldC[k] = (float)((*clr >> (8 * k)) & 0xffu) / 255.0f;
+    float pc[4];
+    m4v(Mr, pt_model, pc);
+    float ix = proj[0] * pc[0] / pc[2] + proj[2];
+    float iy = proj[1] * pc[1] / pc[2] + proj[3];
+    if (isnan(ix) || isnan(iy)) return;
+    if ((ix < 1) || (ix > (float)(W - 2)) || (iy < 1) || (iy > (float)(H - 2))) return;
+    int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+    float dx = ix - (float)x0, dy = iy - (float)y0;
+    static const uint8_t zero[4] = { 0, 0, 0, 0 };
+    const uint8_t* a = rgb + (size_t)y0 * pitch + 4 * (size_t)x0;
+    const uint8_t* b = zero; const uint8_t* cc = zero; const uint8_t* d = zero;
+    if (dx != 0) b = a + 4;
+    if (dy != 0) cc = a + pitch;
+    if (dx != 0 && dy != 0) d = a + pitch + 4;
+    float newW = 1;
+    for (int k = 0; k < 3; ++k) {
+        float m = ((float)a[k] * (1.0f - dx) * (1.0f - dy) + (float)b[k] * dx * (1.0f - dy) +
+                   (float)cc[k] * (1.0f - dx) * dy + (float)d[k] * dx * dy);
+        m = m / 255.0f;
+        newC[k] = oldC[k] * oldW + m * newW;
+    }
+    newW = oldW + newW;
+    for (int k = 0; k < 3; ++k) newC[k] /= newW;
+    float mw = (float)(uint8_t)maxW;
+    newW = (newW < mw) ? newW : mw;
+    *clr = u8_round(newC[0] * 255.0f) | (u8_round(newC[1] * 255.0f) << 8) | (u8_round(newC[2] * 255.0f) << 16) |
+           ((uint32_t)(uint8_t)newW << 24);
+}
+
+/* M_rgb = view->calib.trafo_rgb_to_depth.calib_inv * M_d (SceneReconstructionEngine_host.cu:217):
+   Matrix4 operator* (Matrix.hpp:113-119), r(x, y) += lhs(k, y) * rhs(x, k) from zero */
+static void rgb_matrix(const tfo_ctx* c, const float M[16], float Mr[16])
+{
+    float D[16];
+    rt_to_m4(c->p.depth_to_rgb, D);
+    for (int x = 0; x < 4; ++x)
+        for (int y = 0; y < 4; ++y) {
+            float r = 0.0f;
+            for (int k = 0; k < 4; ++k) r += D[4 * k + y] * M[4 * x + k];
+            Mr[4 * x + y] = r;
+        }
+}
+
+static void rgb_proj(const tfo_ctx* c, float proj[4])
+{
+    const float* q = c->p.rgb_intr;
+    if (q[0] == 0 && q[1] == 0 && q[2] == 0 && q[3] == 0) { proj[0] = c->p.fx; proj[1] = c->p.fy; proj[2] = c->p.cx; proj[3] = c->p.cy; }
+    else { proj[0] = q[0]; proj[1] = q[1]; proj[2] = q[2]; proj[3] = q[3]; }
 }
 
 /* TSDF running average + Voxel_s quantisation, SceneReconstructionEngine.hpp:56-68, VoxelTypes.hpp:71-73 */
@@ -998,14 +1075,17 @@ void tfo_tsdf_update(int16_t* sdf, uint8_t* w, float eta, float mu, int maxW)
     *w = (uint8_t)newW;
 }
 
-/* IntegrateIntoScene + integrateIntoScene_device<Voxel_s,false>, SceneReconstructionEngine_host.cu:197-251,297-329 */
+/* IntegrateIntoScene + integrateIntoScene_device<Voxel_s,false>, SceneReconstructionEngine_host.cu:197-251,297-329;
+   with voxel_rgb and a frame RGB image (c->rgb_in) the Voxel_s_rgb colour update after each voxel's depth update */
 void tfo_integrate(tfo_ctx* c, const float pose_rt[12], const float* dists)
 {
     if (c->noVisibleEntries == 0) return;
-    float M[16];
+    float M[16], Mr[16], proj_rgb[4];
     rt_to_m4(pose_rt, M);
     float proj[4] = { c->p.fx, c->p.fy, c->p.cx, c->p.cy };
-    float vs = c->p.voxelSize;
+    float vs = c->p.voxelSize, mu = c->p.mu;
+    const int colour = c->vba_rgb && c->rgb_in;
+    if (colour) { rgb_matrix(c, M, Mr); rgb_proj(c, proj_rgb); }
 #pragma omp parallel for schedule(dynamic, 16)
     for (int i = 0; i < c->noVisibleEntries; ++i) {
         const tfo_hash_entry* e = &c->hash[c->visibleIds[i]];
@@ -1017,9 +1097,21 @@ void tfo_integrate(tfo_ctx* c, const float pose_rt[12], const float* dists)
                 for (int x = 0; x < BLK; ++x) {
                     float pm[4];
                     pm[0] = (float)(gx + x) * vs; pm[1] = (float)(gy + y) * vs; pm[2] = (float)(gz + z) * vs; pm[3] = 1.0f;
-                    update_voxel(&blk[x + y * BLK + z * BLK * BLK], pm, M, proj, c->p.mu, c->p.maxW, dists, c->p.cols, c->p.rows);
+                    const int lin = x + y * BLK + z * BLK * BLK;
+                    float eta = update_voxel(&blk[lin], pm, M, proj, mu, c->p.maxW, dists, c->p.cols, c->p.rows);
+                    if (!colour || (eta > mu) || (fabsf(eta / mu) > 0.25f)) continue;
+                    update_voxel_colour(&c->vba_rgb[(size_t)e->ptr * BLK3 + lin], pm, Mr, proj_rgb, c->p.maxW, c->rgb_in,
+                                        c->rgb_pitch, c->p.cols, c->p.rows);
                 }
     }
+}
+
+/* the same with the view's RGB image (uchar4 rows of `pitch` bytes, the depth image's size) */
+void tfo_integrate_rgb(tfo_ctx* c, const float pose_rt[12], const float* dists, const uint8_t* rgb, size_t pitch)
+{
+    c->rgb_in = rgb; c->rgb_pitch = pitch ? pitch : (size_t)c->p.cols * 4;
+    tfo_integrate(c, pose_rt, dists);
+    c->rgb_in = 0;
 }
 
 /* ------------------------------------------------------------------------- */
@@ -1071,6 +1163,39 @@ static inline tfo_voxel read_voxel_nc(const tfo_ctx* c, int px, int py, int pz)
 }
 
 static inline int iround(float x) { return (int)((x < 0) ? (x - 0.5f) : (x + 0.5f)); }   /* ROUND, MathUtils.hpp:20 */
+
+/* a voxel's colour word (readVoxel(...).clr, w_color; Voxel_s_rgb() = 0 where no block) */
+static inline uint32_t read_colour(const tfo_ctx* c, int px, int py, int pz)
+{
+    int bx, by, bz;
+    int linearIdx = point_to_block(px, py, pz, &bx, &by, &bz);
+    int hashIdx = hash_index(c, bx, by, bz);
+    while (1) {
+        tfo_hash_entry e = c->hash[hashIdx];
+        if (e.x == (int16_t)bx && e.y == (int16_t)by && e.z == (int16_t)bz && e.ptr >= 0)
+            return c->vba_rgb[(size_t)e.ptr * BLK3 + linearIdx];
+        if (e.offset < 1) return 0;
+        hashIdx = c->p.n_buckets + e.offset - 1;
+    }
+}
+
+/* readFromSDF_color4u_interpolated (RepresentationAccess.hpp:260-294) + drawPixelColour
+   (VisualisationEngine_Shared.hpp:312-322): trilinear colour at the raycast point, / 255, then
+   (uchar)(v * 255); alpha 255 */
+static void colour_at(const tfo_ctx* c, const float pt[3], uint8_t out[4])
+{
+    int px = (int)floorf(pt[0]), py = (int)floorf(pt[1]), pz = (int)floorf(pt[2]);
+    float cx = pt[0] - floorf(pt[0]), cy = pt[1] - floorf(pt[1]), cz = pt[2] - floorf(pt[2]);
+    float ret[3] = { 0.0f, 0.0f, 0.0f };
+    for (int corner = 0; corner < 8; ++corner) {
+        int ux = corner & 1, uy = (corner >> 1) & 1, uz = corner >> 2;
+        float w = (ux ? cx : (1.0f - cx)) * (uy ? cy : (1.0f - cy)) * (uz ? cz : (1.0f - cz));
+        uint32_t v = read_colour(c, px + ux, py + uy, pz + uz);
+        for (int k = 0; k < 3; ++k) ret[k] += w * (float)((v >> (8 * k)) & 0xffu);
+    }
+    for (int k = 0; k < 3; ++k) out[k] = (uint8_t)((ret[k] / 255.0f) * 255.0f);
+    out[3] = 255;
+}
 
 /* readFromSDF_float_uninterpolated (cached), RepresentationAccess.hpp:129-135 */
 static inline float sdf_uninterp(const tfo_ctx* c, const float pt[3], int* vm, icache* k)
@@ -1355,7 +1480,8 @@ static int image_normal_angle(const float* ray, int W, int H, int x, int y, floa
    renderGrey_ImageNormals_device<false>, renderColourFromNormal_device,
    renderColourFromConfidence_device (VisualisationHelper.hpp:76-148); processPixel* /
    drawPixel* VisualisationEngine_Shared.hpp:187-310,399-498.  RENDER_COLOUR_FROM_VOLUME falls
-   back to greyscale for Voxel_s (:251-252).  drawPixelNormal leaves alpha as it was. */
+   back to greyscale for Voxel_s (:251-252) and reads the colour plane for Voxel_s_rgb.
+   drawPixelNormal leaves alpha as it was. */
 void tfo_render_type(tfo_ctx* c, const float invM_rt[12], int type, uint8_t* rgba)
 {
     int W = c->p.cols, H = c->p.rows;
@@ -1366,6 +1492,11 @@ void tfo_render_type(tfo_ctx* c, const float invM_rt[12], int type, uint8_t* rgb
         uint8_t* o = rgba + 4 * i;
         int found = p[3] > 0;
         float n[3] = { 0, 0, 0 }, angle = 0;
+        if (type == 2 && c->vba_rgb) {          /* renderColour_device / processPixelColour (:464-470) */
+            if (found) colour_at(c, p, o);
+            else o[0] = o[1] = o[2] = o[3] = 0;
+            continue;
+        }
         if (type == 1) {
             if (found) found = image_normal_angle(c->raycast, W, H, i % W, i / W, c->p.voxelSize, light, &angle);
             uint8_t v = found ? (uint8_t)((0.8f * angle + 0.2f) * 255.0f) : 0;
@@ -1514,6 +1645,15 @@ static int estimate_transform(tfo_ctx* c, float affine[12])
     return 1;
 }
 
+/* TopFu::operator()(depth, image) with the image integrated into Voxel_s_rgb voxels (voxel_rgb) */
+int tfo_process_frame_rgb(tfo_ctx* c, const uint16_t* depth, const uint8_t* rgb, size_t pitch)
+{
+    c->rgb_in = rgb; c->rgb_pitch = pitch ? pitch : (size_t)c->p.cols * 4;
+    int ok = tfo_process_frame(c, depth);
+    c->rgb_in = 0;
+    return ok;
+}
+
 /* TopFu::operator(), topfu.cpp:161-330 */
 int tfo_process_frame(tfo_ctx* c, const uint16_t* depth)
 {
@@ -1577,6 +1717,7 @@ void tfo_get_counters(const tfo_ctx* c, tfo_counters* o)
 void tfo_get_pose(const tfo_ctx* c, float rt[12]) { memcpy(rt, c->pose, sizeof(float) * 12); }
 tfo_hash_entry* tfo_hash(tfo_ctx* c) { return c->hash; }
 tfo_voxel* tfo_vba(tfo_ctx* c) { return c->vba; }
+uint32_t* tfo_vba_rgb(tfo_ctx* c) { return c->vba_rgb; }
 int* tfo_visible_ids(tfo_ctx* c) { return c->visibleIds; }
 uint8_t* tfo_visible_type(tfo_ctx* c) { return c->visType; }
 float* tfo_range_image(tfo_ctx* c) { return c->range; }

@@ -129,12 +129,16 @@ tfo_ctx* tfo_create(const tfo_params* p);
 void tfo_destroy(tfo_ctx* c);
 void tfo_reset(tfo_ctx* c);                                   /* TopFu::reset */
 int  tfo_process_frame(tfo_ctx* c, const uint16_t* depth);    /* TopFu::operator() */
+/* TopFu::operator()(depth, image): the frame's uchar4 RGB image (pitch bytes per row, 0: cols * 4)
+   integrated into the Voxel_s_rgb colour (voxel_rgb) */
+int  tfo_process_frame_rgb(tfo_ctx* c, const uint16_t* depth, const uint8_t* rgb, size_t pitch);
 void tfo_get_counters(const tfo_ctx* c, tfo_counters* out);
 void tfo_get_pose(const tfo_ctx* c, float rt[12]);            /* getCameraPose(): [R|t] row-major */
 /* stage-level entry points on the context */
 void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists);      /* AllocateSceneFromDepth */
 void tfo_alloc_ex(tfo_ctx* c, const float pose_rt[12], const float* dists, int only_update_visible, int reset_visible);
 void tfo_integrate(tfo_ctx* c, const float pose_rt[12], const float* dists);  /* IntegrateIntoScene */
+void tfo_integrate_rgb(tfo_ctx* c, const float pose_rt[12], const float* dists, const uint8_t* rgb, size_t pitch);
 void tfo_expected_depths(tfo_ctx* c, const float pose_rt[12]);                 /* CreateExpectedDepths */
 void tfo_raycast(tfo_ctx* c, const float invM_rt[12], int update_visible);    /* GenericRaycast */
 void tfo_render_icp(tfo_ctx* c, const float invM_rt[12], float* points, float* normals); /* renderICP */
@@ -153,6 +157,7 @@ tfo_voxel* tfo_swap_stored(tfo_ctx* c);             /* GlobalCache storedVoxelBl
 /* state access */
 tfo_hash_entry* tfo_hash(tfo_ctx* c);
 tfo_voxel* tfo_vba(tfo_ctx* c);
+uint32_t* tfo_vba_rgb(tfo_ctx* c);   /* voxel_rgb: per voxel r | g << 8 | b << 16 | w_color << 24 */
 int* tfo_visible_ids(tfo_ctx* c);
 uint8_t* tfo_visible_type(tfo_ctx* c);
 float* tfo_range_image(tfo_ctx* c);     /* W*H float2 */

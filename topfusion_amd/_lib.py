@@ -18,7 +18,7 @@ STAGE_NAMES = ("preprocess", "icp", "alloc", "integrate", "raycast_render", "gre
 
 (TF_BUF_HASH, TF_BUF_VBA, TF_BUF_VISIBLE_IDS, TF_BUF_VISIBLE_TYPE, TF_BUF_RANGE, TF_BUF_RAYCAST, TF_BUF_DISTS,
  TF_BUF_DEPTH, TF_BUF_CURR_POINTS, TF_BUF_CURR_NORMALS, TF_BUF_PREV_POINTS, TF_BUF_PREV_NORMALS, TF_BUF_GREY,
- TF_BUF_SWAP_STATE, TF_BUF_SWAP_STORED_FLAGS, TF_BUF_SWAP_STORED) = range(16)
+ TF_BUF_SWAP_STATE, TF_BUF_SWAP_STORED_FLAGS, TF_BUF_SWAP_STORED, TF_BUF_VBA_RGB) = range(17)
 
 
 class TfParams(ctypes.Structure):
@@ -98,6 +98,9 @@ def load():
         "tf_process_frame": ([P, P, S, P, ctypes.POINTER(TfStats)], I),
         "tf_process_frame_host": ([P, P, S, P, ctypes.POINTER(TfStats)], I),
         "tf_process_frames": ([P, P, S, I, P], I),
+        "tf_process_frame_rgb": ([P, P, S, P, S, P, ctypes.POINTER(TfStats)], I),
+        "tf_process_frame_rgb_host": ([P, P, S, P, S, P, ctypes.POINTER(TfStats)], I),
+        "tf_process_frames_rgb": ([P, P, S, P, S, I, P], I),
         "tf_render_image": ([P, P, S], I),
         "tf_get_pose": ([P, P], I),
         "tf_get_stats": ([P, ctypes.POINTER(TfStats)], I),
@@ -128,6 +131,7 @@ def load():
                              ctypes.POINTER(I), ctypes.POINTER(I)], I),
         "tf_scene_alloc": ([P, P, P, P, S, I, I], I),
         "tf_scene_integrate": ([P, P, P, P, S], I),
+        "tf_scene_integrate_rgb": ([P, P, P, P, S, P, S], I),
         "tf_vis_expected_depths": ([P, P, P], I),
         "tf_scene_swap": ([P], I),
         "tf_scene_swap_in": ([P], I),

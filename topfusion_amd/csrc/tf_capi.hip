@@ -92,7 +92,9 @@ static bool params_valid(const tf_params* p)
     if (4.0f * p->mu / (8.0f * p->voxelSize) + 2.0f > 60.0f) return false;
     if ((double)p->cols * p->rows * 64.0 > 2147483000.0) return false;
     if (p->use_swapping && (p->swap_transfer_blocks <= 0 || p->swap_transfer_blocks > p->n_buckets + p->n_excess)) return false;
-    if (p->voxel_rgb) return false;                 // Voxel_s_rgb: not built into this library yet
+    // the GlobalCache holds Voxel_s blocks: a swapping colour scene would need the colour half
+    // swapped too (CombineVoxelInformation's colour part) -- not built
+    if (p->voxel_rgb && p->use_swapping) return false;
     return true;
 }
 
@@ -102,7 +104,8 @@ static void ctx_free(tf_ctx* c)
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockBox, c->blockZ, c->blockTiles, c->blockOff, c->edChunk, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
-                     c->frame_ok, c->frame_mode, c->swapState, c->swapFlags, c->swapStore, c->swapCounts };
+                     c->frame_ok, c->frame_mode, c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
+                     c->vba_rgb_guard, c->rgb_in };
     for (void* b : bufs) if (b) (void)hipFree(b);
     // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
     float4* maps[4] = { c->curr_pts[0], c->curr_nrm[0], c->prev_pts[0], c->prev_nrm[0] };
@@ -230,6 +233,14 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         ALLOC(c->swapCounts, sizeof(int) * 2 * (size_t)c->alloc_chunks);
         e = hipMemsetAsync(c->swapState, 0, ntot_pad, c->stream);
         if (e == hipSuccess) e = hipMemsetAsync(c->swapFlags, 0, ntot_pad, c->stream);
+        if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    }
+    if (pin->voxel_rgb) {           // the Voxel_s_rgb colour plane (guard block + n_blocks blocks of 2 KiB)
+        const size_t nb = sizeof(unsigned) * ((size_t)pin->n_blocks + 1) * TF_BLK3;
+        ALLOC(c->vba_rgb_guard, nb);
+        c->vba_rgb = c->vba_rgb_guard + TF_BLK3;
+        ALLOC(c->rgb_in, sizeof(uchar4) * npx);
+        e = hipMemsetAsync(c->vba_rgb_guard, 0, nb, c->stream);
         if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     }
 #undef ALLOC
@@ -385,6 +396,17 @@ struct TfFramePlan {
     TfAhead alloc_bil, pair_pyr, pair_bil;
 };
 
+// the view's RGB image for the integrations enqueued while in scope (voxel_rgb)
+struct RgbScope {
+    tf_ctx* c;
+    RgbScope(tf_ctx* ctx, const uint8_t* rgb, size_t pitch) : c(ctx)
+    {
+        c->rgb_cur = (const uchar4*)rgb;
+        c->rgb_pitch = pitch ? pitch : (size_t)c->W * 4;
+    }
+    ~RgbScope() { c->rgb_cur = nullptr; }
+};
+
 static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, int slot,
                                const TfFramePlan* plan = nullptr)
 {
@@ -507,6 +529,31 @@ extern "C" tf_status tf_process_frame(tf_ctx* c, const uint16_t* dev_depth, size
     return s;
 }
 
+extern "C" tf_status tf_process_frame_rgb(tf_ctx* c, const uint16_t* dev_depth, size_t pitch, const uint8_t* dev_rgb,
+                                          size_t rgb_pitch, float pose_out[12], tf_stats* stats)
+{
+    if (!c) return TF_INVALID_ARG;
+    if (dev_rgb && !c->p.voxel_rgb) return TF_INVALID_ARG;
+    RgbScope rs(c, dev_rgb, rgb_pitch);
+    return tf_process_frame(c, dev_depth, pitch, pose_out, stats);
+}
+
+extern "C" tf_status tf_process_frame_rgb_host(tf_ctx* c, const uint16_t* host_depth, size_t pitch, const uint8_t* host_rgb,
+                                               size_t rgb_pitch, float pose_out[12], tf_stats* stats)
+{
+    if (!c || !host_depth) return TF_INVALID_ARG;
+    if (host_rgb && !c->p.voxel_rgb) return TF_INVALID_ARG;
+    if (!host_rgb) return tf_process_frame_host(c, host_depth, pitch, pose_out, stats);
+    if (rgb_pitch == 0) rgb_pitch = (size_t)c->W * 4;
+    TF_CHECK(hipMemcpy2DAsync(c->rgb_in, (size_t)c->W * 4, host_rgb, rgb_pitch, (size_t)c->W * 4, c->H,
+                              hipMemcpyHostToDevice, c->stream));
+    if (pitch == 0) pitch = (size_t)c->W * 2;
+    TF_CHECK(hipMemcpy2DAsync(c->depth_in, (size_t)c->W * 2, host_depth, pitch, (size_t)c->W * 2, c->H,
+                              hipMemcpyHostToDevice, c->stream));
+    return tf_process_frame_rgb(c, c->depth_in, (size_t)c->W * 2, (const uint8_t*)c->rgb_in, (size_t)c->W * 4, pose_out,
+                                stats);
+}
+
 extern "C" tf_status tf_process_frame_host(tf_ctx* c, const uint16_t* host_depth, size_t pitch, float pose_out[12],
                                            tf_stats* stats)
 {
@@ -519,9 +566,26 @@ extern "C" tf_status tf_process_frame_host(tf_ctx* c, const uint16_t* host_depth
 
 // a batch of device-resident frames: enqueued TF_PROF_RING at a time with no host round trip
 // inside a group (the frame's branches are decided on the device)
+static tf_status process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t stride, const uint8_t* rgb_frames,
+                                size_t rgb_stride, int n, int* ok_out);
+
 extern "C" tf_status tf_process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t stride, int n, int* ok_out)
 {
+    return process_frames(c, dev_frames, stride, nullptr, 0, n, ok_out);
+}
+
+extern "C" tf_status tf_process_frames_rgb(tf_ctx* c, const uint16_t* dev_frames, size_t stride, const uint8_t* rgb_frames,
+                                          size_t rgb_stride, int n, int* ok_out)
+{
+    if (c && rgb_frames && !c->p.voxel_rgb) return TF_INVALID_ARG;
+    return process_frames(c, dev_frames, stride, rgb_frames, rgb_stride, n, ok_out);
+}
+
+static tf_status process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t stride, const uint8_t* rgb_frames,
+                                size_t rgb_stride, int n, int* ok_out)
+{
     if (!c || !dev_frames || n < 0) return TF_INVALID_ARG;
+    if (rgb_frames && rgb_stride == 0) rgb_stride = (size_t)c->W * c->H * 4;
     auto frame = [&](int j) { return (const uint16_t*)((const char*)dev_frames + (size_t)j * stride); };
     for (int first = 0; first < n; first += TF_PROF_RING) {
         const int m = n - first < TF_PROF_RING ? n - first : TF_PROF_RING;
@@ -536,6 +600,7 @@ extern "C" tf_status tf_process_frames(tf_ctx* c, const uint16_t* dev_frames, si
                 if (j == 0) p.alloc_bil = next;
                 if (j + 2 < n) p.pair_bil = TfAhead{ frame(j + 2), c->d0_buf[j & 1] };
             }
+            RgbScope rs(c, rgb_frames ? rgb_frames + (size_t)j * rgb_stride : nullptr, (size_t)c->W * 4);
             tf_status s = enqueue_frame(c, frame(j), (size_t)c->W * 2, i, &p);
             if (s != TF_OK) return s;
         }
@@ -855,6 +920,15 @@ extern "C" tf_status tf_scene_integrate(tf_ctx* c, const float intr[4], const fl
     return TF_OK;
 }
 
+extern "C" tf_status tf_scene_integrate_rgb(tf_ctx* c, const float intr[4], const float pose_rt[12], const float* dists,
+                                           size_t dists_step, const uint8_t* dev_rgb, size_t rgb_step)
+{
+    if (!c || !pose_rt || !dists) return TF_INVALID_ARG;
+    if (dev_rgb && !c->p.voxel_rgb) return TF_INVALID_ARG;
+    RgbScope rs(c, dev_rgb, rgb_step);
+    return tf_scene_integrate(c, intr, pose_rt, dists, dists_step);
+}
+
 static tf_status scene_swap(tf_ctx* c, int which)
 {
     if (!c) return TF_INVALID_ARG;
@@ -987,6 +1061,7 @@ static void* buffer_ptr(tf_ctx* c, int which, int level, size_t* bytes)
     case TF_BUF_SWAP_STATE: *bytes = c->swapState ? (size_t)c->n_total : 0; return c->swapState;
     case TF_BUF_SWAP_STORED_FLAGS: *bytes = c->swapFlags ? (size_t)c->n_total : 0; return c->swapFlags;
     case TF_BUF_SWAP_STORED: *bytes = c->swapStore ? sizeof(TfVoxel) * (size_t)c->n_total * TF_BLK3 : 0; return c->swapStore;
+    case TF_BUF_VBA_RGB: *bytes = c->vba_rgb ? sizeof(unsigned) * (size_t)c->p.n_blocks * TF_BLK3 : 0; return c->vba_rgb;
     }
     *bytes = 0;
     return nullptr;
@@ -1029,7 +1104,7 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
     TF_CHECK(hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
     if (which == TF_BUF_HASH) TF_CHECK(tfk_grid_rebuild(c));       // keep the block grid exact
     static const int one = 1;
-    if (which == TF_BUF_HASH || which == TF_BUF_VBA)    // next reset (in-frame ones too): full clear
+    if (which == TF_BUF_HASH || which == TF_BUF_VBA || which == TF_BUF_VBA_RGB)   // next reset (in-frame ones too): full clear
         TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, scene_external), &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;

@@ -268,6 +268,14 @@ struct tf_ctx {
     unsigned char* swapFlags;    // hasStoredData per entry
     TfVoxel* swapStore;          // storedVoxelBlocks: 512 voxels per entry
     int* swapCounts;             // per 4096-entry chunk: [swap-in candidates, swap-out candidates]
+    // colour (p.voxel_rgb): Voxel_s_rgb's clr + w_color as a second plane beside the Voxel_s one
+    // (r | g << 8 | b << 16 | w_color << 24 per voxel, same block offsets), so the depth-only
+    // passes (raycasts, ICP maps) stream 4 B per voxel, not 8; a guard block of zeros first
+    unsigned* vba_rgb_guard;
+    unsigned* vba_rgb;
+    uchar4* rgb_in;              // staging for host RGB uploads (voxel_rgb)
+    const uchar4* rgb_cur;       // the frame's RGB image while it is enqueued (nullptr: none)
+    size_t rgb_pitch;            // its row step in bytes
     // SceneReconstructionEngine temporaries
     unsigned char* allocType;
     int* winnerKey;          // per-entry last-writer key (pixel*64+step), replaces blockCoords races

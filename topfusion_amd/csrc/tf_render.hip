@@ -659,10 +659,35 @@ __device__ __forceinline__ bool image_normal_angle(const float4* ray, int W, int
     return *angle > 0.0f;
 }
 
+// readFromSDF_color4u_interpolated (RepresentationAccess.hpp:260-294) + drawPixelColour
+// (VisualisationEngine_Shared.hpp:312-322): the eight corners' colour words from the colour plane
+// (same block offsets as the Voxel_s plane; a missing block reads its zero guard block), weights
+// and sums in the reference's order, / 255 then (uchar)(v * 255), alpha 255
+__device__ __forceinline__ uchar4 colour_at(const SceneView& s, const unsigned* rgb_guard, const float* pt)
+{
+    Corners q;
+    corners_lookup(s, pt, q);
+    const int lx[2] = { lin_x(q.fx), lin_x(q.fx + 1) }, ly[2] = { lin_y(q.fy), lin_y(q.fy + 1) };
+    const int lz[2] = { lin_zg(q.fz), lin_zg(q.fz + 1) };
+    unsigned cw[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+        cw[c] = ld_off<unsigned>(rgb_guard, (unsigned)(q.voff[c] + lx[c & 1] + ly[(c >> 1) & 1] + lz[c >> 2]) * 4u);
+    float ret[3] = { 0.0f, 0.0f, 0.0f };
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float w = ((c & 1) ? q.cx : (1.0f - q.cx)) * ((c & 2) ? q.cy : (1.0f - q.cy)) * ((c & 4) ? q.cz : (1.0f - q.cz));
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ret[k] += w * (float)((cw[c] >> (8 * k)) & 0xffu);
+    }
+    return make_uchar4((unsigned char)((ret[0] / 255.0f) * 255.0f), (unsigned char)((ret[1] / 255.0f) * 255.0f),
+                       (unsigned char)((ret[2] / 255.0f) * 255.0f), 255);
+}
+
 template <int TYPE>
 __global__ void __launch_bounds__(256)
 k_render_type(SceneView s, const float4* __restrict__ ray, int W, int H, float voxelSize,
-              const TfDevState* __restrict__ st, uchar4* __restrict__ out)
+              const TfDevState* __restrict__ st, uchar4* __restrict__ out, const unsigned* __restrict__ rgb_guard)
 {
     __shared__ int vtab[256 * VTAB_STRIDE];
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
@@ -674,6 +699,11 @@ k_render_type(SceneView s, const float4* __restrict__ ray, int W, int H, float v
     const float4 p = ray[i];
     bool found = p.w > 0;
     float nn[3], angle = 0.f;
+    if (TYPE == TF_RENDER_COLOUR_FROM_VOLUME) {                      // renderColour_device / processPixelColour
+        const float pt[3] = { p.x, p.y, p.z };
+        out[i] = found ? colour_at(s, rgb_guard, pt) : make_uchar4(0, 0, 0, 0);
+        return;
+    }
     if (TYPE == TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS) {           // processPixelGrey_ImageNormals<true,false>
         if (found) found = image_normal_angle(ray, W, H, x, y, voxelSize, lx, ly, lz, &angle);
         const unsigned char v = found ? grey_of(angle) : (unsigned char)0;
@@ -707,7 +737,7 @@ k_render_type(SceneView s, const float4* __restrict__ ray, int W, int H, float v
         } else {
             out[i] = make_uchar4(0, 0, 0, 0);
         }
-    } else {       // RENDER_SHADED_GREYSCALE; RENDER_COLOUR_FROM_VOLUME falls back to it for Voxel_s (:251-252)
+    } else {       // RENDER_SHADED_GREYSCALE (RENDER_COLOUR_FROM_VOLUME on Voxel_s is sent here, :251-252)
         const unsigned char v = found ? grey_of(angle) : (unsigned char)0;
         out[i] = make_uchar4(v, v, v, v);
     }
@@ -720,15 +750,20 @@ hipError_t tfk_render_type(tf_ctx* c, int type)
     const dim3 g((n + 255) / 256), b(256);
     const float4* ray = (const float4*)c->raycast;
     const float vs = c->p.voxelSize;
+    const unsigned* cg = c->vba_rgb_guard;
+    // RENDER_COLOUR_FROM_VOLUME without colour information: greyscale (VisualisationEngine_CUDA.cu:251-252)
+    if (type == TF_RENDER_COLOUR_FROM_VOLUME && !c->p.voxel_rgb) type = TF_RENDER_SHADED_GREYSCALE;
     switch (type) {
+    case TF_RENDER_COLOUR_FROM_VOLUME:
+        hipLaunchKernelGGL(k_render_type<TF_RENDER_COLOUR_FROM_VOLUME>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey, cg); break;
     case TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS:
-        hipLaunchKernelGGL(k_render_type<TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey); break;
+        hipLaunchKernelGGL(k_render_type<TF_RENDER_SHADED_GREYSCALE_IMAGENORMALS>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey, cg); break;
     case TF_RENDER_COLOUR_FROM_NORMAL:
-        hipLaunchKernelGGL(k_render_type<TF_RENDER_COLOUR_FROM_NORMAL>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey); break;
+        hipLaunchKernelGGL(k_render_type<TF_RENDER_COLOUR_FROM_NORMAL>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey, cg); break;
     case TF_RENDER_COLOUR_FROM_CONFIDENCE:
-        hipLaunchKernelGGL(k_render_type<TF_RENDER_COLOUR_FROM_CONFIDENCE>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey); break;
+        hipLaunchKernelGGL(k_render_type<TF_RENDER_COLOUR_FROM_CONFIDENCE>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey, cg); break;
     default:
-        hipLaunchKernelGGL(k_render_type<TF_RENDER_SHADED_GREYSCALE>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey); break;
+        hipLaunchKernelGGL(k_render_type<TF_RENDER_SHADED_GREYSCALE>, g, b, 0, c->stream, s, ray, c->W, c->H, vs, c->st, c->grey, cg); break;
     }
     return hipGetLastError();
 }

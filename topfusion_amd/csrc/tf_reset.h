@@ -15,6 +15,7 @@ struct ResetArgs {
     int full;                        // clear everything (else only what the frames wrote)
     unsigned char* swapState;        // swapping: GlobalCache states / stored flags, cleared with a reset
     unsigned char* swapFlags;
+    unsigned* vba_rgb;               // voxel_rgb: the colour plane, cleared with its blocks (Voxel_s_rgb(): 0)
 };
 
 // Runs as workgroup `bid` of `nblk` (256 threads): its own launch (k_reset_scene) or the
@@ -52,9 +53,13 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
     const size_t stride = (size_t)nblk * 256;
     uint4 vfill = make_uint4(32767u, 32767u, 32767u, 32767u);   // Voxel_s(): sdf 32767, w 0
     uint4* v4 = (uint4*)vba;
+    uint4* c4 = (uint4*)r.vba_rgb;
+    const uint4 cfill = make_uint4(0, 0, 0, 0);
     TfHashEntry e; e.x = e.y = e.z = e.pad = 0; e.offset = 0; e.ptr = -2;
     if (full) {
         for (size_t i = tid; i < n_vox / 4; i += stride) v4[i] = vfill;
+        if (c4)
+            for (size_t i = tid; i < n_vox / 4; i += stride) c4[i] = cfill;
         for (size_t i = tid; i < (size_t)n_blocks; i += stride) allocList[i] = (int)i;
         for (size_t i = tid; i < (size_t)n_excess; i += stride) excessList[i] = (int)i;
     } else {
@@ -74,7 +79,11 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const size_t i = i0 + k * stride;
-                if (i < n_used4) v4[(size_t)blk[k] * (TF_BLK3 / 4) + i % (TF_BLK3 / 4)] = vfill;
+                if (i < n_used4) {
+                    const size_t o = (size_t)blk[k] * (TF_BLK3 / 4) + i % (TF_BLK3 / 4);
+                    v4[o] = vfill;
+                    if (c4) c4[o] = cfill;
+                }
             }
         }
     }

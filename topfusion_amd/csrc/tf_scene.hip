@@ -55,6 +55,7 @@ void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot)
     // also empties the GlobalCache (swap states, stored flags)
     r->swapState = c->p.use_swapping ? c->swapState : nullptr;
     r->swapFlags = c->p.use_swapping ? c->swapFlags : nullptr;
+    r->vba_rgb = c->p.voxel_rgb ? c->vba_rgb : nullptr;
     if (c->p.use_swapping) r->full = 1;
 }
 
@@ -646,6 +647,11 @@ struct IntegArgs {
     // copying keeps the buffer pointers fixed); levels contiguous, n_maps float4 per map
     const float4* curr_pts; const float4* curr_nrm; float4* prev_pts; float4* prev_nrm;
     int n_maps;
+    // colour (voxel_rgb with a frame RGB image): computeUpdatedVoxelColorInfo on the colour plane
+    const uchar4* rgb; size_t rgb_pitch;
+    unsigned* vba_rgb;
+    float rfx, rfy, rcx, rcy;           // projParams_rgb
+    float D[16];                        // calib_inv (depth -> rgb) as a column-major Matrix4f
 };
 
 // computeUpdatedVoxelDepthInfo (SceneReconstructionEngine.hpp:23-71) in two halves, so that
@@ -666,11 +672,14 @@ __device__ __forceinline__ bool integ_project(float px, float py, float pz, cons
     *idx = (int)(ix + 0.5f) + (int)(iy + 0.5f) * a.W;
     return true;
 }
+// *eta_r: computeUpdatedVoxelDepthInfo's return value (eta, or -1 for no depth)
 __device__ __forceinline__ unsigned integ_update(unsigned vox, float depth_measure, float z, const IntegArgs& a,
-                                                 const float* rw)
+                                                 const float* rw, float* eta_r)
 {
+    *eta_r = -1.0f;
     if (depth_measure <= 0.0f) return vox;
     float eta = depth_measure - z;
+    *eta_r = eta;
     if (eta < -a.mu) return vox;
     short sdf = (short)(vox & 0xffff);
     int oldW = (vox >> 16) & 0xff;
@@ -685,6 +694,63 @@ __device__ __forceinline__ unsigned integ_update(unsigned vox, float depth_measu
     return ((unsigned)(unsigned short)nsdf) | ((unsigned)(newW & 0xff) << 16) | (vox & 0xff000000u);
 }
 
+// ComputeUpdatedVoxelInfo<true, ...>'s gate (SceneReconstructionEngine.hpp:173): colour only
+// unless (eta > mu) || (fabs(eta / mu) > 0.25f).  |eta| > mu fails it whatever the rounding, so
+// the division runs only inside the band.
+__device__ __forceinline__ bool integ_colour_gate(float eta, const IntegArgs& a)
+{
+    if (!(fabsf(eta) <= a.mu)) return false;
+    const float q = a.mu_exact3 ? tf_div_exact3(eta, a.mu, a.inv_mu) : eta / a.mu;
+    return !(fabsf(q) > 0.25f);
+}
+
+// Vector3f::toUChar: CLAMP((int)ROUND(v), 0, 255) (Vector.hpp:242-244, MathUtils.hpp:20)
+__device__ __forceinline__ unsigned integ_u8(float v)
+{
+    const int i = (int)((v < 0) ? (v - 0.5f) : (v + 0.5f));
+    return (unsigned)(i < 0 ? 0 : (i > 255 ? 255 : i));
+}
+
+// computeUpdatedVoxelColorInfo (SceneReconstructionEngine.hpp:116-148) on one colour word
+// (r | g << 8 | b << 16 | w << 24) with interpolateBilinear (PixelUtils.hpp:8-32) of the RGB image;
+// canonical arithmetic.  A NaN image position (pc.z == 0: undefined in the reference) is skipped.
+__device__ __forceinline__ unsigned integ_colour(unsigned clr, float px, float py, float pz, const float* Mr,
+                                                 const IntegArgs& a)
+{
+    float pc[3];
+    tf_m4v3(Mr, px, py, pz, 1.0f, pc);
+    const float ix = a.rfx * pc[0] / pc[2] + a.rcx;
+    const float iy = a.rfy * pc[1] / pc[2] + a.rcy;
+    if (!(ix >= 1 && ix <= (float)(a.W - 2) && iy >= 1 && iy <= (float)(a.H - 2))) return clr;
+    const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+    const float dx = ix - (float)x0, dy = iy - (float)y0;
+    const uchar4* r0 = (const uchar4*)((const char*)a.rgb + (size_t)y0 * a.rgb_pitch);
+    const uchar4* r1 = (const uchar4*)((const char*)r0 + a.rgb_pitch);
+    const uchar4 z4 = make_uchar4(0, 0, 0, 0);
+    const uchar4 A = r0[x0];
+    const uchar4 B = (dx != 0) ? r0[x0 + 1] : z4;
+    const uchar4 C = (dy != 0) ? r1[x0] : z4;
+    const uchar4 D = (dx != 0 && dy != 0) ? r1[x0 + 1] : z4;
+    const float oldW = (float)(clr >> 24);
+    const float ax = 1.0f - dx, ay = 1.0f - dy;
+    const float av[3] = { (float)A.x, (float)A.y, (float)A.z }, bv[3] = { (float)B.x, (float)B.y, (float)B.z };
+    const float cv[3] = { (float)C.x, (float)C.y, (float)C.z }, dv[3] = { (float)D.x, (float)D.y, (float)D.z };
+    const float newW = oldW + 1.0f;
+    float mw = (float)(unsigned char)a.maxW;
+    const float wout = (newW < mw) ? newW : mw;
+    unsigned out = (unsigned)(unsigned char)wout << 24;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float oldC = (float)((clr >> (8 * k)) & 0xffu) / 255.0f;
+        float m = av[k] * ax * ay + bv[k] * dx * ay + cv[k] * ax * dy + dv[k] * dx * dy;
+        m = m / 255.0f;
+        float nc = oldC * oldW + m * 1.0f;
+        nc = nc / newW;
+        out |= integ_u8(nc * 255.0f) << (8 * k);
+    }
+    return out;
+}
+
 typedef unsigned int tf_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 nt_load16(const uint4* p)
 {
@@ -697,11 +763,12 @@ __device__ __forceinline__ void nt_store16(uint4* p, uint4 v)
     __builtin_nontemporal_store(r, reinterpret_cast<tf_u32x4*>(p));
 }
 
-// one lane's 4 consecutive voxels (16 B) of a block: update and store
-// the lane's four voxels of each of two blocks (ptr < 0: no block)
+// the lane's four voxels of each of two blocks (ptr < 0: no block): update and store; RGB: then
+// the colour of those inside the colour gate
+template <bool RGB>
 __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry& e, const TfHashEntry& e2, int vx,
                                            int vy, int vz, const float* M, const IntegArgs& a, uint4* p, uint4* p2,
-                                           const float* rw, bool stream)
+                                           const float* rw, bool stream, const float* Mr, int lin)
 {
     float z[8];
     int di[8];
@@ -722,9 +789,12 @@ __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry&
 #pragma unroll
     for (int k = 0; k < 8; ++k) dm[k] = a.dists[di[k]];
     unsigned w[8] = { v.x, v.y, v.z, v.w, v2.x, v2.y, v2.z, v2.w };
+    float eta[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (ok[k]) w[k] = integ_update(w[k], dm[k], z[k], a, rw);
+    for (int k = 0; k < 8; ++k) {
+        eta[k] = -1.0f;
+        if (ok[k]) w[k] = integ_update(w[k], dm[k], z[k], a, rw, &eta[k]);
+    }
     if (stream) {
         if (e.ptr >= 0) nt_store16(p, make_uint4(w[0], w[1], w[2], w[3]));
         if (e2.ptr >= 0) nt_store16(p2, make_uint4(w[4], w[5], w[6], w[7]));
@@ -732,9 +802,29 @@ __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry&
         if (e.ptr >= 0) *p = make_uint4(w[0], w[1], w[2], w[3]);
         if (e2.ptr >= 0) *p2 = make_uint4(w[4], w[5], w[6], w[7]);
     }
+    if (RGB) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const TfHashEntry& h = b ? e2 : e;
+            if (h.ptr < 0) continue;
+            unsigned gate = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) gate |= (integ_colour_gate(eta[4 * b + k], a) ? 1u : 0u) << k;
+            if (!gate) continue;                   // most lanes: no voxel in the colour band
+            uint4* cp = (uint4*)(a.vba_rgb + (size_t)h.ptr * TF_BLK3 + lin);
+            uint4 c4 = *cp;
+            unsigned cw[4] = { c4.x, c4.y, c4.z, c4.w };
+            const int gx = h.x * TF_BLK, gy = h.y * TF_BLK, gz = h.z * TF_BLK;
+            const float py = (float)(gy + vy) * a.voxelSize, pz = (float)(gz + vz) * a.voxelSize;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (gate & (1u << k)) cw[k] = integ_colour(cw[k], (float)(gx + vx + k) * a.voxelSize, py, pz, Mr, a);
+            *cp = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+        }
+    }
 }
 
-template <bool WITH_ED>
+template <bool WITH_ED, bool RGB>
 __global__ void __launch_bounds__(256)
 k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
             const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed)
@@ -767,6 +857,20 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
     float M[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) M[i] = st->M_alloc[i];
+    // M_rgb = calib_inv * M_d (SceneReconstructionEngine_host.cu:217), Matrix4 operator*
+    // (Matrix.hpp:113-119): r(x, y) += lhs(k, y) * rhs(x, k) from zero
+    float Mr[16];
+    if (RGB) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) {
+                float r = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) r += a.D[4 * k + y] * M[4 * x + k];
+                Mr[4 * x + y] = r;
+            }
+    }
     const int half = threadIdx.x >> 7, t = threadIdx.x & 127;
     const int lin = t * 4;                       // first voxel of this lane: x in {0,4}
     const int vx = lin & 7, vy = (lin >> 3) & 7, vz = lin >> 6;
@@ -788,7 +892,7 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
         uint4 v, v2;
         if (stream) { v = nt_load16(p); v2 = nt_load16(p2); }
         else { v = *p; v2 = *p2; }
-        integ_pair(v, v2, e, e2, vx, vy, vz, M, a, p, p2, rw, stream);
+        integ_pair<RGB>(v, v2, e, e2, vx, vy, vz, M, a, p, p2, rw, stream, Mr, lin);
     }
 }
 
@@ -803,14 +907,26 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
     a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy;
     a.voxelSize = c->p.voxelSize; a.mu = c->p.mu; a.maxW = c->p.maxW;
     a.inv_mu = 1.0f / c->p.mu; a.mu_exact3 = c->mu_exact3;
+    const bool rgb = c->p.voxel_rgb && c->rgb_cur;
+    a.rgb = c->rgb_cur; a.rgb_pitch = c->rgb_pitch; a.vba_rgb = c->vba_rgb;
+    const float* q = c->p.rgb_intr;
+    const bool depth_intr = q[0] == 0 && q[1] == 0 && q[2] == 0 && q[3] == 0;   // rgb_intr all 0
+    a.rfx = depth_intr ? c->p.fx : q[0]; a.rfy = depth_intr ? c->p.fy : q[1];
+    a.rcx = depth_intr ? c->p.cx : q[2]; a.rcy = depth_intr ? c->p.cy : q[3];
+    const float* d = c->p.depth_to_rgb;          // row-major [R|t] -> column-major Matrix4f
+    for (int col = 0; col < 4; ++col)
+        for (int row = 0; row < 4; ++row)
+            a.D[4 * col + row] = row < 3 ? d[4 * row + col] : (col == 3 ? 1.0f : 0.0f);
     EdArgs ed = {};
+    const dim3 g(2048), b(256);
     if (with_ed) {
         tf_ed_args(c, &ed);
-        hipLaunchKernelGGL(k_integrate<true>, dim3(2048 + TF_ED_BLOCKS), dim3(256), 0, c->stream, a, c->st, c->hash,
-                           c->visibleIds, c->vba, ed);
+        const dim3 ge(2048 + TF_ED_BLOCKS);
+        if (rgb) hipLaunchKernelGGL((k_integrate<true, true>), ge, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed);
+        else hipLaunchKernelGGL((k_integrate<true, false>), ge, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed);
     } else {
-        hipLaunchKernelGGL(k_integrate<false>, dim3(2048), dim3(256), 0, c->stream, a, c->st, c->hash, c->visibleIds,
-                           c->vba, ed);
+        if (rgb) hipLaunchKernelGGL((k_integrate<false, true>), g, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed);
+        else hipLaunchKernelGGL((k_integrate<false, false>), g, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed);
     }
     return hipGetLastError();
 }

@@ -72,6 +72,42 @@ def render_depth(R, t, cols=640, rows=480, sphere=True, noise_mm=0.0, holes=0.0,
     return mm
 
 
+def render_colour(R, t, cols=640, rows=480, sphere=True, intr=None):
+    """The colour camera's view of the same room (pose R, t camera->world): a smooth texture of the
+    surface point hit by each pixel's ray, uint8 (rows, cols, 4), alpha 255, black where nothing is
+    hit -- the RGB stream for the colour TSDF (Voxel_s_rgb)."""
+    fx, fy, cx, cy = intr if intr is not None else intrinsics(cols, rows)
+    u = np.arange(cols, dtype=np.float64)
+    v = np.arange(rows, dtype=np.float64)
+    uu, vv = np.meshgrid(u, v)
+    dc = np.stack([(uu - cx) / fx, (vv - cy) / fy, np.ones_like(uu)], axis=-1)
+    dw = dc @ np.asarray(R, np.float64).T
+    o = np.asarray(t, np.float64)
+    best = np.full((rows, cols), np.inf)
+    planes = [(2, 1.8), (1, 0.6), (0, -0.8), (0, 1.1), (1, -0.9), (2, -0.6)]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for ax, off in planes:
+            tt = (off - o[ax]) / dw[..., ax]
+            best = np.minimum(best, np.where(tt > 1e-6, tt, np.inf))
+        if sphere:
+            c = np.array([0.15, 0.25, 1.3])
+            oc = o - c
+            b = dw @ oc
+            a = np.einsum("ijk,ijk->ij", dw, dw)
+            disc = b * b - a * (oc @ oc - 0.09)
+            t0 = (-b - np.sqrt(np.maximum(disc, 0))) / a
+            best = np.minimum(best, np.where((disc >= 0) & (t0 > 1e-6), t0, np.inf))
+    hit = np.isfinite(best)
+    p = o + dw * np.where(hit, best, 0)[..., None]
+    out = np.zeros((rows, cols, 4), np.uint8)
+    out[..., 0] = np.rint(127.5 + 120 * np.sin(2 * np.pi * p[..., 0] / 0.13))
+    out[..., 1] = np.rint(127.5 + 120 * np.sin(2 * np.pi * (p[..., 1] + p[..., 2]) / 0.17))
+    out[..., 2] = np.rint(127.5 + 120 * np.cos(2 * np.pi * (p[..., 2] - p[..., 0]) / 0.23))
+    out[..., 3] = 255
+    out[~hit] = 0
+    return out
+
+
 def room_corner(cols=640, rows=480, noise_mm=1.0, holes=0.01, seed=42):
     """C1: single frame at the identity pose."""
     return render_depth(np.eye(3), np.zeros(3), cols, rows, sphere=False, noise_mm=noise_mm, holes=holes, seed=seed)

@@ -68,27 +68,46 @@ class TopFu:
         return self.params_
 
     # -- TopFu API ----------------------------------------------------------------------
-    def __call__(self, depth, pitch=0):
-        """TopFu::operator(): returns the frame's bool (False = ICP failed, scene reset)."""
+    def __call__(self, depth, pitch=0, rgb=None):
+        """TopFu::operator()(depth, image): returns the frame's bool (False = ICP failed, scene
+        reset).  rgb (voxel_rgb contexts): the frame's uchar4 (rows, cols, 4) image -- a host array
+        with a host depth, a device pointer with a device depth."""
         lib = L.load()
         stats = L.TfStats()
         pose = np.zeros(12, np.float32)
         if isinstance(depth, int):
-            s = lib.tf_process_frame(self._h, ctypes.c_void_p(depth), pitch, _ptr(pose), ctypes.byref(stats))
+            if rgb is None:
+                s = lib.tf_process_frame(self._h, ctypes.c_void_p(depth), pitch, _ptr(pose), ctypes.byref(stats))
+            else:
+                s = lib.tf_process_frame_rgb(self._h, ctypes.c_void_p(depth), pitch, ctypes.c_void_p(int(rgb)), 0,
+                                             _ptr(pose), ctypes.byref(stats))
         else:
             d = np.ascontiguousarray(depth, np.uint16)
             assert d.shape == (self.H, self.W), d.shape
-            s = lib.tf_process_frame_host(self._h, _ptr(d), self.W * 2, _ptr(pose), ctypes.byref(stats))
+            if rgb is None:
+                s = lib.tf_process_frame_host(self._h, _ptr(d), self.W * 2, _ptr(pose), ctypes.byref(stats))
+            else:
+                c = np.ascontiguousarray(rgb, np.uint8)
+                assert c.shape == (self.H, self.W, 4), c.shape
+                s = lib.tf_process_frame_rgb_host(self._h, _ptr(d), self.W * 2, _ptr(c), self.W * 4, _ptr(pose),
+                                                  ctypes.byref(stats))
         L.check(s, "tf_process_frame", allow=(L.TF_OK, L.TF_ICP_FAIL))
         self.last_stats = stats.as_dict()
         return s == L.TF_OK
 
-    def process_frames(self, dev_frames, n, stride=None):
-        """Runs n device-resident frames; returns the per-frame bools."""
+    def process_frames(self, dev_frames, n, stride=None, rgb_frames=None, rgb_stride=None):
+        """Runs n device-resident frames (and, voxel_rgb, their device-resident RGB images);
+        returns the per-frame bools."""
         ok = np.zeros(n, np.int32)
         stride = stride if stride is not None else self.W * self.H * 2
-        L.check(L.load().tf_process_frames(self._h, ctypes.c_void_p(dev_frames), stride, n, _ptr(ok)),
-                "tf_process_frames")
+        if rgb_frames is None:
+            L.check(L.load().tf_process_frames(self._h, ctypes.c_void_p(dev_frames), stride, n, _ptr(ok)),
+                    "tf_process_frames")
+        else:
+            rs = rgb_stride if rgb_stride is not None else self.W * self.H * 4
+            L.check(L.load().tf_process_frames_rgb(self._h, ctypes.c_void_p(dev_frames), stride,
+                                                   ctypes.c_void_p(int(rgb_frames)), rs, n, _ptr(ok)),
+                    "tf_process_frames_rgb")
         return ok.astype(bool)
 
     def renderImage(self, type=0):
@@ -269,6 +288,10 @@ class TopFu:
 
     def vba(self):
         return self.download(L.TF_BUF_VBA).view(VOXEL_DTYPE)
+
+    def vba_rgb(self):
+        """voxel_rgb: the colour plane, uint32 per voxel (r | g << 8 | b << 16 | w_color << 24)."""
+        return self.download(L.TF_BUF_VBA_RGB).view(np.uint32)
 
     def visible_ids(self):
         n = self.stats()["noVisibleEntries"]
