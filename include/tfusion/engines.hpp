@@ -42,6 +42,18 @@ namespace tfusion
         static short floatToValue(float x) { return (short)(x * 32767.0f); }
         static const bool hasColorInformation = false;
     };
+    // Voxel_s_rgb (VoxelTypes.hpp:39-67): the context keeps its colour half (clr, w_color) as a
+    // second plane (TF_BUF_VBA_RGB); this struct is the combined view a caller assembles
+    struct Voxel_s_rgb {
+        short sdf;
+        unsigned char w_depth;
+        Vector3u clr;
+        unsigned char w_color;
+        static short SDF_initialValue() { return 32767; }
+        static float valueToFloat(float x) { return x / 32767.0f; }
+        static short floatToValue(float x) { return (short)(x * 32767.0f); }
+        static const bool hasColorInformation = true;
+    };
     struct VoxelBlockHash {
         enum { noTotalEntries = 0x100000 + 0x20000 };   // SDF_BUCKET_NUM + SDF_EXCESS_LIST_SIZE (defaults)
     };
@@ -124,6 +136,7 @@ namespace tfusion
                 c.viewFrustum_min = params->viewFrustum_min; c.viewFrustum_max = params->viewFrustum_max;
             }
             c.use_swapping = useSwapping ? 1 : 0;
+            c.voxel_rgb = TVoxel::hasColorInformation ? 1 : 0;    // Scene<Voxel_s_rgb, ...>
             tf_engine_check(tf_create(&c, &ctx_), "Scene: tf_create");
             intr_ = tp.intr;
             if (useSwapping) globalCache = new GlobalCache<TVoxel>(ctx_);
@@ -208,6 +221,17 @@ namespace tfusion
             detail::intr4(intr, in);
             detail::rt_of(pose, rt);
             tf_engine_check(tf_scene_integrate(scene->context(), in, rt, dist.ptr(), dist.step()), "IntegrateIntoScene");
+        }
+        // with the view's RGBA image (view->rgb, :225): the colour update of a Voxel_s_rgb scene
+        void IntegrateIntoScene(Scene<TVoxel, TIndex>* scene, const Intr intr, const Affine3f pose, cuda::Dists& dist,
+                                const cuda::image4u& rgb, const RenderState* = nullptr)
+        {
+            float in[4], rt[12];
+            detail::intr4(intr, in);
+            detail::rt_of(pose, rt);
+            tf_engine_check(tf_scene_integrate_rgb(scene->context(), in, rt, dist.ptr(), dist.step(),
+                                                   reinterpret_cast<const uint8_t*>(rgb.ptr()), rgb.step()),
+                            "IntegrateIntoScene(rgb)");
         }
     };
 

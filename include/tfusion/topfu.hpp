@@ -89,6 +89,9 @@ namespace tfusion
             tf_default_params(&d);
             p.n_buckets = d.n_buckets; p.n_excess = d.n_excess; p.n_blocks = d.n_blocks;
             p.vis_capacity = d.vis_capacity; p.max_render_blocks = d.max_render_blocks;
+            p.integrate_colour = false;
+            p.rgb_intr = Intr(0.f, 0.f, 0.f, 0.f);
+            p.depth_to_rgb = Affine3f::Identity();
             return p;
         }
 
@@ -107,6 +110,12 @@ namespace tfusion
         Vec3f light_pose;
         std::shared_ptr<SceneParams> sceneParams;   // the reference leaks a raw pointer (topfu.cpp:50)
         int n_buckets, n_excess, n_blocks, vis_capacity, max_render_blocks;
+        // colour (an addition): Voxel_s_rgb voxels, the RGB image of operator()(depth, rgba)
+        // integrated (VoxelTypes.hpp:39-67, SceneReconstructionEngine.hpp:116-148); rgb_intr all 0
+        // = the depth intrinsics; depth_to_rgb = trafo_rgb_to_depth.calib_inv (identity: registered)
+        bool integrate_colour;
+        Intr rgb_intr;
+        Affine3f depth_to_rgb;
 
         tf_params to_c() const
         {
@@ -127,6 +136,9 @@ namespace tfusion
             }
             c.n_buckets = n_buckets; c.n_excess = n_excess; c.n_blocks = n_blocks;
             c.vis_capacity = vis_capacity; c.max_render_blocks = max_render_blocks;
+            c.voxel_rgb = integrate_colour ? 1 : 0;
+            c.rgb_intr[0] = rgb_intr.fx; c.rgb_intr[1] = rgb_intr.fy; c.rgb_intr[2] = rgb_intr.cx; c.rgb_intr[3] = rgb_intr.cy;
+            depth_to_rgb.toRt(c.depth_to_rgb);
             return c;
         }
     };
@@ -172,9 +184,24 @@ namespace tfusion
         // TopFu::operator() (topfu.cpp:161-330); the colour image is unused by the reference too
         bool operator()(const cuda::Depth& depth, const cuda::Image& = cuda::Image())
         {
+            return frame(depth, nullptr);
+        }
+        // with params().integrate_colour: the frame's RGBA image (Vector4u, the engine's view->rgb)
+        // integrated into the Voxel_s_rgb colour (an addition)
+        bool operator()(const cuda::Depth& depth, const cuda::image4u& rgba)
+        {
+            return frame(depth, &rgba);
+        }
+
+    private:
+        bool frame(const cuda::Depth& depth, const cuda::image4u* rgba)
+        {
             float rt[12];
             tf_stats st;
-            const tf_status s = tf_process_frame(ctx_, depth.ptr(), depth.step(), rt, &st);
+            const tf_status s = rgba && !rgba->empty()
+                ? tf_process_frame_rgb(ctx_, depth.ptr(), depth.step(), reinterpret_cast<const uint8_t*>(rgba->ptr()),
+                                       rgba->step(), rt, &st)
+                : tf_process_frame(ctx_, depth.ptr(), depth.step(), rt, &st);
             if (s == TF_ICP_FAIL) {                   // reset(), return false (topfu.cpp:263-264)
                 frame_counter_ = 0;
                 poses_.clear();
@@ -186,6 +213,8 @@ namespace tfusion
             ++frame_counter_;
             return true;
         }
+
+    public:
 
         // TopFu::renderImage (topfu.cpp:332-377): grey shading of the current pose.  The type
         // argument (default: the reference's RENDER_SHADED_GREYSCALE) selects one of the engine's

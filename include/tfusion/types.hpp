@@ -154,6 +154,7 @@ namespace tfusion
 
     struct Point { union { float data[4]; struct { float x, y, z; }; }; };
     typedef Point Normal;
+    struct Vector3u { unsigned char x, y, z; };
     struct Vector4u { unsigned char x, y, z, w; };
     struct Vector4f {
         float x, y, z, w;

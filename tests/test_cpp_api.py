@@ -63,6 +63,25 @@ def test_swap_api_runs(tmp_path):
     assert m and int(m.group(2)) > 0 and int(m.group(3)) > 0, r.stdout
 
 
+def test_colour_api_builds_and_links():
+    exe = _build("colour_check")
+    syms = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True, check=True).stdout
+    for fn in ("tf_process_frame_rgb", "tf_scene_integrate_rgb", "tf_render_image_type", "tf_vis_render_image"):
+        assert fn in syms, fn
+
+
+@pytest.mark.gpu
+def test_colour_api_matches_topfu():
+    """apps/colour_check: TopFu::operator()(depth, rgba) with integrate_colour against the same
+    frames over a Scene<Voxel_s_rgb> and IntegrateIntoScene(..., rgb): hash, voxel plane, colour
+    plane and RENDER_COLOUR_FROM_VOLUME bit-exact; an unregistered colour camera."""
+    exe = _build("colour_check")
+    r = subprocess.run([exe, "24", "320", "240"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = re.search(r"coloured voxels (\d+) lit pixels (\d+): MATCH", r.stdout)
+    assert m and int(m.group(1)) > 10000 and int(m.group(2)) > 10000, r.stdout
+
+
 @pytest.mark.gpu
 def test_engine_api_matches_topfu():
     """apps/engine_check: TopFu::operator() against the same frames spelled out over the L4
