@@ -81,13 +81,18 @@ def parse():
     return ap.parse_args()
 
 
-def stage_bytes(stage, p, nvis, W, H):
-    """Algorithmic HBM bytes of ONE launch of a stage."""
+def stage_bytes(stage, p, nvis, W, H, lanes=None):
+    """Algorithmic HBM bytes of ONE launch of a stage.  integrate: the visible
+    entries, the depth image and the voxel bytes the update needs -- the 16-B lanes (4 voxels)
+    with an update read, those whose value changed written (`lanes` = (read, written) per
+    launch, counted on the device); without counts every voxel read and written."""
     if stage == "raycast_icp":
         # both raycasts in one launch: float4 ray image + uchar4 grey image out, every visible
         # block read once per raycast
         return W * H * (16 + 4) + 2 * nvis * (2048 + 16)
     if stage == "integrate":
+        if lanes is not None:
+            return nvis * 20 + W * H * 4 + 16 * (lanes[0] + lanes[1])
         return nvis * (4096 + 20) + W * H * 4           # voxel R+W + entry/id + depth image
     if stage == "grey":
         return W * H * (16 + 4) + nvis * (2048 + 16)
@@ -250,12 +255,19 @@ def c3_integrate(args):
     """C3I ("integrate over the active list is truly HBM-bound"): one
     IntegrateIntoScene pass per step over the c3_scene() blocks against the wall at 1.5 m, all
     passes back to back on the context stream, timed by HIP events.  Algorithmic bytes per
-    pass: Nvis x (4096 voxel R+W + 20 entry/id) + W x H x 4 (dists)."""
+    pass: Nvis x 20 (entry/id) + W x H x 4 (dists) + 16 B per voxel lane read (those with an
+    update: a depth and eta >= -mu) and per lane written (those that changed), counted on the
+    device; the reference's pass reads and writes every voxel (Nvis x 4096 B), reported beside
+    as the reference-equivalent rate."""
     tf, p, W, H, vox, nb = c3_scene()
     I = np.eye(4, dtype=np.float32)[:3]
     tf.time_stage("integrate", I, 2)                        # warm-up
+    tf.reset_totals()
     ms = tf.time_stage("integrate", I, args.steps)
-    b = nb * (4096 + 20) + W * H * 4
+    tot = tf.totals()
+    rd, wr = tot["integrate_lanes_read"] / args.steps, tot["integrate_lanes_written"] / args.steps
+    b = stage_bytes("integrate", p, nb, W, H, (rd, wr))
+    b_ref = nb * (4096 + 20) + W * H * 4
     ach = b / (ms * 1e-3) / 1e9
     pmc = _pmc("C3I", "integrate")
     out = {"metric": f"IntegrateIntoScene passes/sec over {nb} active voxel blocks @{W}x{H}, {vox * 1000:g} mm",
@@ -266,8 +278,12 @@ def c3_integrate(args):
                       "cols": W, "rows": H, "voxel_m": vox, "active_blocks": int(nb), "parallelism": "replicas1"},
            "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": pmc.get("bytes_per_launch"),
-                        "kernel": "k_integrate", "algorithmic_bytes_per_launch": b, "avg_launch_ms": round(ms, 5),
-                        "timing": "HIP events around back-to-back launches on the context stream"}}
+                        "kernel": "k_integrate", "algorithmic_bytes_per_launch": int(b), "avg_launch_ms": round(ms, 5),
+                        "timing": "HIP events around back-to-back launches on the context stream",
+                        "voxel_lanes_read": int(rd), "voxel_lanes_written": int(wr),
+                        "voxel_lanes_total": int(nb) * 128,
+                        "reference_equivalent_bytes": int(b_ref),
+                        "reference_equivalent_GBs": round(b_ref / (ms * 1e-3) / 1e9, 2)}}
     print(json.dumps(out))
     tf.close()
 
@@ -450,14 +466,20 @@ def main():
     tot = tf.totals()
     st = tf.stats()
     prof = {}
+    lanes_bd = nvis_bd = None
     if n_breakdown:
         # per-stage breakdown: a fresh context replays the warm-up and the first frames of the
         # timed region with every stage timed (outside the timed region)
         tb = TopFu(default_params(**pkw), device=local_rank)
         tb.process_frames(base, args.warmup * F)
         tb.profile(True)
+        tb.reset_totals()
         tb.process_frames(base + args.warmup * F * frame_bytes, n_breakdown)
         prof = tb.profile_read()
+        tbt = tb.totals()
+        n_int = max(1, tbt["frames"] - tbt["resets"])
+        lanes_bd = (tbt["integrate_lanes_read"] / n_int, tbt["integrate_lanes_written"] / n_int)
+        nvis_bd = tbt["visible_sum"] / n_int
         tb.close()
         torch.cuda.synchronize()
     # TopFu::operator() per call (one host round trip per frame, no lookahead), beside the
@@ -500,7 +522,10 @@ def main():
                 ms = timed_ms if (k == dominant and timed_ms) else per_stage.get(k)
                 if not ms:
                     continue
-                b = stage_bytes(k, tf.params(), nvis_mean, W, H)
+                if k == "integrate" and lanes_bd is not None:    # lanes counted in the breakdown pass
+                    b = stage_bytes(k, tf.params(), nvis_bd, W, H, lanes_bd)
+                else:
+                    b = stage_bytes(k, tf.params(), nvis_mean, W, H)
                 ach = b / (ms * 1e-3) / 1e9
                 roof_all[k] = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                "frac": round(ach / PEAK_HBM_GBS, 5),

@@ -334,6 +334,8 @@ typedef struct tf_totals {
     long long tiles_sum;            /* noTotalBlocks summed over the tracked frames */
     long long swapped_in;           /* blocks swapped in (use_swapping) */
     long long swapped_out;          /* blocks swapped out (use_swapping) */
+    long long integrate_lanes_read;     /* 16-B voxel lanes (4 voxels) integration read: those with an update */
+    long long integrate_lanes_written;  /* ... and wrote back: those whose value changed */
 } tf_totals;
 tf_status tf_get_totals(tf_ctx* ctx, tf_totals* totals);
 tf_status tf_reset_totals(tf_ctx* ctx);

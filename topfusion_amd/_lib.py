@@ -48,7 +48,8 @@ class TfStats(ctypes.Structure):
 
 class TfTotals(ctypes.Structure):
     _fields_ = [(n, ctypes.c_longlong) for n in ("frames", "frames_tracked", "resets", "visible_sum", "tiles_sum",
-                                                 "swapped_in", "swapped_out")]
+                                                 "swapped_in", "swapped_out", "integrate_lanes_read",
+                                                 "integrate_lanes_written")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -157,7 +158,10 @@ def load():
         "tf_profile_reset": ([P], I),
         "tf_profile_read": ([P, P, P, I], I),
     }
+    override = bool(os.environ.get("TFUSION_HIP_LIB"))    # an A/B build (tools/gpu_ab_c3i.sh) may be older
     for name, (args, res) in sig.items():
+        if override and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

@@ -5,6 +5,8 @@
 // reference has ~27).  ICP, pose algebra and every counter live on the device
 // (TfDevState); the host only reads the frame's bool + counters back.
 #include "tf_internal.h"
+
+#include <vector>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -105,7 +107,7 @@ static void ctx_free(tf_ctx* c)
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockBox, c->blockZ, c->blockTiles, c->blockOff, c->edChunk, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->frame_ok, c->frame_mode, c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
-                     c->vba_rgb_guard, c->rgb_in };
+                     c->vba_rgb_guard, c->rgb_in, c->integ_cnt };
     for (void* b : bufs) if (b) (void)hipFree(b);
     // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
     float4* maps[4] = { c->curr_pts[0], c->curr_nrm[0], c->prev_pts[0], c->prev_nrm[0] };
@@ -226,6 +228,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->icp_ticket, 64);
     ALLOC(c->icp_tagged, sizeof(unsigned long long) * TF_ICP_TAG_WORDS);
     ALLOC(c->st, sizeof(TfDevState));
+    ALLOC(c->integ_cnt, sizeof(long long) * 2 * TF_INTEG_WG);
     if (pin->use_swapping) {        // the GlobalCache in HBM: 2 KiB per hash entry + flags
         ALLOC(c->swapState, ntot_pad);
         ALLOC(c->swapFlags, ntot_pad);
@@ -256,6 +259,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = tfk_grid_clear(c);
     if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)c->vba_guard, 0x7fff, TF_BLK3, c->stream);   // Voxel_s()
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_tagged, 0, sizeof(unsigned long long) * TF_ICP_TAG_WORDS, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->integ_cnt, 0, sizeof(long long) * 2 * TF_INTEG_WG, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->allocType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->winnerKey, 0xff, sizeof(int) * ntot_pad, c->stream);
     // the request pass counts into these; every frame's k_vis_count returns them to zero
@@ -461,6 +465,7 @@ extern "C" tf_status tf_profile_enable(tf_ctx* c, int enable)
         for (int i = 0; i < 2 * TF_NUM_STAGES * TF_PROF_RING; ++i) TF_CHECK(hipEventCreate(&c->prof_ev[i]));
     }
     c->prof_enabled = enable ? 1 : 0;
+    c->count_lanes = enable ? 1 : 0;
     c->prof_mask = (1u << TF_NUM_STAGES) - 1;
     c->prof_period = 1;
     c->prof_seq = 0;
@@ -473,6 +478,7 @@ extern "C" tf_status tf_profile_stages(tf_ctx* c, unsigned mask)
     tf_status s = tf_profile_enable(c, mask != 0);
     if (s != TF_OK) return s;
     c->prof_mask = mask;
+    c->count_lanes = 0;          // (selected stages: a timed run, no counting atomics in it)
     return TF_OK;
 }
 
@@ -1141,14 +1147,20 @@ extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)
     t->frames = d->tot_frames; t->frames_tracked = d->tot_tracked; t->resets = d->tot_resets;
     t->visible_sum = d->tot_visible; t->tiles_sum = d->tot_tiles;
     t->swapped_in = d->tot_swap_in; t->swapped_out = d->tot_swap_out;
+    t->integrate_lanes_read = t->integrate_lanes_written = 0;
+    std::vector<long long> h(2 * TF_INTEG_WG);
+    TF_CHECK(hipMemcpyAsync(h.data(), c->integ_cnt, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < TF_INTEG_WG; ++i) { t->integrate_lanes_read += h[2 * i]; t->integrate_lanes_written += h[2 * i + 1]; }
     return TF_OK;
 }
 
 extern "C" tf_status tf_reset_totals(tf_ctx* c)
 {
     if (!c) return TF_INVALID_ARG;
-    const long long zero[7] = { 0, 0, 0, 0, 0, 0, 0 };
-    TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, tot_frames), zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
+    const size_t b = offsetof(TfDevState, tot_frames), e = offsetof(TfDevState, tot_pad_) + sizeof(long long);
+    TF_CHECK(hipMemsetAsync((char*)c->st + b, 0, e - b, c->stream));
+    TF_CHECK(hipMemsetAsync(c->integ_cnt, 0, sizeof(long long) * 2 * TF_INTEG_WG, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }

@@ -310,6 +310,8 @@ struct tf_ctx {
     unsigned long long* icp_tagged;   // persistent ICP: [256][28] tagged column sums + [16] broadcast
     int icp_persistent;      // 1: one launch per frame (k_icp_frame), 0: one launch per iteration
     int icp_max_cta;
+    int count_lanes;         // frame path: count integration's voxel lanes (profiling)
+    long long* integ_cnt;    // [TF_INTEG_WG][2] per-workgroup running counts of voxel lanes read / written
     float min_cosine, dist2_thres;
     // device state
     TfDevState* st;
@@ -368,6 +370,7 @@ hipError_t tfk_icp_maps_end(tf_ctx* c, int slot);
 #define TF_END_BLOCKS 256        // workgroups of the frame-end / in-frame reset pass
 hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0);
 #define TF_ED_BLOCKS 256         // workgroups of the expected-depth projection pass
+#define TF_INTEG_WG 2048         // workgroups of the integration pass (grid-stride)
 hipError_t tfk_frame0_matrices(tf_ctx* c);
 // swapping (tf_swap.hip): reallocation of listed swapped-out entries (after the visible list),
 // and IntegrateGlobalIntoLocal + SaveToGlobalMemory (after integration)

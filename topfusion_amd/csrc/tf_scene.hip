@@ -183,12 +183,65 @@ __device__ __forceinline__ bool alloc_segment(const AllocArgs& a, const float* i
     return true;
 }
 
+// An allocation request of this workgroup's 16x16 pixel tile: requests are aggregated per hash
+// entry in LDS (the raster-order maximum key, the request type) and go out as one global
+// atomicMax per entry and tile when the tile is done -- every pixel whose segment crosses a new
+// block requests it, a few hundred atomics on one word per new block at C2, serialised at the
+// memory side.  The maximum and the stores are order-independent: the same winners, types and
+// counts.  A full table sends the request straight to memory.
+#define AR_SLOTS 256
+struct AllocLds {
+    int idx[AR_SLOTS];                 // hash entry index, -1 free
+    int key[AR_SLOTS];                 // max requesting key
+    unsigned char exc[AR_SLOTS];       // request type: excess (chain end) or bucket
+    int seen[AR_SLOTS];                // entries found through the block grid (their visType store made)
+};
+
+// visType = 1 for an entry the block grid holds: once per entry and tile (a block is found by
+// every step of every pixel crossing it; the stores are all the same byte)
+__device__ __forceinline__ void alloc_mark_found(AllocLds& t, unsigned char* __restrict__ visType, int hashIdx)
+{
+    unsigned h = ((unsigned)hashIdx * 2654435761u) >> 24;
+    for (int probe = 0; probe < AR_SLOTS; ++probe, h = (h + 1) & (AR_SLOTS - 1)) {
+        const int prev = atomicCAS(&t.seen[h], -1, hashIdx);
+        if (prev == hashIdx) return;                       // marked by this tile already
+        if (prev == -1) break;                             // first in this tile
+    }
+    visType[hashIdx] = 1;
+}
+
+__device__ __forceinline__ void alloc_request_global(int* __restrict__ winnerKey, int* __restrict__ counts, int hashIdx,
+                                                     bool isExcess, int key)
+{
+    // raster-order last writer; the first request of an entry this frame (the key was -1)
+    // counts it for its chunk (the hash is read-only here, so an entry's request type is the
+    // same for every requester)
+    if (atomicMax(&winnerKey[hashIdx], key) < 0) {
+        atomicAdd(&counts[2 * (hashIdx / CHUNK)], 1);
+        if (isExcess) atomicAdd(&counts[2 * (hashIdx / CHUNK) + 1], 1);
+    }
+}
+
+__device__ __forceinline__ bool alloc_request_lds(AllocLds& t, int hashIdx, bool isExcess, int key)
+{
+    unsigned h = ((unsigned)hashIdx * 2654435761u) >> 24;
+    for (int probe = 0; probe < AR_SLOTS; ++probe, h = (h + 1) & (AR_SLOTS - 1)) {
+        const int prev = atomicCAS(&t.idx[h], -1, hashIdx);
+        if (prev == -1 || prev == hashIdx) {
+            atomicMax(&t.key[h], key);
+            t.exc[h] = isExcess ? 1 : 0;
+            return true;
+        }
+    }
+    return false;
+}
+
 // the hash probe of one step whose block the grid does not hold: found (outside the grid) ->
 // visible type; otherwise an allocation request in the bucket (1) or at the chain end (2)
 __device__ __forceinline__ void alloc_probe(const AllocArgs& a, const TfHashEntry* __restrict__ hash,
                                             unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType,
                                             int* __restrict__ winnerKey, int* __restrict__ counts,
-                                            int bx, int by, int bz, int key)
+                                            int bx, int by, int bz, int key, AllocLds& lt)
 {
     {
         int hashIdx = tf_hash_index(bx, by, bz, a.mask);
@@ -212,16 +265,10 @@ __device__ __forceinline__ void alloc_probe(const AllocArgs& a, const TfHashEntr
                 }
                 isExcess = true;
             }
-            if (!found) {
+            if (!found && !alloc_request_lds(lt, hashIdx, isExcess, key)) {
                 allocType[hashIdx] = isExcess ? 2 : 1;
                 if (!isExcess) visType[hashIdx] = 1;
-                // raster-order last writer; the first request of an entry this frame (the key
-                // was -1) counts it for its chunk (the hash is read-only here, so an entry's
-                // request type is the same for every requester)
-                if (atomicMax(&winnerKey[hashIdx], key) < 0) {
-                    atomicAdd(&counts[2 * (hashIdx / CHUNK)], 1);
-                    if (isExcess) atomicAdd(&counts[2 * (hashIdx / CHUNK) + 1], 1);
-                }
+                alloc_request_global(winnerKey, counts, hashIdx, isExcess, key);
             }
         }
     }
@@ -241,11 +288,15 @@ k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEnt
         return;
     }
     if (st->abort) return;
+    __shared__ AllocLds lt;
+    lt.idx[threadIdx.x] = -1;
+    lt.key[threadIdx.x] = -1;
+    lt.seen[threadIdx.x] = -1;
+    __syncthreads();
     const int bx = (int)blockIdx.x % gx, by = (int)blockIdx.x / gx;
     const int x = bx * 16 + (threadIdx.x & 15), y = by * 16 + (threadIdx.x >> 4);
-    if (x >= a.W || y >= a.H) return;
-    float point[3], dir[3]; int noSteps;
-    if (!alloc_segment(a, st->invM_alloc, x, y, point, dir, &noSteps)) return;
+    float point[3], dir[3]; int noSteps = 0;
+    if (!(x < a.W && y < a.H && alloc_segment(a, st->invM_alloc, x, y, point, dir, &noSteps))) noSteps = 0;
     const int key0 = (y * a.W + x) * 64;
     // Steps in batches of 8: the block grid answers "already allocated" for every step with one
     // batch of independent loads (the grid mirrors the hash exactly, tf_internal.h); only the
@@ -266,9 +317,18 @@ k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEnt
         for (int j = 0; j < 8; ++j) {
             const int i = i0 + j;
             if (i >= noSteps) break;
-            if (g[j].x >= 0) { visType[g[j].x] = 1; continue; }     // found, ptr >= 0 (swapped-out entries have no cell: the probe finds them)
-            alloc_probe(a, hash, allocType, visType, winnerKey, counts, sbx[j], sby[j], sbz[j], key0 + i);
+            if (g[j].x >= 0) { alloc_mark_found(lt, visType, g[j].x); continue; }   // found, ptr >= 0 (swapped-out entries have no cell: the probe finds them)
+            alloc_probe(a, hash, allocType, visType, winnerKey, counts, sbx[j], sby[j], sbz[j], key0 + i, lt);
         }
+    }
+    // the tile's requests: one global request per entry
+    __syncthreads();
+    const int hi = lt.idx[threadIdx.x];
+    if (hi >= 0) {
+        const bool exc = lt.exc[threadIdx.x] != 0;
+        allocType[hi] = exc ? 2 : 1;
+        if (!exc) visType[hi] = 1;
+        alloc_request_global(winnerKey, counts, hi, exc, lt.key[threadIdx.x]);
     }
 }
 
@@ -768,7 +828,7 @@ __device__ __forceinline__ void nt_store16(uint4* p, uint4 v)
 template <bool RGB>
 __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry& e, const TfHashEntry& e2, int vx,
                                            int vy, int vz, const float* M, const IntegArgs& a, uint4* p, uint4* p2,
-                                           const float* rw, bool stream, const float* Mr, int lin)
+                                           const float* rw, bool stream, const float* Mr, int lin, int* n_rd, int* n_wr)
 {
     float z[8];
     int di[8];
@@ -795,12 +855,20 @@ __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry&
         eta[k] = -1.0f;
         if (ok[k]) w[k] = integ_update(w[k], dm[k], z[k], a, rw, &eta[k]);
     }
+    // a lane whose four voxels all kept their value (behind the surface by more than mu, outside
+    // the image, no depth) stores nothing: at HBM scale most of a frustum lies behind the surface.
+    // (The voxels are still read up front, with the depth samples: skipping the reads of such
+    // lanes would put a second dependent round trip on every lane, slower on the C3I scene.)
+    const bool ch1 = e.ptr >= 0 && ((w[0] ^ v.x) | (w[1] ^ v.y) | (w[2] ^ v.z) | (w[3] ^ v.w)) != 0;
+    const bool ch2 = e2.ptr >= 0 && ((w[4] ^ v2.x) | (w[5] ^ v2.y) | (w[6] ^ v2.z) | (w[7] ^ v2.w)) != 0;
+    *n_rd += (int)(e.ptr >= 0) + (int)(e2.ptr >= 0);
+    *n_wr += (int)ch1 + (int)ch2;
     if (stream) {
-        if (e.ptr >= 0) nt_store16(p, make_uint4(w[0], w[1], w[2], w[3]));
-        if (e2.ptr >= 0) nt_store16(p2, make_uint4(w[4], w[5], w[6], w[7]));
+        if (ch1) nt_store16(p, make_uint4(w[0], w[1], w[2], w[3]));
+        if (ch2) nt_store16(p2, make_uint4(w[4], w[5], w[6], w[7]));
     } else {
-        if (e.ptr >= 0) *p = make_uint4(w[0], w[1], w[2], w[3]);
-        if (e2.ptr >= 0) *p2 = make_uint4(w[4], w[5], w[6], w[7]);
+        if (ch1) *p = make_uint4(w[0], w[1], w[2], w[3]);
+        if (ch2) *p2 = make_uint4(w[4], w[5], w[6], w[7]);
     }
     if (RGB) {
 #pragma unroll
@@ -826,8 +894,8 @@ __device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry&
 
 template <bool WITH_ED, bool RGB>
 __global__ void __launch_bounds__(256)
-k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
-            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed)
+k_integrate(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed, long long* __restrict__ cnt)
 {
     // WITH_ED: the first TF_ED_BLOCKS workgroups run CreateExpectedDepths' projection pass (it
     // reads only the visible list and the pose; integration writes only voxels): one launch
@@ -878,6 +946,7 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
     // either is computed: twice the bytes in flight per wave (at C3 scale, 2^21 blocks, the
     // pass is a stream over 8.6 GB)
     const int stride = nblk * 2;
+    int n_rd = 0, n_wr = 0;
     for (int i = bid * 2 + half; i < n; i += 2 * stride) {
         const int i2 = i + stride;
         const bool has2 = i2 < n;                    // (loads unconditional: both chains together)
@@ -889,10 +958,25 @@ k_integrate(IntegArgs a, const TfDevState* __restrict__ st, const TfHashEntry* _
         uint4* p2 = (uint4*)(vba + (size_t)(e2.ptr < 0 ? 0 : e2.ptr) * TF_BLK3 + lin);
         // the voxel stream is read and written once per pass: non-temporal, so it does not
         // evict the depth image every voxel samples from L2
+        // the voxel stream is read and written once per pass: non-temporal, so it does not
+        // evict the depth image every voxel samples from L2
         uint4 v, v2;
         if (stream) { v = nt_load16(p); v2 = nt_load16(p2); }
         else { v = *p; v2 = *p2; }
-        integ_pair<RGB>(v, v2, e, e2, vx, vy, vz, M, a, p, p2, rw, stream, Mr, lin);
+        integ_pair<RGB>(v, v2, e, e2, vx, vy, vz, M, a, p, p2, rw, stream, Mr, lin, &n_rd, &n_wr);
+    }
+    // lanes read / written (profiling / stand-alone passes): the workgroup's running counts in
+    // its own slot, plain read-modify-write (launches on one stream; no atomics to contend)
+    if (!cnt) return;
+    __shared__ int wsum[2][4];
+    const int wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) { n_rd += __shfl_xor(n_rd, o, 64); n_wr += __shfl_xor(n_wr, o, 64); }
+    if ((threadIdx.x & 63) == 0) { wsum[0][wv] = n_rd; wsum[1][wv] = n_wr; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        cnt[2 * bid] += (long long)wsum[0][0] + wsum[0][1] + wsum[0][2] + wsum[0][3];
+        cnt[2 * bid + 1] += (long long)wsum[1][0] + wsum[1][1] + wsum[1][2] + wsum[1][3];
     }
 }
 
@@ -918,15 +1002,20 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
         for (int row = 0; row < 4; ++row)
             a.D[4 * col + row] = row < 3 ? d[4 * row + col] : (col == 3 ? 1.0f : 0.0f);
     EdArgs ed = {};
-    const dim3 g(2048), b(256);
+    // 2048 workgroups, 8 per CU (7 are resident at once under the SGPR budget): measured faster
+    // on the C3I scene than a grid of exactly the resident count (2.43 vs 2.75 ms)
+    const int nwg = TF_INTEG_WG;
+    long long* count = (frame_path ? c->count_lanes : 1) ? c->integ_cnt : nullptr;
+    const dim3 b(256);
     if (with_ed) {
         tf_ed_args(c, &ed);
-        const dim3 ge(2048 + TF_ED_BLOCKS);
-        if (rgb) hipLaunchKernelGGL((k_integrate<true, true>), ge, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed);
-        else hipLaunchKernelGGL((k_integrate<true, false>), ge, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed);
+        const dim3 ge(nwg + TF_ED_BLOCKS);
+        if (rgb) hipLaunchKernelGGL((k_integrate<true, true>), ge, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
+        else hipLaunchKernelGGL((k_integrate<true, false>), ge, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
     } else {
-        if (rgb) hipLaunchKernelGGL((k_integrate<false, true>), g, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed);
-        else hipLaunchKernelGGL((k_integrate<false, false>), g, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed);
+        const dim3 g(nwg);
+        if (rgb) hipLaunchKernelGGL((k_integrate<false, true>), g, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
+        else hipLaunchKernelGGL((k_integrate<false, false>), g, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
     }
     return hipGetLastError();
 }
