@@ -38,8 +38,10 @@ SINGLE_KERNEL_STAGES = tuple(KERNEL_OF_STAGE)
 C3_CAPACITY = dict(n_buckets=1 << 22, n_excess=1 << 20, n_blocks=(1 << 21) - 1, vis_capacity=1 << 21,
                    max_render_blocks=1 << 20)
 CONFIGS = {
-    "C2": dict(cols=640, rows=480, voxel=0.005, capacity={}, walk=False, steps=10),
-    "C3": dict(cols=1280, rows=960, voxel=0.002, capacity=C3_CAPACITY, walk=False, steps=10),
+    # C2 / C3 default to the driver's own command (--steps 20 --warmup 5), so the committed line
+    # and the driver's time the same 640 frames of the orbit
+    "C2": dict(cols=640, rows=480, voxel=0.005, capacity={}, walk=False, steps=20),
+    "C3": dict(cols=1280, rows=960, voxel=0.002, capacity=C3_CAPACITY, walk=False, steps=20),
     # C5 hash stress: 10 mm voxels, 50 k-frame random walk (seed 13 + rank, <= 1 cm / 0.5 deg per
     # frame), reference capacities; frames rendered on the GPU (synth.render_depth_torch)
     "C5": dict(cols=640, rows=480, voxel=0.01, capacity={}, walk=True, steps=1563),
@@ -50,8 +52,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None,
-                    help="timed steps of --frames-per-step frames each (default: C2/C3 10, C5 1563 = 50 k frames)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed warm-up steps (default 2)")
+                    help="timed steps of --frames-per-step frames each (default: C2/C3 20, C5 1563 = 50 k frames)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed warm-up steps (default 5)")
     ap.add_argument("--frames-per-step", type=int, default=32,
                     help="frames per step: one tf_process_frames batch (32 = one enqueue group)")
     ap.add_argument("--per-call-frames", type=int, default=64,
@@ -412,7 +414,7 @@ def main():
     if args.steps is None:
         args.steps = cfg["steps"]
     if args.warmup is None:
-        args.warmup = 2
+        args.warmup = 5
     W = args.cols or cfg["cols"]
     H = args.rows or cfg["rows"]
     if args.voxel is None:

@@ -341,6 +341,8 @@ tf_status tf_get_totals(tf_ctx* ctx, tf_totals* totals);
 tf_status tf_reset_totals(tf_ctx* ctx);
 /* Measurement: `iters` back-to-back launches of one stage's kernels on the context stream
  * with the pose/matrices of tf_stage_* (stage = TF_STAGE_INTEGRATE: k_integrate;
+ * TF_STAGE_EXPECTED_DEPTHS: k_ed_fill over the boxes one projection pass of the current list
+ * made first;
  * TF_STAGE_RAYCAST_ICP: castRay<true> into raycastResult; TF_STAGE_RAYCAST_RENDER: the frame's
  * k_raycast_pair -- castRay<true> + renderImage's castRay and grey, over the current range
  * image), timed by HIP events on that stream; *ms_per_iter = elapsed / iters.  The scene is

@@ -167,8 +167,30 @@ def test_sequence(oracle_mod, cols, rows, nframes, icp_schedule):
     """Whole TopFu::operator() frames: state identical after every frame."""
     g, o = make_pair(oracle_mod, cols, rows)
     _check_schedule(g, icp_schedule)
+    _run_sequence(g, o, cols, rows, nframes)
+
+
+def test_sequence_ed_atomic(oracle_mod, monkeypatch):
+    """k_ed_fill's device-scope-atomic path (taken past ED_LDS_MAX_N visible entries, forced
+    here with a threshold of 0): the whole range image after every frame, spill area included."""
+    monkeypatch.setenv("TFUSION_ED_LDS_MAX_N", "0")
+    g, o = make_pair(oracle_mod, 320, 240)
+    _run_sequence(g, o, 320, 240, 16)
+
+
+@pytest.mark.parametrize("lds_max_n", ["16384", "0"])
+def test_sequence_render_block_cap(oracle_mod, monkeypatch, lds_max_n):
+    """MAX_RENDERING_BLOCKS engaged (a cap of 48 tiles): blocks whose tiles do not fit are
+    dropped in visible-list order (VisualisationHelper.cu:70-74), on both k_ed_fill paths."""
+    monkeypatch.setenv("TFUSION_ED_LDS_MAX_N", lds_max_n)
+    g, o = make_pair(oracle_mod, 320, 240, max_render_blocks=48)
+    capped = _run_sequence(g, o, 320, 240, 8, need_spill=False)
+    assert capped > 0, "the cap never engaged"
+
+
+def _run_sequence(g, o, cols, rows, nframes, need_spill=True):
     seq = synth.orbit_sequence(nframes, cols, rows, seed=7)
-    spilled = 0
+    spilled = capped = 0
     for k in range(nframes):
         okg = g(seq[k])
         oko = o(seq[k])
@@ -178,6 +200,7 @@ def test_sequence(oracle_mod, cols, rows, nframes, icp_schedule):
             assert sg[key] == so[key], f"frame {k} {key}: gpu {sg[key]} oracle {so[key]}"
         if k > 0:
             assert sg["noTotalBlocks"] == so["noTotalBlocks"], f"frame {k} noTotalBlocks"
+            capped += int(oko and so["noTotalBlocks"] == o.params.max_render_blocks)
         assert_bit_exact(f"frame {k} pose", g.getCameraPose()[:3, :4], o.pose())
         if k > 0 and oko:
             assert_bit_exact(f"frame {k} renderImage grey", g.frame_grey(), o.frame_grey())
@@ -189,7 +212,7 @@ def test_sequence(oracle_mod, cols, rows, nframes, icp_schedule):
             spill = rg.copy()
             spill[:rr, :rc] = 0
             spilled += int((spill[..., 1] > np.float32(0.05)).sum())
-    assert spilled > 0, "no frame filled the range image outside its /8 region"
+    assert spilled > 0 or not need_spill, "no frame filled the range image outside its /8 region"
     compare_scene(g, o, "final")
     assert_bit_exact("final raycast", g.raycast_result(), o.raycast_result())
     for l in range(3):
@@ -197,6 +220,7 @@ def test_sequence(oracle_mod, cols, rows, nframes, icp_schedule):
         op, on = o.prev_maps(l)
         assert_bit_exact(f"final prev points L{l}", gp, op)
         assert_bit_exact(f"final prev normals L{l}", gn, on)
+    return capped
 
 
 def test_sequence_c3_geometry(oracle_mod):

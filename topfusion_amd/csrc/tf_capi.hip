@@ -93,6 +93,7 @@ static bool params_valid(const tf_params* p)
     // steps per pixel ceil(2*|e-s|) with |e-s| ~ 2*mu/(8*voxel) must fit the 6-bit key field
     if (4.0f * p->mu / (8.0f * p->voxelSize) + 2.0f > 60.0f) return false;
     if ((double)p->cols * p->rows * 64.0 > 2147483000.0) return false;
+    if (p->cols > 65535 || p->rows > 65535) return false;               // k_ed_fill's 16-bit box records
     if (p->use_swapping && (p->swap_transfer_blocks <= 0 || p->swap_transfer_blocks > p->n_buckets + p->n_excess)) return false;
     // the GlobalCache holds Voxel_s blocks: a swapping colour scene would need the colour half
     // swapped too (CombineVoxelInformation's colour part) -- not built
@@ -105,8 +106,8 @@ static void ctx_free(tf_ctx* c)
     if (!c) return;
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
-                     c->blockBox, c->blockZ, c->blockTiles, c->blockOff, c->edChunk, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
-                     c->frame_ok, c->frame_mode, c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
+                     c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
+                     c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
                      c->vba_rgb_guard, c->rgb_in, c->integ_cnt };
     for (void* b : bufs) if (b) (void)hipFree(b);
     // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
@@ -199,11 +200,11 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->range_render, sizeof(float) * 2 * npx);
     ALLOC(c->raycast, sizeof(float) * 4 * npx);
     ALLOC(c->grey, sizeof(uchar4) * npx);
-    ALLOC(c->blockBox, sizeof(int4) * (size_t)pin->vis_capacity);
-    ALLOC(c->blockZ, sizeof(float2) * (size_t)pin->vis_capacity);
+    ALLOC(c->blockRec, sizeof(uint4) * (size_t)pin->vis_capacity);
     ALLOC(c->blockTiles, sizeof(int) * (size_t)pin->vis_capacity);
     ALLOC(c->blockOff, sizeof(int) * (size_t)pin->vis_capacity);
     ALLOC(c->edChunk, sizeof(int) * ((size_t)pin->vis_capacity / 256 + 1));
+    ALLOC(c->edSpill, sizeof(int2) * (size_t)ed_nrows(c->H));
     ALLOC(c->depth_in, sizeof(uint16_t) * npx);
     ALLOC(c->dists, sizeof(float) * npx);
     {   // each map's three pyramid levels are contiguous in one allocation
@@ -222,12 +223,13 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         for (int k = 0; k < 2; ++k) ALLOC(c->d0_buf[k], sizeof(uint16_t) * (size_t)c->lw[0] * c->lh[0]);
         c->depth_pyr[0] = c->d0_buf[0];
     }
-    ALLOC(c->frame_ok, sizeof(int) * TF_PROF_RING);
-    ALLOC(c->frame_mode, sizeof(int) * TF_PROF_RING);
     ALLOC(c->icp_partial, sizeof(float) * 28 * 256);
     ALLOC(c->icp_ticket, 64);
     ALLOC(c->icp_tagged, sizeof(unsigned long long) * TF_ICP_TAG_WORDS);
-    ALLOC(c->st, sizeof(TfDevState));
+    // the device state, then the per-slot ok / mode rings: one copy back per host sync
+    ALLOC(c->st, TF_ST_BYTES);
+    c->frame_ok = (int*)(c->st + 1);
+    c->frame_mode = c->frame_ok + TF_PROF_RING;
     ALLOC(c->integ_cnt, sizeof(long long) * 2 * TF_INTEG_WG);
     if (pin->use_swapping) {        // the GlobalCache in HBM: 2 KiB per hash entry + flags
         ALLOC(c->swapState, ntot_pad);
@@ -247,7 +249,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     }
 #undef ALLOC
-    e = hipHostMalloc((void**)&c->st_host, sizeof(TfDevState), hipHostMallocDefault);
+    e = hipHostMalloc((void**)&c->st_host, TF_ST_BYTES, hipHostMallocDefault);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     // initial device state
     TfDevState s0;
@@ -282,7 +284,14 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         for (size_t i = 0; i < npx; ++i) tmp[i] = make_float2(pin->viewFrustum_min, pin->viewFrustum_max);
         e = hipMemcpy(c->range, tmp, sizeof(float2) * npx, hipMemcpyHostToDevice);
         free(tmp);
+        if (e == hipSuccess) e = ed_spill_all(c);       // the first CreateExpectedDepths clears the whole buffer
         if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    }
+    {   // k_ed_fill: LDS rows up to ED_LDS_MAX_N visible entries, device-scope atomics past that
+        // (TFUSION_ED_LDS_MAX_N overrides the threshold; the parity tests run both paths)
+        const char* env = getenv("TFUSION_ED_LDS_MAX_N");
+        c->ed_lds_max_n = env ? atoi(env) : ED_LDS_MAX_N;
+        if (c->ed_lds_max_n > ED_LDS_MAX_N) c->ed_lds_max_n = ED_LDS_MAX_N;
     }
     e = tfk_reset_scene(c);                              // topfu.cpp:75
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -441,11 +450,11 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
 // sync, read back slots [first, first+n) and the state; ok_out gets 1/0 per frame
 static tf_status finish_frames(tf_ctx* c, int first, int n, int* ok_out)
 {
-    int okb[TF_PROF_RING], modeb[TF_PROF_RING];
-    TF_CHECK(hipMemcpyAsync(okb, c->frame_ok + first, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
-    TF_CHECK(hipMemcpyAsync(modeb, c->frame_mode + first, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
-    tf_status s = sync_state(c);
-    if (s != TF_OK) return s;
+    // one device-to-host copy into the pinned mirror: the state and the slots' ok / mode
+    TF_CHECK(hipMemcpyAsync(c->st_host, c->st, TF_ST_BYTES, hipMemcpyDeviceToHost, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    const int* okb = (const int*)(c->st_host + 1) + first;
+    const int* modeb = (const int*)(c->st_host + 1) + TF_PROF_RING + first;
     c->frame_counter = c->st_host->frame_counter;
     c->n_resets = c->st_host->n_resets;
     prof_collect(c, first, n, okb, modeb);
@@ -785,11 +794,13 @@ extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
 extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12], int iters, float* ms_per_iter)
 {
     if (!c || !pose_rt || iters <= 0 || !ms_per_iter) return TF_INVALID_ARG;
-    if (stage != TF_STAGE_INTEGRATE && stage != TF_STAGE_RAYCAST_ICP && stage != TF_STAGE_RAYCAST_RENDER)
+    if (stage != TF_STAGE_INTEGRATE && stage != TF_STAGE_RAYCAST_ICP && stage != TF_STAGE_RAYCAST_RENDER &&
+        stage != TF_STAGE_EXPECTED_DEPTHS)
         return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
-    tf_status s = set_pose_in(c, pose_rt, stage == TF_STAGE_INTEGRATE ? TF_POSE_ALLOC_NOINV : 0);
+    tf_status s = set_pose_in(c, pose_rt, stage == TF_STAGE_INTEGRATE || stage == TF_STAGE_EXPECTED_DEPTHS ? TF_POSE_ALLOC_NOINV : 0);
     if (s != TF_OK) return s;
+    if (stage == TF_STAGE_EXPECTED_DEPTHS) TF_CHECK(tfk_expected_depths(c));    // boxes of the current list
     // the pair's renderImage half reads the snapshot of the raycast matrix / range region
     if (stage == TF_STAGE_RAYCAST_RENDER) TF_CHECK(tfk_render_snapshot(c));
     hipEvent_t e0, e1;
@@ -798,6 +809,7 @@ extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12]
     hipError_t e = hipEventRecord(e0, c->stream);
     for (int i = 0; i < iters && e == hipSuccess; ++i)
         e = stage == TF_STAGE_INTEGRATE ? tfk_integrate(c)
+          : stage == TF_STAGE_EXPECTED_DEPTHS ? tfk_expected_depths(c, 1)
           : stage == TF_STAGE_RAYCAST_ICP ? tfk_raycast(c, 1) : tfk_raycast_pair(c);
     if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
     if (e == hipSuccess) e = hipEventSynchronize(e1);
@@ -1109,6 +1121,7 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
     if (!p || n != bytes) return TF_INVALID_ARG;
     TF_CHECK(hipMemcpyAsync(p, host, n, hipMemcpyHostToDevice, c->stream));
     if (which == TF_BUF_HASH) TF_CHECK(tfk_grid_rebuild(c));       // keep the block grid exact
+    if (which == TF_BUF_RANGE) TF_CHECK(ed_spill_all(c));          // next CreateExpectedDepths: whole buffer
     static const int one = 1;
     if (which == TF_BUF_HASH || which == TF_BUF_VBA || which == TF_BUF_VBA_RGB)   // next reset (in-frame ones too): full clear
         TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, scene_external), &one, sizeof(int), hipMemcpyHostToDevice, c->stream));

@@ -8,8 +8,14 @@ struct EdArgs {
     const TfHashEntry* hash;
     const int* visibleIds;
     float2* range;
-    int4* box; float2* z; int* tiles; int* off; int* chunk;
+    uint4* rec;          // per visible entry: ulx | uly << 16, lrx | lry << 16, zmin, zmax bits (x ~0u: none)
+    int* tiles; int* off; int* chunk;
+    int2* spill;         // per fill row: extent of the pixels the last fill wrote outside the /8 region
     int W, H;
+    int rc, rr;          // the /8 region: (W-1)/8+1 columns, (H-1)/8+1 rows
+    int nrows;           // k_ed_fill's LDS rows (ed_nrows: rr + ED_XROWS, at most H)
+    int lds_max_n;       // k_ed_fill's LDS-row path up to this many visible entries
+    int vcap, nchunk_max;   // box / chunk-total buffer lengths (k_ed_fill's early loads)
     float fx, fy, cx, cy, voxelSize;
     unsigned cap;
 };
@@ -28,17 +34,44 @@ __device__ __forceinline__ void ed_project_block(const EdArgs& a, const TfDevSta
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int tid = bid * 256 + threadIdx.x, stride = nblk * 256;
     // memsetKernel(FAR_AWAY, VERY_CLOSE) over the whole buffer (VisualisationEngine_CUDA.cu:133),
-    // two pixels per 16-byte store.  The fill writes outside the /8 region castRay reads too
-    // (boxes are clamped to the full-resolution W-1 / H-1, VisualisationEngine_Shared.hpp:67-70),
-    // so anything less than the whole buffer leaves stale min/max values there.
+    // restated by what differs from it.  k_ed_fill writes every pixel of the /8 region castRay
+    // reads (rc x rr, its LDS rows) with plain stores, so only two parts are written here:
+    //  - the pixels the previous fill wrote outside that region (boxes are clamped to the
+    //    full-resolution W-1 / H-1, VisualisationEngine_Shared.hpp:67-70): the extents its rows
+    //    recorded in a.spill, or the whole buffer after creation / a host upload;
+    //  - the /8 region itself when the fill will take its atomic path (n > a.lds_max_n).
+    const int n = st->noVisibleEntries;
     {
-        const int npx = a.W * a.H;
-        float4* r4 = (float4*)a.range;
-        for (int i = tid; i < (npx >> 1); i += stride) r4[i] = make_float4(TF_FAR_AWAY, TF_VERY_CLOSE, TF_FAR_AWAY, TF_VERY_CLOSE);
-        if ((npx & 1) && tid == 0) a.range[npx - 1] = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
+        __shared__ int sxy[2];
+        if (threadIdx.x < 2) sxy[threadIdx.x] = 0;
+        __syncthreads();
+        int sx = 0, sy = 0;
+        for (int r = threadIdx.x; r < a.nrows; r += 256) { const int2 e = a.spill[r]; sx = max(sx, e.x); sy = max(sy, e.y); }
+        if (sx) atomicMax(&sxy[0], sx);
+        if (sy) atomicMax(&sxy[1], sy);
+        __syncthreads();
+        const int SX = sxy[0], SY = sxy[1];
+        const float2 init = make_float2(TF_FAR_AWAY, TF_VERY_CLOSE);
+        if (n > a.lds_max_n)
+            for (int i = tid; i < a.rc * a.rr; i += stride) {
+                const int y = i / a.rc, x = i - y * a.rc;
+                a.range[x + y * a.W] = init;
+            }
+        if (SX > 0 && SY > 0) {
+            if (SX >= a.W && SY >= a.H) {                  // whole buffer, two pixels per 16-byte store
+                const int npx = a.W * a.H;
+                float4* r4 = (float4*)a.range;
+                for (int i = tid; i < (npx >> 1); i += stride) r4[i] = make_float4(init.x, init.y, init.x, init.y);
+                if ((npx & 1) && tid == 0) a.range[npx - 1] = init;
+            } else {
+                for (int i = tid; i < SX * SY; i += stride) {
+                    const int y = i / SX, x = i - y * SX;
+                    if (x >= a.rc || y >= a.rr) a.range[x + y * a.W] = init;
+                }
+            }
+        }
     }
     __shared__ int wsum[4];
-    const int n = st->noVisibleEntries;
     const int nchunks = (n + ED_CHUNK - 1) / ED_CHUNK;
     const float* M = st->M_alloc;          // pose.inv() (topfu.cpp:306)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -47,8 +80,7 @@ __device__ __forceinline__ void ed_project_block(const EdArgs& a, const TfDevSta
         int ntiles = 0;
         if (i < n) {
             TfHashEntry e = a.hash[a.visibleIds[i]];
-            int4 box = make_int4(-1, -1, -1, -1);
-            float2 zr = make_float2(0.f, 0.f);
+            uint4 rec = make_uint4(0xffffffffu, 0xffffffffu, 0u, 0u);
             if (e.ptr >= 0) {
                 int ulx = a.W / TF_SUBSAMPLE, uly = a.H / TF_SUBSAMPLE, lrx = -1, lry = -1;
                 float zmin = TF_FAR_AWAY, zmax = TF_VERY_CLOSE;
@@ -80,11 +112,11 @@ __device__ __forceinline__ void ed_project_block(const EdArgs& a, const TfDevSta
                     int nbx = (int)ceilf((float)(lrx - ulx + 1) / TF_RB_SIZE);
                     int nby = (int)ceilf((float)(lry - uly + 1) / TF_RB_SIZE);
                     ntiles = nbx * nby;
-                    box = make_int4(ulx, uly, lrx, lry);
-                    zr = make_float2(zmin, zmax);
+                    rec = make_uint4((unsigned)ulx | (unsigned)uly << 16, (unsigned)lrx | (unsigned)lry << 16,
+                                     __float_as_uint(zmin), __float_as_uint(zmax));
                 }
             }
-            a.box[i] = box; a.z[i] = zr; a.tiles[i] = ntiles;
+            a.rec[i] = rec; a.tiles[i] = ntiles;
         }
         // exclusive prefix of the tile counts inside the chunk (wave scan + 4 wave totals)
         int incl = ntiles;

@@ -20,6 +20,7 @@
 #define TF_LEVELS 3
 #define TF_NUM_STAGES 9     // tf_stage_id in include/tfusion_hip.h
 #define TF_PROF_RING 32     // frames enqueued between host syncs (and timing-event ring slots)
+#define TF_ST_BYTES (sizeof(TfDevState) + 2 * sizeof(int) * TF_PROF_RING)   // c->st + frame_ok / frame_mode rings
 #define TF_ICP_TAG_WORDS (2 * 256 * 28 + 16 + 2 * 8 * 28)   // persistent ICP tagged granules (tf_icp.hip)
 
 // HashEntry, VoxelBlockHash.hpp:32-44 (16 B; one dwordx4 probe)
@@ -290,11 +291,13 @@ struct tf_ctx {
     float* raycast;          // float4
     uchar4* grey;
     // expected-depths scratch
-    int4* blockBox;          // per visible entry: ulx, uly, lrx, lry (ulx < 0 -> invalid)
-    float2* blockZ;
+    uint4* blockRec;         // per visible entry: box (4 x u16: ulx, uly, lrx, lry) + z range (invalid: x = ~0u)
     int* blockTiles;
     int* blockOff;           // exclusive tile offset inside the entry's 256-entry chunk
     int* edChunk;            // tile total per chunk
+    int2* edSpill;           // per k_ed_fill row (ed_nrows): extent [0,x) x [0,y) of the pixels k_ed_fill wrote outside
+                             // the /8 region (cleared by the next projection pass)
+    int ed_lds_max_n;        // k_ed_fill reduces in LDS per /8 row up to this many visible entries
     // frame buffers
     uint16_t* depth_in;      // staging for host uploads / pitched input
     float* dists;
@@ -320,6 +323,7 @@ struct tf_ctx {
     int n_resets;            // host mirror of st->n_resets
     int* frame_ok;           // per enqueued frame of a batch: 1 ok, 0 ICP failure (reset), -1 error
     int* frame_mode;         // per enqueued frame of a batch: st->mode it ran with
+                             // (both rings follow TfDevState in c->st's allocation, TF_ST_BYTES)
     int alloc_chunks;        // N_tot / 4096
     int vis_chunks;
     // per-stage HIP-event timing on the context stream (tf_profile_*)
@@ -370,6 +374,11 @@ hipError_t tfk_icp_maps_end(tf_ctx* c, int slot);
 #define TF_END_BLOCKS 256        // workgroups of the frame-end / in-frame reset pass
 hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0);
 #define TF_ED_BLOCKS 256         // workgroups of the expected-depth projection pass
+#define ED_MAX_W 4096            // k_ed_fill: columns of a row held in LDS (wider images: atomics past it)
+#define ED_XROWS 8               // k_ed_fill: LDS rows below the /8 region (where boxes spill)
+static inline int ed_nrows(int H) { const int n = (H - 1) / TF_SUBSAMPLE + 1 + ED_XROWS; return n < H ? n : H; }
+#define ED_LDS_MAX_N 16384       // k_ed_fill: per-/8-row LDS reduction up to this many visible entries
+hipError_t ed_spill_all(tf_ctx* c);   // mark the whole range buffer for clearing by the next projection pass
 #define TF_INTEG_WG 2048         // workgroups of the integration pass (grid-stride)
 hipError_t tfk_frame0_matrices(tf_ctx* c);
 // swapping (tf_swap.hip): reallocation of listed swapped-out entries (after the visible list),
