@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=None, help="untimed warm-up steps (default 5)")
     ap.add_argument("--frames-per-step", type=int, default=32,
                     help="frames per step: one tf_process_frames batch (32 = one enqueue group)")
-    ap.add_argument("--per-call-frames", type=int, default=64,
+    ap.add_argument("--per-call-frames", type=int, default=256,
                     help="frames of the per-call (one tf_process_frame per frame) rate beside the batched one; 0 = skip")
     ap.add_argument("--config", choices=["C2", "C3", "C3I", "C3R", "C5"], default="C2",
                     help="C2: 640x480 orbit, 5 mm (BASELINE configs[1], the headline); "
@@ -376,6 +376,17 @@ def per_call_rate(tf, base, frame_bytes, n):
     return n / (time.perf_counter() - t0)
 
 
+def batched_rate(tf, base, n, F):
+    """The same frames through tf_process_frames in F-frame batches (wall clock)."""
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k0 in range(0, n, F):
+        tf.process_frames(base + k0 * tf.W * tf.H * 2, min(F, n - k0))
+    torch.cuda.synchronize()
+    return n / (time.perf_counter() - t0)
+
+
 def icp_occupancy():
     """The ICP kernel's occupancy / wait / LDS figures from the committed rocprofv3 PMC pass
     (profiles/icp_occupancy.json, tools/icp_occupancy.py), if present."""
@@ -484,13 +495,18 @@ def main():
         nvis_bd = tbt["visible_sum"] / n_int
         tb.close()
         torch.cuda.synchronize()
-    # TopFu::operator() per call (one host round trip per frame, no lookahead), beside the
-    # batched rate; a fresh context on the same frames, outside the timed region
-    per_call = None
-    if args.per_call_frames > 0:
+    # TopFu::operator() per call (one host round trip per frame, no lookahead) over the first
+    # frames of the timed region, from a fresh context, and the batched rate of a fresh context on
+    # the same frames beside it (the orbit's cost per frame varies along it: compare like with like)
+    per_call = per_call_batched = None
+    nc = min(args.per_call_frames, args.steps * F)
+    if nc > 0:
+        pc_base = base + args.warmup * F * frame_bytes
         tc = TopFu(default_params(**pkw), device=local_rank)
-        nc = min(args.per_call_frames, n_frames)
-        per_call = per_call_rate(tc, base, frame_bytes, nc)
+        per_call = per_call_rate(tc, pc_base, frame_bytes, nc)
+        tc.close()
+        tc = TopFu(default_params(**pkw), device=local_rank)
+        per_call_batched = batched_rate(tc, pc_base, nc, F)
         tc.close()
 
     total_steps_frames = args.steps * F
@@ -578,8 +594,10 @@ def main():
                                     "per frame") if args.swapping else "off (topfu.cpp:67)"},
             "ms_per_frame": round(elapsed_max / total_steps_frames * 1000.0, 5),
             "per_call_frames_per_sec": None if per_call is None else round(per_call, 2),
-            "per_call": (f"TopFu::operator() per call: tf_process_frame on {min(args.per_call_frames, n_frames)} frames, "
-                         "one host round trip per frame, no lookahead (demo.cpp:102-105 semantics), rank 0 only")
+            "per_call_batched_same_frames": None if per_call_batched is None else round(per_call_batched, 2),
+            "per_call": (f"TopFu::operator() per call: tf_process_frame on the timed region's first {nc} frames from a "
+                         "fresh context, one host round trip per frame, no lookahead (demo.cpp:102-105 semantics); "
+                         "per_call_batched_same_frames: tf_process_frames on the same frames from a fresh context")
                         if per_call is not None else None,
             "icp_integrate_ms_per_frame": None if icp_integ is None else round(icp_integ, 4),
             "stage_ms_per_frame": {k: (None if v is None else round(v, 4)) for k, v in per_stage.items()},

@@ -1,0 +1,77 @@
+// Latency of the persistent ICP kernel's serial tail on one wave (gfx950): the LDL^T solve,
+// Rodrigues and compose of tf_icp.hip, and the f64 primitives they chain, each repeated N times
+// with every repetition depending on the last.  hipcc --offload-arch=gfx950 -O3 -ffp-contract=off
+//   -fhip-fp32-correctly-rounded-divide-sqrt icp_tail.hip -o icp_tail  (tools/micro/Makefile)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include "../../topfusion_amd/csrc/tf_icp_tail.h"
+#include "../../topfusion_amd/csrc/tf_pose.h"
+
+__global__ void k_tail(const float* in, float* out, long long* cyc, int n, int which)
+{
+    float Am[6][6], bv[6], aff[12];
+    for (int i = 0; i < 6; ++i) { bv[i] = in[36 + i]; for (int j = 0; j < 6; ++j) Am[i][j] = in[i * 6 + j]; }
+    for (int i = 0; i < 12; ++i) aff[i] = (i % 5 == 0) ? 1.f : 0.f;
+    double dx = in[0], dacc = 0;
+    const long long t0 = clock64();
+    for (int it = 0; it < n; ++it) {
+        if (which == 0) {                       // solve + Rodrigues + compose (the tail)
+            float rv[6], R[9], tinc[12];
+            icp_solve6_ldl(Am, bv, rv);
+            icp_rodrigues(rv, R);
+            for (int j = 0; j < 3; ++j) {
+                tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1];
+                tinc[j * 4 + 2] = R[j * 3 + 2]; tinc[j * 4 + 3] = rv[3 + j];
+            }
+            tf_rigid_mul(tinc, aff, aff);
+            bv[0] += aff[3] * 1e-30f;           // next repetition depends on this one
+        } else if (which == 1) {                // solve only
+            float rv[6];
+            icp_solve6_ldl(Am, bv, rv);
+            bv[0] += rv[0] * 1e-30f;
+        } else if (which == 2) {                // Rodrigues only
+            float rv[6] = { bv[0] * 1e-3f, bv[1] * 1e-3f, bv[2] * 1e-3f, 0, 0, 0 }, R[9];
+            icp_rodrigues(rv, R);
+            bv[0] += R[1] * 1e-30f;
+        } else if (which == 3) {                // 10 dependent f64 divides
+            for (int k = 0; k < 10; ++k) dx = 1.0 / (dx + 1.0);
+        } else if (which == 4) {                // 10 dependent f64 sqrt
+            for (int k = 0; k < 10; ++k) dx = sqrt(dx + 1.0);
+        } else if (which == 5) {                // 10 dependent f64 fma
+            for (int k = 0; k < 10; ++k) dx = fma(dx, 0.999, 1e-3);
+        } else if (which == 6) {                // 10 dependent f32 fma
+            float f = (float)dx;
+            for (int k = 0; k < 10; ++k) f = fmaf(f, 0.999f, 1e-3f);
+            dx = f;
+        } else if (which == 7) {                // 10 dependent f32 IEEE divides
+            float f = (float)dx;
+            for (int k = 0; k < 10; ++k) f = 1.0f / (f + 1.0f);
+            dx = f;
+        }
+    }
+    const long long t1 = clock64();
+    dacc += dx;
+    if (threadIdx.x == 0) { cyc[which] = t1 - t0; out[which] = aff[3] + bv[0] + (float)dacc; }
+}
+
+int main()
+{
+    float hA[42];
+    // a symmetric positive-definite normal matrix and a right-hand side of ICP's scale
+    for (int i = 0; i < 6; ++i) for (int j = 0; j < 6; ++j) hA[i * 6 + j] = (i == j) ? 1000.f + 10 * i : 3.f / (1 + i + j);
+    for (int i = 0; i < 6; ++i) hA[36 + i] = 0.01f * (i + 1);
+    float *dA, *dO; long long* dC;
+    hipMalloc(&dA, sizeof(hA)); hipMalloc(&dO, 64); hipMalloc(&dC, 8 * sizeof(long long));
+    hipMemcpy(dA, hA, sizeof(hA), hipMemcpyHostToDevice);
+    const int N = 1000;
+    const char* names[] = { "solve+rodrigues+compose", "solve (LDL^T)", "rodrigues", "10x f64 div", "10x f64 sqrt",
+                            "10x f64 fma", "10x f32 fma", "10x f32 div" };
+    for (int w = 0; w < 8; ++w) {
+        hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, 0, dA, dO, dC, 10, w);   // warm
+        hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, 0, dA, dO, dC, N, w);
+        long long c = 0;
+        hipMemcpy(&c, dC + w, sizeof(c), hipMemcpyDeviceToHost);
+        printf("%-26s %8.1f cycles per repetition (s_memtime)\n", names[w], (double)c / N);
+    }
+    return 0;
+}
