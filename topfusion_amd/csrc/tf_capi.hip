@@ -343,14 +343,26 @@ static void swap_pyramids(tf_ctx* c)
 // ---- per-stage event timing -----------------------------------------------------------
 // Events ring: TF_PROF_RING frames x (start, end) per stage.  Frames are attributed after a
 // sync, once their mode / ok flags are known, and only for the stages that did work.
+// A single-kernel stage (stage_single) is timed by its dispatch's own timestamps (tf_launch,
+// hipExtLaunchKernelGGL); the others by event records around their launches.
 #define STAGE_ON(strm, id, expr)                                                              \
     do {                                                                                      \
         const bool timed_ = c->prof_slot_on[slot] && ((c->prof_mask >> (id)) & 1u);          \
-        if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id)), (strm)));          \
+        const bool ext_ = timed_ && stage_single(c, id);                                      \
+        if (ext_) { c->ev_start = prof_event(c, slot, 2 * (id)); c->ev_stop = prof_event(c, slot, 2 * (id) + 1); } \
+        else if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id)), (strm)));     \
         TF_CHECK(expr);                                                                       \
-        if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id) + 1), (strm)));      \
+        if (ext_ && c->ev_start) { c->ev_start = c->ev_stop = nullptr; return TF_HIP_ERROR; } \
+        if (timed_ && !ext_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id) + 1), (strm))); \
     } while (0)
 #define STAGE(id, expr) STAGE_ON(c->stream, id, expr)
+
+// stages whose frame-path launcher issues exactly one kernel (through tf_launch)
+static bool stage_single(const tf_ctx* c, int id)
+{
+    return (id == TF_STAGE_ICP && c->icp_persistent) || id == TF_STAGE_INTEGRATE || id == TF_STAGE_EXPECTED_DEPTHS ||
+           id == TF_STAGE_RAYCAST_ICP || id == TF_STAGE_ICP_MAPS;
+}
 
 static hipEvent_t prof_event(tf_ctx* c, int slot, int k)
 {

@@ -293,6 +293,9 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 #define IP_WAVES 8
 #define IP_SREG 1                       // CTA slots kept in registers per wave (8 per WG; larger images use k_icp_iter)
 #define IP_SPIN_LIMIT (1u << 21)
+#ifndef IP_SLEEP
+#define IP_SLEEP 1                      // s_sleep between hand-off polls (x 64 cycles)
+#endif
 #define IP_PART (2 * ICP_NWG * ICP_T_STRIDE + 16)   // column slots (double-buffered by generation parity), then
                                                  // the 8 residue-class partials, double-buffered
 #define IP_NPART 8                               // residue classes of the final tree's first five steps
@@ -663,7 +666,7 @@ k_icp_frame(IcpFrameArgs a)
                     }
                     if (ready) break;
                     if (spins > IP_SPIN_LIMIT) { timeout = true; break; }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(IP_SLEEP);
                 }
 #pragma unroll
                 for (int k = 0; k < PER; ++k) {
@@ -683,11 +686,12 @@ k_icp_frame(IcpFrameArgs a)
                 bool timeout = false;
                 if (tid < IP_NPART * 27) {
                     const int x = tid / 27, q = tid - x * 27;
-                    unsigned long long v = ip_load(&parts[x * ICP_T_STRIDE + q]);
+                    const unsigned long long* pp = &parts[x * ICP_T_STRIDE + q];
+                    unsigned long long v = ip_load(pp);
                     for (unsigned spins = 0; (unsigned)(v >> 32) != gen; ++spins) {
                         if (spins > IP_SPIN_LIMIT) { timeout = true; break; }
-                        __builtin_amdgcn_s_sleep(1);
-                        v = ip_load(&parts[x * ICP_T_STRIDE + q]);
+                        __builtin_amdgcn_s_sleep(IP_SLEEP);
+                        v = ip_load(pp);
                     }
                     tv[q][x] = __uint_as_float((unsigned)v);
                 }
@@ -891,7 +895,7 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
         }
         // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
         // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up
-        hipLaunchKernelGGL(k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, c->stream, a);
+        tf_launch(c, k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, c->stream, c->st, frame_begin);

@@ -7,6 +7,7 @@
 // against the CPU oracle (oracle/tf_oracle.c, test infrastructure only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
 #include "../../include/tfusion_hip.h"
@@ -334,9 +335,26 @@ struct tf_ctx {
     unsigned char prof_slot_on[TF_PROF_RING];   // batch slot carries stage events
     unsigned char prof_slot_pre[TF_PROF_RING];  // batch slot ran its own preprocessing (no lookahead)
     hipEvent_t prof_ev[2 * TF_NUM_STAGES * TF_PROF_RING];
+    // a single-kernel stage being timed: its launch (tf_launch) carries these events, which
+    // hipExtLaunchKernelGGL ties to the dispatch's own begin / end (what rocprofv3 reports);
+    // event records around a launch were measured to include earlier work (ICP: 148 vs 85 us)
+    hipEvent_t ev_start, ev_stop;
     double prof_ms[TF_NUM_STAGES];
     long long prof_count[TF_NUM_STAGES];
 };
+
+// the launch of a stage's single kernel: timed by the dispatch's own timestamps when the
+// stage is being timed (c->ev_start set by STAGE_ON, consumed here), plain otherwise
+template <typename... KArgs, typename... Args>
+inline void tf_launch(tf_ctx* c, void (*kern)(KArgs...), dim3 grid, dim3 block, unsigned shm, Args... args)
+{
+    if (c->ev_start) {
+        hipExtLaunchKernelGGL(kern, grid, block, shm, c->stream, c->ev_start, c->ev_stop, 0, args...);
+        c->ev_start = c->ev_stop = nullptr;
+    } else {
+        hipLaunchKernelGGL(kern, grid, block, shm, c->stream, args...);
+    }
+}
 
 // ---------------------------------------------------------------------------------------
 // launchers (one per kernel family); all enqueue on ctx->stream

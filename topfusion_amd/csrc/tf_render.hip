@@ -599,7 +599,7 @@ hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch)
         bil_gx = tf_div_up(c->W, PRE_TX);
         n_bil = bil_gx * tf_div_up(c->H, PRE_TY);
     }
-    hipLaunchKernelGGL(k_raycast_pair, dim3(2 * nb + n_pyr + n_bil), dim3(256), 0, c->stream, ai, ar, c->st, tx, n, nb,
+    tf_launch(c, k_raycast_pair, dim3(2 * nb + n_pyr + n_bil), dim3(256), 0, ai, ar, c->st, tx, n, nb,
                        pp, n_pyr, pyr_gx, bb, bil_gx);
     return hipGetLastError();
 }
@@ -933,7 +933,7 @@ hipError_t tfk_icp_maps_end(tf_ctx* c, int slot)
     ResetArgs r;
     tf_reset_args(c, &r, 1, slot);
     const int gx = (c->W + 31) / 32, nmaps = gx * ((c->H + 31) / 32);
-    hipLaunchKernelGGL(k_icp_maps_end, dim3(nmaps + TF_END_BLOCKS), dim3(256), 0, c->stream, a, r, gx, nmaps);
+    tf_launch(c, k_icp_maps_end, dim3(nmaps + TF_END_BLOCKS), dim3(256), 0, a, r, gx, nmaps);
     return hipGetLastError();
 }
 
@@ -1155,6 +1155,6 @@ hipError_t tfk_expected_depths(tf_ctx* c, int project_done)
     tf_ed_args(c, &a);
     if (!project_done) hipLaunchKernelGGL(k_ed_project, dim3(TF_ED_BLOCKS), dim3(256), 0, c->stream, a, c->st);
     // one workgroup per LDS row (the atomic path grid-strides the same grid)
-    hipLaunchKernelGGL(k_ed_fill, dim3(a.nrows), dim3(ED_THREADS), 0, c->stream, a, c->st);
+    tf_launch(c, k_ed_fill, dim3(a.nrows), dim3(ED_THREADS), 0, a, c->st);
     return hipGetLastError();
 }

@@ -1010,12 +1010,12 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
     if (with_ed) {
         tf_ed_args(c, &ed);
         const dim3 ge(nwg + TF_ED_BLOCKS);
-        if (rgb) hipLaunchKernelGGL((k_integrate<true, true>), ge, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
-        else hipLaunchKernelGGL((k_integrate<true, false>), ge, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
+        if (rgb) tf_launch(c, k_integrate<true, true>, ge, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
+        else tf_launch(c, k_integrate<true, false>, ge, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
     } else {
         const dim3 g(nwg);
-        if (rgb) hipLaunchKernelGGL((k_integrate<false, true>), g, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
-        else hipLaunchKernelGGL((k_integrate<false, false>), g, b, 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
+        if (rgb) tf_launch(c, k_integrate<false, true>, g, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
+        else tf_launch(c, k_integrate<false, false>, g, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
     }
     return hipGetLastError();
 }
