@@ -550,14 +550,19 @@ def main():
                                "traffic": (pmc.get(k) or {}).get("bytes_per_launch"),
                                "kernel": KERNEL_OF_STAGE[k], "algorithmic_bytes_per_launch": int(b),
                                "avg_launch_ms": round(ms, 5),
-                               "timing": (f"HIP events around every {args.profile_every}-th launch of the timed region "
-                                          f"({prof_timed[k][1]} launches)") if (k == dominant and timed_ms)
-                                         else "HIP events in the breakdown pass"}
+                               "timing": (f"HIP events tied to the dispatch of every {args.profile_every}-th launch of the "
+                                          f"timed region (hipExtLaunchKernelGGL; {prof_timed[k][1]} launches that ran the "
+                                          "whole stage)") if (k == dominant and timed_ms)
+                                         else "HIP events tied to each launch's dispatch in the breakdown pass"}
             if dominant in roof_all:
                 roof = roof_all[dominant]
             occ = icp_occupancy()
             if occ and "icp" in roof_all:
                 roof_all["icp"]["occupancy"] = (occ.get(args.config) or occ.get("C2"))
+            if "icp" in roof_all:
+                roof_all["icp"]["limit"] = ("latency, not HBM: 19 dependent iterations, each rows -> two cross-CU "
+                                            "hand-offs -> the serial 6x6 solve (DESIGN.md 5); the previous-frame "
+                                            "gathers hit L2, so PMC traffic is a fraction of the algorithmic bytes")
         stream_gbs = round(hbm_stream_copy(device), 1)
         cpu = None
         if not args.no_cpu_baseline:

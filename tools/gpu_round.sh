@@ -18,3 +18,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 tail -1 $O/prof.log
 cd $R
 bash tools/gpu_pmc.sh $TAG
+for cfg in C3 C3I C3R; do
+  timeout -k 10 400 python bench.py --config $cfg --no-cpu-baseline > $O/bench_$cfg.log 2>&1 || { tail -30 $O/bench_$cfg.log; exit 1; }
+  tail -1 $O/bench_$cfg.log | cut -c1-160
+done

@@ -1,11 +1,14 @@
 """Occupancy, wait and LDS figures of the ICP kernel (k_icp_frame) from a rocprofv3 PMC pass
 (tools/gpu_pmc.sh pass "occ": SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT
 SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE), derived with rocprofiler-sdk's
-gfx950 definitions (counter_defs.yaml): SQ_WAVE_CYCLES counts in units of 4 cycles, so
-mean resident waves per CU = 4 * SQ_WAVE_CYCLES / GRBM_GUI_ACTIVE / CU_NUM (OccupancyPercent =
-that / 32 waves per CU); wait fraction = SQ_WAIT_ANY / SQ_WAVE_CYCLES; LDS bank-conflict
-cycles per conflict-free cycle = SQ_LDS_BANK_CONFLICT / (SQ_LDS_IDX_ACTIVE - SQ_LDS_BANK_CONFLICT);
-LDS utilisation = SQ_LDS_IDX_ACTIVE / (GRBM_GUI_ACTIVE * CU_NUM).  Writes
+gfx950 definitions (counter_defs.yaml): SQ_WAVE_CYCLES counts in units of 4 cycles and rocprofv3
+reports GRBM_GUI_ACTIVE summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back), so with
+T = GRBM_GUI_ACTIVE / 8 the dispatch's active cycles: mean resident waves per CU =
+4 * SQ_WAVE_CYCLES / T / CU_NUM (OccupancyPercent = that / 32 waves per CU); wait fraction =
+SQ_WAIT_ANY / SQ_WAVE_CYCLES; LDS bank-conflict cycles per conflict-free cycle =
+SQ_LDS_BANK_CONFLICT / (SQ_LDS_IDX_ACTIVE - SQ_LDS_BANK_CONFLICT); LDS utilisation =
+SQ_LDS_IDX_ACTIVE / (T * CU_NUM).  Only full launches count (GRBM_GUI_ACTIVE at least half its
+90th percentile: the frames whose ICP ran every iteration, as bench.py times).  Writes
 profiles/icp_occupancy.json, which bench.py attaches to the ICP roofline entry.
 
     python tools/icp_occupancy.py gpurun_out/pmc_TAG/occ [CONFIG=C2] [profiles/icp_occupancy.json]
@@ -14,6 +17,7 @@ import csv, glob, json, os, sys
 from collections import defaultdict
 
 CU_NUM = 256
+XCD_NUM = 8
 KERNEL = "k_icp_frame"
 
 
@@ -31,12 +35,14 @@ def main():
     # dispatches that ran the tracking path (frame-0 / post-reset launches exit at once)
     ds = [d for d in per.values() if d.get("SQ_WAVE_CYCLES", 0) > 0 and d.get("GRBM_GUI_ACTIVE", 0) > 0]
     ds.sort(key=lambda d: d["GRBM_GUI_ACTIVE"])
-    ds = ds[len(ds) // 4:]                              # drop the short (no-op) dispatches
+    p90 = ds[int(0.9 * (len(ds) - 1))]["GRBM_GUI_ACTIVE"] if ds else 0
+    ds = [d for d in ds if d["GRBM_GUI_ACTIVE"] >= 0.5 * p90]   # full launches only
     if not ds:
         print("no k_icp_frame dispatches found")
         return 1
     avg = {k: sum(d.get(k, 0.0) for d in ds) / len(ds) for k in ds[0]}
-    waves_cu = 4.0 * avg["SQ_WAVE_CYCLES"] / avg["GRBM_GUI_ACTIVE"] / CU_NUM
+    T = avg["GRBM_GUI_ACTIVE"] / XCD_NUM
+    waves_cu = 4.0 * avg["SQ_WAVE_CYCLES"] / T / CU_NUM
     res = {
         "kernel": KERNEL, "dispatches": len(ds),
         "designed": "256 workgroups x 8 waves, one workgroup per CU (56 KiB LDS pad): 8 waves/CU = 2 per SIMD",
@@ -45,7 +51,8 @@ def main():
         "occupancy_pct_of_32_waves_per_cu": round(100 * waves_cu / 32, 2),
         "wait_any_frac_of_wave_cycles": round(avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"], 4),
         "lds_bank_conflict_ratio": round(avg["SQ_LDS_BANK_CONFLICT"] / max(1.0, avg["SQ_LDS_IDX_ACTIVE"] - avg["SQ_LDS_BANK_CONFLICT"]), 5),
-        "lds_util_frac": round(avg["SQ_LDS_IDX_ACTIVE"] / (avg["GRBM_GUI_ACTIVE"] * CU_NUM), 5),
+        "lds_util_frac": round(avg["SQ_LDS_IDX_ACTIVE"] / (T * CU_NUM), 5),
+        "active_cycles_per_launch": round(T, 1),
         "lds_insts_per_wave": round(avg.get("SQ_INSTS_LDS", 0.0) / max(1.0, avg["SQ_WAVES"]), 1),
         "raw_avg": {k: round(v, 1) for k, v in avg.items()},
         "source": os.path.relpath(root),

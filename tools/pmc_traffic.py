@@ -1,7 +1,9 @@
 """HBM-side traffic per launch of the bench's single-kernel stages, from the rocprofv3 PMC
 passes of tools/gpu_pmc.sh, corrected as MI355X_MICROARCH.md §HBM prescribes (gfx950
 FETCH_SIZE reports half the bytes of wide reads: x2; WRITE_SIZE as is; both in KiB).
-Writes profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
+Only full launches count (per counter: at least half its 90th percentile), as bench.py times
+only frames whose stage ran.  Writes profiles/pmc_traffic.json, which bench.py reads for
+roofline.traffic.
 
     python tools/pmc_traffic.py gpurun_out/pmc_TAG [CONFIG=C2] [profiles/pmc_traffic.json]
 
@@ -22,6 +24,15 @@ def per_kernel(root, counter):
     return vals
 
 
+def full(vals):
+    """The launches that did the stage's whole work: at least half the 90th percentile (frame-0
+    and failed-ICP frames launch the kernels too, and they exit early)."""
+    if not vals:
+        return vals
+    p90 = sorted(vals)[int(0.9 * (len(vals) - 1))]
+    return [v for v in vals if v >= 0.5 * p90]
+
+
 def main():
     root = sys.argv[1]
     config = sys.argv[2] if len(sys.argv) > 2 else "C2"
@@ -30,8 +41,8 @@ def main():
     fetch, write = per_kernel(root, "FETCH_SIZE"), per_kernel(root, "WRITE_SIZE")
     res = {}
     for key, stage in STAGE_OF:
-        f = [v for k, vs in fetch.items() if key in k for v in vs]
-        w = [v for k, vs in write.items() if key in k for v in vs]
+        f = full([v for k, vs in fetch.items() if key in k for v in vs])
+        w = full([v for k, vs in write.items() if key in k for v in vs])
         if not f or not w:
             continue
         fb = sum(f) / len(f) * 1024 * 2

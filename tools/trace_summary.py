@@ -3,7 +3,10 @@
 The device-driven frame loop enqueues every stage of every frame; on frames where the device
 decided a stage does not run (frame-0 path after a reset, ICP failure) the launch exits at
 once (~1.5 us).  `avg_exec` averages only the launches that did work (> EARLY_US), which is
-what bench.py's HIP events report ("averages per executed launch")."""
+what bench.py's HIP events report ("averages per executed launch").  `avg_full` averages the
+launches of at least half the 90th-percentile duration: for k_icp_frame these are the frames whose
+ICP ran all its iterations (bench.py times only those: stage_ran), the others ending early at a
+failed det check."""
 import csv, sys
 from collections import defaultdict
 EARLY_US = 3.0
@@ -18,8 +21,11 @@ tot = sum(sum(v) for v in by.values())
 for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
     ex = [x for x in v if x > EARLY_US]
     avg_ex = sum(ex) / len(ex) if ex else 0.0
+    p90 = sorted(v)[int(0.9 * (len(v) - 1))]
+    full = [x for x in v if x >= 0.5 * p90]
     print(f"{k[0]:24s} grid={k[1]:>8} n={len(v):5d} avg={sum(v)/len(v):8.2f}us n_exec={len(ex):5d} "
-          f"avg_exec={avg_ex:8.2f}us min={min(v):8.2f} tot%={100*sum(v)/tot:5.1f}")
+          f"avg_exec={avg_ex:8.2f}us n_full={len(full):5d} avg_full={sum(full)/len(full):8.2f}us "
+          f"min={min(v):8.2f} tot%={100*sum(v)/tot:5.1f}")
 gaps = defaultdict(list)
 for a, b in zip(rows, rows[1:]):
     gaps[a["Kernel_Name"].split("(")[0] + "->" + b["Kernel_Name"].split("(")[0]].append((int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1000)
