@@ -60,6 +60,8 @@ def lib(omp=False):
         P = ctypes.c_void_p
         L.tfo_default_params.argtypes = [ctypes.POINTER(Params)]
         L.tfo_exp.argtypes = [ctypes.c_float]; L.tfo_exp.restype = ctypes.c_float
+        L.tfo_interp_bilinear_u8x4.argtypes = [P, ctypes.c_size_t, ctypes.c_float, ctypes.c_float, P]
+        L.tfo_colour_average.argtypes = [ctypes.c_uint32, P, ctypes.c_int]; L.tfo_colour_average.restype = ctypes.c_uint32
         L.tfo_compute_dists.argtypes = [P, ctypes.c_int, ctypes.c_int, P]
         L.tfo_bilateral.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float]
         L.tfo_truncate.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_float]
@@ -213,6 +215,24 @@ def tsdf_update(sdf, w, eta, mu=0.02, maxW=100):
     ww = np.array([w], np.uint8)
     lib().tfo_tsdf_update(ptr(s), ptr(ww), eta, mu, maxW)
     return int(s[0]), int(ww[0])
+
+
+def interp_bilinear_u8x4(rgba, x, y):
+    """interpolateBilinear<uchar> (PixelUtils.hpp:8-32) of an HxWx4 uint8 image at (x, y)."""
+    img = np.ascontiguousarray(rgba, np.uint8)
+    out = np.zeros(4, np.float32)
+    lib().tfo_interp_bilinear_u8x4(ptr(img), img.shape[1] * 4, x, y, ptr(out))
+    return out
+
+
+def colour_average(rgb, w, sample, maxW=100):
+    """computeUpdatedVoxelColorInfo's running average (SceneReconstructionEngine.hpp:124-147):
+    (r, g, b), w_color and an interpolated sample -> (r', g', b'), w_color'."""
+    clr = int(rgb[0]) | (int(rgb[1]) << 8) | (int(rgb[2]) << 16) | (int(w) << 24)
+    s = np.zeros(4, np.float32)
+    s[:3] = sample[:3]
+    o = lib().tfo_colour_average(clr, ptr(s), maxW)
+    return (o & 255, (o >> 8) & 255, (o >> 16) & 255), o >> 24
 
 
 # ---- stateful pipeline -------------------------------------------------------

@@ -12,8 +12,14 @@
 //   dot / length (generic)              Vector.hpp:814-824  (castRay totalLength, VisualisationEngine_Shared.hpp:116)
 //   Voxel_s layout / conversions        VoxelTypes.hpp:69-92
 //   MIN-based TSDF update arithmetic     MathUtils.hpp:3-4 with Voxel_s (SceneReconstructionEngine.hpp:56-68)
+//   interpolateBilinear<uchar>          PixelUtils.hpp:8-32 (computeUpdatedVoxelColorInfo's RGB sample,
+//                                       SceneReconstructionEngine.hpp:138)
+//   colour running average              Vector3f / Vector3u operators, TO_FLOAT3 / TO_UCHAR3 (Math.hpp:56-68,
+//                                       Vector.hpp:242-244) with Voxel_s_rgb (SceneReconstructionEngine.hpp:124-147)
+//   Voxel_s_rgb layout / initial value   VoxelTypes.hpp:39-67
 #include "Math.hpp"
 #include "tfusion/cuda/VoxelTypes.hpp"
+#include "tfusion/cuda/PixelUtils.hpp"
 #include <cstdio>
 #include <cstdint>
 #include <cstring>
@@ -130,6 +136,68 @@ int main(int argc, char** argv)
             io.push_back((float)out_sdf); io.push_back((float)newW);
         }
         write_f32(out + "/ref_pin_voxel.bin", io);
+    }
+    // 5. interpolateBilinear<uchar> over an RGBA8 image (PixelUtils.hpp:8-32), at positions inside
+    //    computeUpdatedVoxelColorInfo's window [1, W-2] x [1, H-2], integer coordinates included
+    //    (the delta == 0 branches); record: x, y, 4 results (the image is written first)
+    {
+        const int W = 23, H = 17;
+        std::vector<Vector4u> img(W * H);
+        std::vector<float> io;
+        for (int k = 0; k < W * H; ++k) {
+            uint32_t r = rnd_u32();
+            img[k] = Vector4u((uchar)(r & 255), (uchar)((r >> 8) & 255), (uchar)((r >> 16) & 255), (uchar)((r >> 24) & 255));
+            io.push_back((float)img[k].x); io.push_back((float)img[k].y); io.push_back((float)img[k].z); io.push_back((float)img[k].w);
+        }
+        const Vector2i sz(W, H);
+        for (int k = 0; k < 4096; ++k) {
+            float x = rnd_f(1.0f, (float)(W - 2)), y = rnd_f(1.0f, (float)(H - 2));
+            const int sel = rnd_u32() % 4;
+            if (sel == 0) x = floorf(x);
+            if (sel == 1) y = floorf(y);
+            if (sel == 2) { x = floorf(x); y = floorf(y); }
+            const Vector2f pos(x, y);
+            Vector4f r = interpolateBilinear(&img[0], pos, sz);
+            io.push_back(x); io.push_back(y);
+            io.push_back(r.x); io.push_back(r.y); io.push_back(r.z); io.push_back(r.w);
+        }
+        write_f32(out + "/ref_pin_bilinear.bin", io);
+    }
+    // 6. Voxel_s_rgb layout and the colour running average of computeUpdatedVoxelColorInfo
+    //    (SceneReconstructionEngine.hpp:124-147) in the reference's own vector types; record:
+    //    r, g, b, w_color, sample r, g, b, then r', g', b', w_color'
+    {
+        std::vector<float> io;
+        Voxel_s_rgb v0;
+        io.push_back((float)sizeof(Voxel_s_rgb)); io.push_back((float)v0.sdf); io.push_back((float)v0.w_depth);
+        io.push_back((float)v0.clr.x); io.push_back((float)v0.clr.y); io.push_back((float)v0.clr.z); io.push_back((float)v0.w_color);
+        const uchar maxW = 100;
+        for (int k = 0; k < 8192; ++k) {
+            Voxel_s_rgb voxel;
+            voxel.clr = Vector3u((uchar)(rnd_u32() % 256), (uchar)(rnd_u32() % 256), (uchar)(rnd_u32() % 256));
+            voxel.w_color = (uchar)(rnd_u32() % 101);
+            // an interpolated sample: a convex combination of four uchar values (PixelUtils.hpp:23-24)
+            const Vector4f sample(rnd_f(0.f, 255.f), rnd_f(0.f, 255.f), rnd_f(0.f, 255.f), 0.f);
+            io.push_back((float)voxel.clr.x); io.push_back((float)voxel.clr.y); io.push_back((float)voxel.clr.z);
+            io.push_back((float)voxel.w_color);
+            io.push_back(sample.x); io.push_back(sample.y); io.push_back(sample.z);
+            Vector3f rgb_measure, oldC, newC; Vector3u buffV3u;
+            float newW, oldW;
+            buffV3u = voxel.clr;
+            oldW = (float)voxel.w_color;
+            oldC = TO_FLOAT3(buffV3u) / 255.0f;
+            rgb_measure = TO_VECTOR3(sample) / 255.0f;
+            newW = 1;
+            newC = oldC * oldW + rgb_measure * newW;
+            newW = oldW + newW;
+            newC /= newW;
+            newW = MIN(newW, maxW);
+            voxel.clr = TO_UCHAR3(newC * 255.0f);
+            voxel.w_color = (uchar)newW;
+            io.push_back((float)voxel.clr.x); io.push_back((float)voxel.clr.y); io.push_back((float)voxel.clr.z);
+            io.push_back((float)voxel.w_color);
+        }
+        write_f32(out + "/ref_pin_colour.bin", io);
     }
     printf("ref_pin: wrote goldens to %s\n", out.c_str());
     return 0;

@@ -1006,15 +1006,20 @@ static inline uint32_t u8_round(float v)
 static inline void update_voxel_colour(uint32_t* clr, const float pt_model[4], const float Mr[16], const float proj[4],
                                        int maxW, const uint8_t* rgb, size_t pitch, int W, int H)
 {
-    float oldW = (float)(*clr >> 24);
-    float oldC[3], newC[3];
-    for (int k = 0; k < 3; ++k) oldC[k] = (float)((*clr >> (8 * k)) & 0xffu) / 255.0f;
     float pc[4];
     m4v(Mr, pt_model, pc);
     float ix = proj[0] * pc[0] / pc[2] + proj[2];
     float iy = proj[1] * pc[1] / pc[2] + proj[3];
     if (isnan(ix) || isnan(iy)) return;
     if ((ix < 1) || (ix > (float)(W - 2)) || (iy < 1) || (iy > (float)(H - 2))) return;
+    float m4[4];
+    tfo_interp_bilinear_u8x4(rgb, pitch, ix, iy, m4);
+    *clr = tfo_colour_average(*clr, m4, maxW);
+}
+
+/* interpolateBilinear<uchar> (PixelUtils.hpp:8-32) of an RGBA8 image at (ix, iy) */
+void tfo_interp_bilinear_u8x4(const uint8_t* rgb, size_t pitch, float ix, float iy, float out[4])
+{
     int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
     float dx = ix - (float)x0, dy = iy - (float)y0;
     static const uint8_t zero[4] = { 0, 0, 0, 0 };
@@ -1023,18 +1028,28 @@ static inline void update_voxel_colour(uint32_t* clr, const float pt_model[4], c
     if (dx != 0) b = a + 4;
     if (dy != 0) cc = a + pitch;
     if (dx != 0 && dy != 0) d = a + pitch + 4;
+    for (int k = 0; k < 4; ++k)
+        out[k] = ((float)a[k] * (1.0f - dx) * (1.0f - dy) + (float)b[k] * dx * (1.0f - dy) +
+                  (float)cc[k] * (1.0f - dx) * dy + (float)d[k] * dx * dy);
+}
+
+/* the running colour average of computeUpdatedVoxelColorInfo (SceneReconstructionEngine.hpp:
+   124-147) on a colour word r | g << 8 | b << 16 | w_color << 24, given the interpolated sample */
+uint32_t tfo_colour_average(uint32_t clr, const float sample[4], int maxW)
+{
+    float oldW = (float)(clr >> 24);
+    float oldC[3], newC[3];
+    for (int k = 0; k < 3; ++k) oldC[k] = (float)((clr >> (8 * k)) & 0xffu) / 255.0f;
     float newW = 1;
     for (int k = 0; k < 3; ++k) {
-        float m = ((float)a[k] * (1.0f - dx) * (1.0f - dy) + (float)b[k] * dx * (1.0f - dy) +
-                   (float)cc[k] * (1.0f - dx) * dy + (float)d[k] * dx * dy);
-        m = m / 255.0f;
+        float m = sample[k] / 255.0f;
         newC[k] = oldC[k] * oldW + m * newW;
     }
     newW = oldW + newW;
     for (int k = 0; k < 3; ++k) newC[k] /= newW;
     float mw = (float)(uint8_t)maxW;
     newW = (newW < mw) ? newW : mw;
-    *clr = u8_round(newC[0] * 255.0f) | (u8_round(newC[1] * 255.0f) << 8) | (u8_round(newC[2] * 255.0f) << 16) |
+    return u8_round(newC[0] * 255.0f) | (u8_round(newC[1] * 255.0f) << 8) | (u8_round(newC[2] * 255.0f) << 16) |
            ((uint32_t)(uint8_t)newW << 24);
 }
 

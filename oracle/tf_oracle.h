@@ -121,6 +121,8 @@ void tfo_m4v(const float m[16], const float v[4], float r[4]);
 void tfo_tsdf_update(int16_t* sdf, uint8_t* w, float eta, float mu, int maxW);
 void tfo_rodrigues(const float r[3], float R[9]);
 void tfo_point_conv(const float p[3], float out[13]);     /* floor/round/length conversions */
+void tfo_interp_bilinear_u8x4(const uint8_t* rgb, size_t pitch, float ix, float iy, float out[4]); /* interpolateBilinear<uchar> */
+uint32_t tfo_colour_average(uint32_t clr, const float sample[4], int maxW);  /* colour running average */
 int  tfo_hash_index(int x, int y, int z, int n_buckets);
 
 /* ---- stateful pipeline (TopFu) ---- */

@@ -3,9 +3,10 @@ container, where /root/reference exists; the GPU box only reads the committed fi
 
   1. `make -C oracle ref` compiles oracle/ref_pin/ref_pin.cpp against the reference's own,
      self-contained headers (tfusion/include/Math.hpp, Vector.hpp, Matrix.hpp,
-     MathUtils.hpp, tfusion/cuda/VoxelTypes.hpp) into oracle/_ref/ref_pin -- no stand-in
+     MathUtils.hpp, tfusion/cuda/VoxelTypes.hpp, tfusion/cuda/PixelUtils.hpp) into
+     oracle/_ref/ref_pin -- no stand-in
      headers, nothing from the reference is copied into the repo.
-  2. oracle/_ref/ref_pin writes ref_pin_{inv,m4v,round,voxel}.bin here (raw little-endian
+  2. oracle/_ref/ref_pin writes ref_pin_{inv,m4v,round,voxel,bilinear,colour}.bin here (raw little-endian
      f32 records; layouts in tests/test_oracle.py).
 
     python tests/golden/make_golden.py
