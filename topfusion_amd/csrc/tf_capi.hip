@@ -296,11 +296,6 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     e = tfk_reset_scene(c);                              // topfu.cpp:75
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = tfk_check_div3(c, pin->mu, &c->mu_exact3);   // integrate: eta / mu
-    if (e == hipSuccess) e = tfk_check_rcp(c, &c->div_rcp);               // integrate: projection
-    {
-        const char* env = getenv("TFUSION_DIV_RCP");
-        if (env && env[0] == '0') c->div_rcp = 0;
-    }
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     {   // ICP: one persistent launch per frame when all its workgroups fit at once; otherwise (or
         // with TFUSION_ICP_PERSISTENT=0) one k_icp_iter launch per iteration

@@ -186,29 +186,6 @@ __device__ __forceinline__ float tf_div_exact3(float x, float d, float rd)
     return fmaf(-fmaf(q0, d, -x), rd, q0);
 }
 
-// n / z for the integrate projection in six operations instead of two IEEE division sequences:
-// y = RN(1/z) by one Newton step from v_rcp_f32 (checked at tf_create on the device for every
-// mantissa of a binade, tf_ctx::div_rcp), q0 = RN(n*y), r = n - z*q0 (exact by fma), q =
-// RN(q0 + r*y) -- Markstein's correction, which is the correctly rounded quotient whenever y is
-// RN(1/z) and nothing over- or underflows.  tf_div_rcp_ok bounds the operands so that nothing
-// does (z, |n| in [2^-40, 2^40]) and excludes the all-ones mantissa of z, the reciprocal the
-// Newton step can miss; the rest take the IEEE division.
-__device__ __forceinline__ float tf_rcp_rn(float z)
-{
-    const float y0 = __builtin_amdgcn_rcpf(z);
-    return fmaf(fmaf(-z, y0, 1.0f), y0, y0);
-}
-__device__ __forceinline__ float tf_div_rcp(float n, float z, float y)
-{
-    const float q0 = n * y;
-    return fmaf(fmaf(-z, q0, n), y, q0);
-}
-__device__ __forceinline__ bool tf_div_rcp_ok(float nx, float ny, float z)
-{
-    const float hi = fmaxf(fmaxf(fabsf(nx), fabsf(ny)), z), lo = fminf(fminf(fabsf(nx), fabsf(ny)), z);
-    return hi <= 0x1p40f && lo >= 0x1p-40f && (__float_as_uint(z) & 0x7fffffu) != 0x7fffffu;
-}
-
 // A missing block's VBA offset in the block grid: the render side reads voxels relative to a
 // guard block of Voxel_s() values placed just before the VBA (tf_ctx::vba_guard), so a voxel
 // load needs no "is the block there" select -- it lands in the guard and reads (32767, 0).
@@ -285,7 +262,6 @@ struct tf_ctx {
     int* excessList;
     TfVoxel* vba;
     int mu_exact3;          // eta / mu by tf_div_exact3 (checked on the device at tf_create)
-    int div_rcp;            // integrate's n / z by tf_div_rcp (tf_rcp_rn checked on the device at tf_create)
     TfVoxel* vba_guard;      // allocation: one guard block of Voxel_s() (TF_VOFF_NONE reads), then vba
     int* allocList;
     int2* bgrid;             // block grid (TF_GRID_*), mirrors the hash
@@ -393,8 +369,7 @@ hipError_t tfk_reset_scene(tf_ctx* c);
 hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot);   // frame end + ResetScene if ICP failed
 hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a hash upload)
 hipError_t tfk_grid_clear(tf_ctx* c);     // every cell (-1, TF_VOFF_NONE)
-hipError_t tfk_check_div3(tf_ctx* c, float d, int* ok);
-hipError_t tfk_check_rcp(tf_ctx* c, int* ok);             // tf_rcp_rn(z) == 1 / z over a binade   // tf_div_exact3(x, d) == x / d over a binade
+hipError_t tfk_check_div3(tf_ctx* c, float d, int* ok);   // tf_div_exact3(x, d) == x / d over a binade
 // a later frame of the batch whose preprocessing (part) runs in a frame kernel's grid tail
 struct TfAhead {
     const uint16_t* src;     // raw depth (nullptr: none)

@@ -17,9 +17,6 @@
 #include "tf_vis.h"
 
 #define TF_INTEG_STREAM_BLOCKS 16384   // 32 MiB of voxels
-#ifndef TF_INTEG_PIPE
-#define TF_INTEG_PIPE 0
-#endif
 #define CHUNK 4096          // hash entries per workgroup in the scan passes (256 thr x 16)
 
 // byte i (0..15) of a 16-byte group held as two 64-bit words (no dynamic register indexing)
@@ -129,37 +126,6 @@ hipError_t tfk_check_div3(tf_ctx* c, float d, int* ok)
     hipError_t e = hipMemcpyAsync(dok, &one, sizeof(int), hipMemcpyHostToDevice, c->stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_check_div3, dim3((1u << 23) / 256), dim3(256), 0, c->stream, d, dok);
-    e = hipMemcpyAsync(ok, dok, sizeof(int), hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    int zero = 0;
-    if (e == hipSuccess) e = hipMemcpyAsync(dok, &zero, sizeof(int), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    return e;
-}
-
-// tf_rcp_rn(z) == 1 / z for every mantissa of the binades [1, 2) and [2^20, 2^21) but the
-// all-ones one (tf_div_rcp_ok excludes it); v_rcp_f32 and the Newton step scale exactly with the
-// exponent over the range tf_div_rcp_ok admits
-__global__ void k_check_rcp(int* ok)
-{
-    const unsigned m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= (1u << 23) - 1) return;
-    bool good = true;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        const float z = __uint_as_float((b ? 0x49800000u : 0x3f800000u) | m);
-        good = good && __float_as_uint(tf_rcp_rn(z)) == __float_as_uint(1.0f / z);
-    }
-    if (!good) atomicAnd(ok, 0);
-}
-
-hipError_t tfk_check_rcp(tf_ctx* c, int* ok)
-{
-    int* dok = (int*)c->icp_ticket;              // scratch word (the ticket is idle at creation)
-    int one = 1;
-    hipError_t e = hipMemcpyAsync(dok, &one, sizeof(int), hipMemcpyHostToDevice, c->stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_check_rcp, dim3((1u << 23) / 256), dim3(256), 0, c->stream, dok);
     e = hipMemcpyAsync(ok, dok, sizeof(int), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     int zero = 0;
@@ -736,7 +702,6 @@ struct IntegArgs {
     float voxelSize, mu;
     float inv_mu;                       // RN(1/mu) when mu_exact3 (eta / mu in three operations)
     int mu_exact3;
-    int div_rcp;                        // fx * pc.x / pc.z by tf_div_rcp (tf_ctx::div_rcp)
     int maxW;
     // frame 0 of the device-driven frame: prev_ = curr_ (topfu.cpp:205 swaps the pyramids;
     // copying keeps the buffer pointers fixed); levels contiguous, n_maps float4 per map
@@ -761,16 +726,8 @@ __device__ __forceinline__ bool integ_project(float px, float py, float pz, cons
     tf_m4v3(M, px, py, pz, 1.0f, pc);
     *z = pc[2];
     if (pc[2] <= 0) return false;
-    const float nx = a.fx * pc[0], ny = a.fy * pc[1];
-    float qx, qy;
-    if (a.div_rcp && tf_div_rcp_ok(nx, ny, pc[2])) {
-        const float y = tf_rcp_rn(pc[2]);
-        qx = tf_div_rcp(nx, pc[2], y); qy = tf_div_rcp(ny, pc[2], y);
-    } else {
-        qx = nx / pc[2]; qy = ny / pc[2];
-    }
-    float ix = qx + a.cx;
-    float iy = qy + a.cy;
+    float ix = a.fx * pc[0] / pc[2] + a.cx;
+    float iy = a.fy * pc[1] / pc[2] + a.cy;
     if ((ix < 1) || (ix > (float)(a.W - 2)) || (iy < 1) || (iy > (float)(a.H - 2))) return false;
     *idx = (int)(ix + 0.5f) + (int)(iy + 0.5f) * a.W;
     return true;
@@ -938,21 +895,6 @@ __device__ __forceinline__ void integ_apply_pair(uint4 v, uint4 v2, const float 
     }
 }
 
-// the lane's four voxels of each of two blocks (ptr < 0: no block): project, sample, update
-template <bool RGB>
-__device__ __forceinline__ void integ_pair(uint4 v, uint4 v2, const TfHashEntry& e, const TfHashEntry& e2, int vx,
-                                           int vy, int vz, const float* M, const IntegArgs& a, uint4* p, uint4* p2,
-                                           const float* rw, bool stream, const float* Mr, int lin, int* n_rd, int* n_wr)
-{
-    float z[8], dm[8];
-    int di[8];
-    bool ok[8];
-    integ_proj_pair(e, e2, vx, vy, vz, M, a, z, di, ok);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) dm[k] = a.dists[di[k]];
-    integ_apply_pair<RGB>(v, v2, dm, z, ok, e, e2, vx, vy, vz, a, p, p2, rw, stream, Mr, lin, n_rd, n_wr);
-}
-
 template <bool WITH_ED, bool RGB>
 __global__ void __launch_bounds__(256)
 k_integrate(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
@@ -1008,7 +950,6 @@ k_integrate(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restr
     // pass is a stream over 8.6 GB)
     const int stride = nblk * 2;
     int n_rd = 0, n_wr = 0;
-#if TF_INTEG_PIPE == 2
     // Software pipeline over the grid-stride passes, three deep: pass k projects pass k+1's
     // voxels (its entries arrived during pass k-1) and issues their voxel loads and depth
     // samples, issues pass k+2's entry loads and pass k+3's id loads, and only then updates pass
@@ -1069,53 +1010,6 @@ k_integrate(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restr
             for (int k = 0; k < 8; ++k) { z[k] = zn[k]; dm[k] = dmn[k]; ok[k] = okn[k]; }
         }
     }
-#elif TF_INTEG_PIPE
-    // Software pipeline over the grid-stride passes: at the top of pass k the hash entries of
-    // pass k and the visible ids of pass k+1 are in registers; pass k issues its voxel loads,
-    // pass k+1's entry loads and pass k+2's id loads together, so the id -> entry -> voxel
-    // chain costs one round trip per pass instead of three.  Loads past the list read its last
-    // element (valid memory; the results are discarded).
-    const int step = 2 * stride;
-    int i = bid * 2 + half;
-    TfHashEntry e, e2;
-    int nid1 = 0, nid2 = 0;
-    if (i < n) {
-        const int id1 = visibleIds[i], id2 = visibleIds[min(i + stride, n - 1)];
-        const int j = min(i + step, n - 1), j2 = min(i + step + stride, n - 1);
-        nid1 = visibleIds[j]; nid2 = visibleIds[j2];
-        e = hash[id1]; e2 = hash[id2];
-    }
-    for (; i < n; i += step) {
-        if (!(i + stride < n)) e2.ptr = -1;
-        uint4* p = (uint4*)(vba + (size_t)(e.ptr < 0 ? 0 : e.ptr) * TF_BLK3 + lin);
-        uint4* p2 = (uint4*)(vba + (size_t)(e2.ptr < 0 ? 0 : e2.ptr) * TF_BLK3 + lin);
-        uint4 v, v2;
-        if (stream) { v = nt_load16(p); v2 = nt_load16(p2); }
-        else { v = *p; v2 = *p2; }
-        const TfHashEntry ne = hash[nid1], ne2 = hash[nid2];
-        const int j = min(i + 2 * step, n - 1), j2 = min(i + 2 * step + stride, n - 1);
-        const int nn1 = visibleIds[j], nn2 = visibleIds[j2];
-        integ_pair<RGB>(v, v2, e, e2, vx, vy, vz, M, a, p, p2, rw, stream, Mr, lin, &n_rd, &n_wr);
-        e = ne; e2 = ne2; nid1 = nn1; nid2 = nn2;
-    }
-#else
-    for (int i = bid * 2 + half; i < n; i += 2 * stride) {
-        const int i2 = i + stride;
-        const bool has2 = i2 < n;                    // (loads unconditional: both chains together)
-        const int id1 = visibleIds[i], id2 = visibleIds[has2 ? i2 : i];
-        const TfHashEntry e = hash[id1];
-        TfHashEntry e2 = hash[id2];
-        if (!has2) e2.ptr = -1;
-        uint4* p = (uint4*)(vba + (size_t)(e.ptr < 0 ? 0 : e.ptr) * TF_BLK3 + lin);
-        uint4* p2 = (uint4*)(vba + (size_t)(e2.ptr < 0 ? 0 : e2.ptr) * TF_BLK3 + lin);
-        // the voxel stream is read and written once per pass: non-temporal, so it does not
-        // evict the depth image every voxel samples from L2
-        uint4 v, v2;
-        if (stream) { v = nt_load16(p); v2 = nt_load16(p2); }
-        else { v = *p; v2 = *p2; }
-        integ_pair<RGB>(v, v2, e, e2, vx, vy, vz, M, a, p, p2, rw, stream, Mr, lin, &n_rd, &n_wr);
-    }
-#endif
     // lanes read / written (profiling / stand-alone passes): the workgroup's running counts in
     // its own slot, plain read-modify-write (launches on one stream; no atomics to contend)
     if (!cnt) return;
@@ -1141,7 +1035,7 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
     a.dists = c->dists; a.W = c->W; a.H = c->H;
     a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy;
     a.voxelSize = c->p.voxelSize; a.mu = c->p.mu; a.maxW = c->p.maxW;
-    a.inv_mu = 1.0f / c->p.mu; a.mu_exact3 = c->mu_exact3; a.div_rcp = c->div_rcp;
+    a.inv_mu = 1.0f / c->p.mu; a.mu_exact3 = c->mu_exact3;
     const bool rgb = c->p.voxel_rgb && c->rgb_cur;
     a.rgb = c->rgb_cur; a.rgb_pitch = c->rgb_pitch; a.vba_rgb = c->vba_rgb;
     const float* q = c->p.rgb_intr;
