@@ -394,6 +394,53 @@ def test_two_contexts_one_device(oracle_mod):
     g2.close()
 
 
+def test_concurrent_contexts_one_device(oracle_mod):
+    """Three contexts on one device driven at the same time from three host threads (C4's
+    replicas, several per GPU): batched 320x240 streams seeded 7, 8 and 9 enqueued together, so
+    their kernels interleave on the device -- the persistent ICP launches, which each need the
+    whole chip, ordered across the contexts (tf_icp_order_*).  Each context bit-exact with its own
+    oracle: per-frame ok flags, counters, final pose, raycast and scene."""
+    import threading
+    from parity_util import DeviceFrames
+    from topfusion_amd import TopFu, default_params
+    cols, rows, n = 320, 240, 24
+    fx, fy, cx, cy = synth.intrinsics(cols, rows)
+    args = dict(cols=cols, rows=rows, fx=fx, fy=fy, cx=cx, cy=cy)
+    seeds = (7, 8, 9)
+    seqs = [synth.orbit_sequence(n, cols, rows, seed=sd) for sd in seeds]
+    ctxs = [TopFu(default_params(**args)) for _ in seeds]
+    devs = [DeviceFrames(sq) for sq in seqs]
+    res, errs = {}, []
+
+    def run(i):
+        try:
+            res[i] = ctxs[i].process_frames(devs[i].ptr, n)
+        except Exception as ex:                     # reported by the main thread
+            errs.append(f"context {i}: {ex!r}")
+
+    threads = [threading.Thread(target=run, args=(i,)) for i in range(len(seeds))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in threads), "a context did not finish"
+    assert not errs, errs
+    for i, sd in enumerate(seeds):
+        o = oracle_mod.Oracle(oracle_mod.default_params(**args))
+        oko = np.array([o(seqs[i][k]) for k in range(n)])
+        tag = f"concurrent ctx seed {sd}"
+        assert np.array_equal(res[i], oko), (tag, res[i], oko)
+        sg, so = ctxs[i].stats(), o.counters()
+        for key in ("frame_counter", "n_resets", "icp_iterations"):
+            assert sg[key] == so[key], f"{tag} {key}: gpu {sg[key]} oracle {so[key]}"
+        assert_bit_exact(f"{tag} final pose", ctxs[i].getCameraPose()[:3, :4], o.pose())
+        assert_bit_exact(f"{tag} final raycast", ctxs[i].raycast_result(), o.raycast_result())
+        compare_scene(ctxs[i], o, tag)
+    for g, d in zip(ctxs, devs):
+        g.close()
+        d.free()
+
+
 def test_c3_capacity_top_block(oracle_mod):
     """The C3 bench capacity (2^21 - 1 voxel blocks = 4 GiB, 2^22 buckets, 2^20 excess) at C3
     geometry (1280x960, 2 mm): allocation hands out blocks from the top of the free list, so the

@@ -101,9 +101,54 @@ static bool params_valid(const tf_params* p)
     return true;
 }
 
+// ---------------------------------------------------------------------------------------
+// persistent-ICP ordering among the contexts of one device (see tf_internal.h)
+// ---------------------------------------------------------------------------------------
+#include <mutex>
+#define TF_MAX_DEVICES 64
+static std::mutex g_icp_mu;
+static int g_icp_ctx_count[TF_MAX_DEVICES];          // live contexts per device
+static tf_ctx* g_icp_last[TF_MAX_DEVICES];          // context of the last persistent ICP launch
+
+static void icp_order_register(tf_ctx* c, int add)
+{
+    if (c->device < 0 || c->device >= TF_MAX_DEVICES) return;
+    std::lock_guard<std::mutex> lk(g_icp_mu);
+    g_icp_ctx_count[c->device] += add;
+    if (add < 0 && g_icp_last[c->device] == c) g_icp_last[c->device] = nullptr;
+    // a single context records nothing (an event record per frame costs the device ~4 us): when
+    // a second one arrives, the last launcher's stream is marked here, so the newcomer's first
+    // ICP waits for everything already enqueued there
+    tf_ctx* last = g_icp_last[c->device];
+    if (add > 0 && last && last != c) (void)hipEventRecord(last->icp_ev, last->stream);
+}
+
+// called with the launch enqueued between before() and after(), from one host thread per context
+hipError_t tf_icp_order_before(tf_ctx* c)
+{
+    if (c->device < 0 || c->device >= TF_MAX_DEVICES || !c->icp_ev) return hipSuccess;
+    g_icp_mu.lock();                                  // released by tf_icp_order_after
+    tf_ctx* last = g_icp_last[c->device];
+    if (g_icp_ctx_count[c->device] > 1 && last && last != c) return hipStreamWaitEvent(c->stream, last->icp_ev, 0);
+    return hipSuccess;
+}
+
+hipError_t tf_icp_order_after(tf_ctx* c)
+{
+    if (c->device < 0 || c->device >= TF_MAX_DEVICES || !c->icp_ev) return hipSuccess;
+    const hipError_t e = g_icp_ctx_count[c->device] > 1 ? hipEventRecord(c->icp_ev, c->stream) : hipSuccess;
+    g_icp_last[c->device] = c;
+    g_icp_mu.unlock();
+    return e;
+}
+
 static void ctx_free(tf_ctx* c)
 {
     if (!c) return;
+    if (c->icp_ev) {
+        icp_order_register(c, -1);
+        (void)hipEventDestroy(c->icp_ev);
+    }
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
@@ -301,6 +346,11 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         // with TFUSION_ICP_PERSISTENT=0) one k_icp_iter launch per iteration
         const char* env = getenv("TFUSION_ICP_PERSISTENT");
         c->icp_persistent = (env && env[0] == '0') ? 0 : tfk_icp_persistent_ok(c);
+    }
+    if (c->icp_persistent) {
+        e = hipEventCreateWithFlags(&c->icp_ev, hipEventDisableTiming);
+        if (e != hipSuccess) { c->icp_ev = nullptr; ctx_free(c); return tf_from_hip(e); }
+        icp_order_register(c, +1);
     }
     *out = c;
     return TF_OK;

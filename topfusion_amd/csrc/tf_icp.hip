@@ -895,8 +895,13 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
         }
         // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
         // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up
-        tf_launch(c, k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, a);
-        return hipGetLastError();
+        hipError_t e = tf_icp_order_before(c);
+        if (e == hipSuccess) {
+            tf_launch(c, k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, a);
+            e = hipGetLastError();
+        }
+        const hipError_t e2 = tf_icp_order_after(c);     // (always: releases the ordering lock)
+        return e != hipSuccess ? e : e2;
     }
     hipLaunchKernelGGL(k_icp_begin, dim3(1), dim3(1), 0, c->stream, c->st, frame_begin);
     int last_l = -1;

@@ -339,6 +339,8 @@ struct tf_ctx {
     // hipExtLaunchKernelGGL ties to the dispatch's own begin / end (what rocprofv3 reports);
     // event records around a launch were measured to include earlier work (ICP: 148 vs 85 us)
     hipEvent_t ev_start, ev_stop;
+    // persistent-ICP ordering among the contexts of one device (tf_icp_order_*, tf_capi.hip)
+    hipEvent_t icp_ev;
     double prof_ms[TF_NUM_STAGES];
     long long prof_count[TF_NUM_STAGES];
 };
@@ -362,7 +364,14 @@ inline void tf_launch(tf_ctx* c, void (*kern)(KArgs...), dim3 grid, dim3 block, 
 hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStream_t strm, uint16_t* d0);   // no st access
 // fold_t3: k_set_type3's work in the persistent ICP grid's tail (frame path; the caller then
 // passes snapshot = 2 to tfk_alloc)
-hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin = 0, int fold_t3 = 0);   // frame_begin: frame path (tf_frame_begin)
+hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin = 0, int fold_t3 = 0);
+// Persistent ICP launches of different contexts on one device must not run at the same time:
+// each needs all 256 of its workgroups resident at once (one per CU) and spins on the others, so
+// two of them dispatched together could each hold part of the chip and wait on each other.  With
+// more than one context on a device, every persistent ICP launch waits (on the device) for the
+// previous one of another context.  One context per device (the bench, C4) waits on nothing.
+hipError_t tf_icp_order_before(tf_ctx* c);
+hipError_t tf_icp_order_after(tf_ctx* c);   // frame_begin: frame path (tf_frame_begin)
 int tfk_icp_persistent_ok(tf_ctx* c);      // k_icp_frame fits (co-residency, slot count)
 hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / raycast matrices
 hipError_t tfk_reset_scene(tf_ctx* c);
