@@ -442,29 +442,6 @@ __device__ __forceinline__ float ip_cta_reduce(const float (&r)[4][7], int lane)
     return v[0] + xor1(v[0]);
 }
 
-// final 256-wide tree of the column sums in LDS -> the 27 sums in every lane (uniform)
-__device__ __forceinline__ void ip_final_tree(const float (*tv)[ICP_NWG + 1], int lane, float (&sm)[27])
-{
-    float v[32];
-#pragma unroll
-    for (int q = 0; q < 27; ++q) {
-        float a0 = tv[q][lane] + tv[q][lane + 128];
-        float a1 = tv[q][lane + 64] + tv[q][lane + 192];
-        v[q] = a0 + a1;
-    }
-#pragma unroll
-    for (int q = 27; q < 32; ++q) v[q] = 0.f;
-    tstep<32, 32>(v, lane);
-    tstep<16, 16>(v, lane);
-    tstep<8, 8>(v, lane);
-    tstep<4, 4>(v, lane);
-    tstep<2, 2>(v, lane);
-    const float tot = v[0] + xor1(v[0]);
-#pragma unroll
-    for (int q = 0; q < 27; ++q)
-        sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), 2 * q));
-}
-
 __device__ __forceinline__ void ip_unpack(const float (&sm)[27], float (&Am)[6][6], float (&bv)[6])
 {   // StreamHelper::get (projective_icp.cpp:51-61)
     int shift = 0;
