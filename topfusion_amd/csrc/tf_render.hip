@@ -36,6 +36,9 @@ struct RCache { int bx, by, bz; };
 // reference's serial corner order.  Values, the IndexCache state and vmIndex are exactly
 // those of the reference's serial reads (RepresentationAccess.hpp:73-199).
 // ---------------------------------------------------------------------------------------
+#ifndef TF_RAY_SPEC
+#define TF_RAY_SPEC 1
+#endif
 __device__ __forceinline__ int vblk(int p) { return p >> 3; }   // floor(p / 8) (:9-17), arithmetic shift
 __device__ __forceinline__ int vlin(int x, int y, int z) { return (x & 7) + ((y & 7) << 3) + ((z & 7) << 6); }
 
@@ -369,6 +372,57 @@ __device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, 
 {
     Ray R;
     ray_init(a, invM, x, y, R);
+#if TF_RAY_SPEC
+    if (!MARK) {
+        // castRay<false> (renderImage, stand-alone raycasts): speculative block lookups, per lane.
+        // While a step's voxels are in flight, the eight VBA offsets of the position the NEXT step
+        // has if this one is the common kind -- sdf = 1 in an allocated block (step
+        // max(stepScale, 1)) or no block (step SDF_BLOCK_SIZE), computed by ray_step's own
+        // operations -- are loaded too.  A lane whose actual position equals its speculated one
+        // bit for bit starts the next step with its lookups done; a step whose live lanes all hit
+        // skips the grid round trip.  (Without visibility marks only vmIndex != 0 matters, so the
+        // hash index of the ROUND corner is not needed.)
+        const float qq1 = 1.0f * (a.mu * a.oneOverVoxelSize);
+        const float Lsdf1 = (qq1 < 1.0f) ? 1.0f : qq1;
+        bool have = false;
+        int sv[8];
+        while (R.active) {
+            Corners q;
+            unsigned o[8];
+            const bool in = corners_prep(R.pt, q, o);
+            if (wave_any(!have)) {
+                int2 g[8];
+                if (wave_any(!have && !in)) corners_slow(a.s, q, g);
+                else if (!have) blk_load8(a.s, o, g);
+                if (!have) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) sv[c] = g[c].y;
+                }
+            }
+            q.valid = 0;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) { q.voff[c] = sv[c]; q.valid |= (sv[c] >= 0 ? 1u : 0u) << c; }
+            q.hU = 0;
+            const bool found = (q.valid >> q.cu) & 1u;
+            if (wave_any(found)) corners_vox(a.s, q);
+            const float L = found ? Lsdf1 : (float)TF_BLK;
+            float ps[3];
+            ps[0] = R.pt[0] + L * R.dir[0]; ps[1] = R.pt[1] + L * R.dir[1]; ps[2] = R.pt[2] + L * R.dir[2];
+            {
+                Corners qs;
+                unsigned os[8];
+                have = corners_prep(ps, qs, os);
+                if (have) {
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) sv[c] = ld_off<int>(a.s.grid, os[c] + 4u);
+                }
+            }
+            ray_step<MARK>(a, R, q);
+            have = have && __float_as_uint(R.pt[0]) == __float_as_uint(ps[0]) &&
+                   __float_as_uint(R.pt[1]) == __float_as_uint(ps[1]) && __float_as_uint(R.pt[2]) == __float_as_uint(ps[2]);
+        }
+    } else
+#endif
     while (R.active) {
         Corners q;
         corners_lookup(a.s, R.pt, q);
