@@ -301,6 +301,14 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 #define IP_NPART 8                               // residue classes of the final tree's first five steps
 #define IP_LDS_PAD (56 * 1024)
 #define IP_DETW (IP_WAVES - 1)                   // the wave that runs the det check off the critical path
+// Column sums go to the residue-class leader (workgroup wg % 8).  Each leader publishes its XCD
+// (HW_REG_XCC_ID) at launch; a workgroup that finds its leader on its own XCD publishes its
+// columns with plain stores (kept in the shared L2), any other with write-through sc1 stores.
+// Placement is checked, never assumed: an unknown or different XCD takes the sc1 path.
+#ifndef IP_XCD_STORE
+#define IP_XCD_STORE 1
+#endif
+#define IP_XCC_AT (IP_PART + 2 * IP_NPART * ICP_T_STRIDE)   // the leaders' XCD ids (TF_ICP_TAG_WORDS)
 
 struct IcpFrameArgs {
     IcpLevel lv[TF_LEVELS];             // in processing order (coarse -> fine)
@@ -375,6 +383,19 @@ __device__ __forceinline__ void ip_store(unsigned long long* p, unsigned long lo
 __device__ __forceinline__ unsigned long long ip_load(const unsigned long long* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a granule for a reader on this workgroup's own XCD: a plain 8-byte store stays in the XCD's
+// L2, where the reader's agent-scope (L1-bypassing) loads find it; an sc1 store would drop the
+// line and send the reader to memory
+__device__ __forceinline__ void ip_store_xcd(unsigned long long* p, unsigned long long v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ unsigned ip_xcc_id()
+{
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x;
 }
 
 // find_coresp (points variant) + row (proj_icp.cu:80-117, 365-377) for 4 pixels per lane, with
@@ -515,6 +536,11 @@ k_icp_frame(IcpFrameArgs a)
     }
     const unsigned base = st->icp_gen;
     unsigned gen = base;
+#if IP_XCD_STORE
+    const unsigned my_xcc = ip_xcc_id();
+    if (wg < IP_NPART && tid == 0) ip_store(&tag[IP_XCC_AT + wg], ip_pack(base, __uint_as_float(my_xcc)));
+    int leader_same = wg < IP_NPART ? 1 : -1;          // -1: the leader's XCD not yet known
+#endif
     float aff[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) aff[i] = (i % 5 == 0) ? 1.0f : 0.0f;     // affine = Identity
@@ -615,6 +641,15 @@ k_icp_frame(IcpFrameArgs a)
                     if (wg + ICP_NWG * sl >= L.nct) break;
                     sum += red[sl][tid];
                 }
+#if IP_XCD_STORE
+                if (leader_same < 0) {
+                    const unsigned long long x = ip_load(&tag[IP_XCC_AT + (wg & (IP_NPART - 1))]);
+                    if ((unsigned)(x >> 32) == base) leader_same = __float_as_uint(__uint_as_float((unsigned)x)) == my_xcc ? 1 : 0;
+                }
+                if (leader_same > 0)
+                    ip_store_xcd(&tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE + wg * ICP_T_STRIDE + tid], ip_pack(gen, sum));
+                else
+#endif
                 ip_store(&tag[(gen & 1) * ICP_NWG * ICP_T_STRIDE + wg * ICP_T_STRIDE + tid], ip_pack(gen, sum));
             }
             IPT_REC(done, ICP_NWG + wg);

@@ -22,7 +22,7 @@
 #define TF_NUM_STAGES 9     // tf_stage_id in include/tfusion_hip.h
 #define TF_PROF_RING 32     // frames enqueued between host syncs (and timing-event ring slots)
 #define TF_ST_BYTES (sizeof(TfDevState) + 2 * sizeof(int) * TF_PROF_RING)   // c->st + frame_ok / frame_mode rings
-#define TF_ICP_TAG_WORDS (2 * 256 * 28 + 16 + 2 * 8 * 28)   // persistent ICP tagged granules (tf_icp.hip)
+#define TF_ICP_TAG_WORDS (2 * 256 * 28 + 16 + 2 * 8 * 28 + 16)   // persistent ICP tagged granules (tf_icp.hip)
 
 // HashEntry, VoxelBlockHash.hpp:32-44 (16 B; one dwordx4 probe)
 struct __attribute__((aligned(16))) TfHashEntry {
