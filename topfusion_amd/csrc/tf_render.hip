@@ -1012,11 +1012,13 @@ k_ed_project(EdArgs a, const TfDevState* __restrict__ st)
 //    width (min/max as ints: the z values are positive floats) and writes the row with plain
 //    stores: the /8 columns always, the columns past them up to the last one a box touched.
 //    Rows further down (boxes of blocks close to the camera) take device-scope atomics, spread
-//    over the workgroups by entry index; boxes wider than ED_WIDE are queued for the workgroup.
+//    over the workgroups by entry index; boxes wider than ED_WIDE are queued, one wave each.
 //    Each row records the extent it wrote outside the /8 region for the next projection pass.
 //  - n > a.lds_max_n: one wave per block, its lanes over the block's pixel box, with
 //    device-scope atomics (the projection pass initialised the /8 region).
-#define ED_WIDE 24        // box columns in a row above which the whole workgroup fills it
+#ifndef ED_WIDE
+#define ED_WIDE 4         // box columns in a row above which a wave fills it (queued)
+#endif
 #define ED_QUEUE 256      // queued segments per workgroup (beyond: filled by their thread)
 #define ED_THREADS 1024   // k_ed_fill workgroup: 8 records in flight per thread cover 8192 entries
 #define ED_INFLIGHT 8     // (16 measured slower: 8.5 vs 7.6 us at 6k entries)
@@ -1156,12 +1158,12 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
     if (sy) atomicMax(&sxy[1], sy);
     __syncthreads();
     const int nseg = nq < ED_QUEUE ? nq : ED_QUEUE;
-    for (int j = 0; j < nseg; ++j) {             // queued segments: the whole workgroup over them
+    for (int j = wv; j < nseg; j += ED_THREADS / 64) {   // queued segments: one wave each, lanes over columns
         const EdSeg g = q[j];
         if (g.lds) {
-            for (int x = g.x0 + threadIdx.x; x <= g.x1; x += ED_THREADS) { atomicMin(&lmin[x], g.zmin); atomicMax(&lmax[x], g.zmax); }
+            for (int x = g.x0 + lane; x <= g.x1; x += 64) { atomicMin(&lmin[x], g.zmin); atomicMax(&lmax[x], g.zmax); }
         } else {
-            ed_fill_global(a, g.y0, g.y1, g.x0, g.x1, g.zmin, g.zmax, threadIdx.x, ED_THREADS);
+            ed_fill_global(a, g.y0, g.y1, g.x0, g.x1, g.zmin, g.zmax, lane, 64);
         }
     }
     __syncthreads();
