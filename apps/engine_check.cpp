@@ -57,6 +57,10 @@ int main(int argc, char** argv)
     const int frames = argc > 1 ? std::atoi(argv[1]) : 40;
     const int cols = argc > 2 ? std::atoi(argv[2]) : 320;
     const int rows = argc > 3 ? std::atoi(argv[3]) : 240;
+    // "nowait": no cuda::waitAllDefaultStream() between the imgproc calls (legacy default
+    // stream) and the engines (the context's own stream): the entry points must order
+    // themselves after the caller's stream-0 work
+    const bool wait_default = !(argc > 4 && std::strcmp(argv[4], "nowait") == 0);
     cuda::setDevice(0);
 
     TopFuParams p = TopFuParams::default_params();
@@ -115,7 +119,7 @@ int main(int argc, char** argv)
         if (p.icp_truncate_depth_dist > 0) cuda::depthTruncation(curr.depth_pyr[0], p.icp_truncate_depth_dist);
         for (int l = 1; l < LEVELS; ++l) cuda::depthBuildPyramid(curr.depth_pyr[l - 1], curr.depth_pyr[l], p.bilateral_sigma_depth);
         for (int l = 0; l < LEVELS; ++l) cuda::computePointNormals(p.intr(l), curr.depth_pyr[l], curr.points_pyr[l], curr.normals_pyr[l]);
-        cuda::waitAllDefaultStream();
+        if (wait_default) cuda::waitAllDefaultStream();
         if (frame_counter == 0) {
             sceneEngine.AllocateSceneFromDepth(&scene, p.intr, poses.back(), dists, &renderState);
             sceneEngine.IntegrateIntoScene(&scene, p.intr, poses.back(), dists, &renderState);

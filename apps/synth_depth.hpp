@@ -1,6 +1,6 @@
 // synth_depth.hpp -- the synthetic C2 scene of SURVEY.md §8d for the C++ apps: an analytic room
 // (+ sphere) rendered from a camera pose, and the orbit the bench / tests use (0.25 deg per
-// frame about a pivot 1.2 m ahead).  Same geometry as topfusion_amd/synth.py (no noise).
+// frame about a pivot 1.2 m ahead, swinging +-25 deg).  Same geometry as topfusion_amd/synth.py (no noise).
 #pragma once
 #include <tfusion/types.hpp>
 
@@ -83,10 +83,20 @@ inline void render_colour(const double R[9], const double t[3], int cols, int ro
         }
 }
 
+// orbit angle of frame i in degrees: a ping-pong between -25 and +25 deg at 0.25 deg per frame
+// (synth.orbit_angle_deg), so the camera stays inside the room however long the stream is
+inline double orbit_angle_deg(int i)
+{
+    const double A = 25.0, a = 0.25 * i, ph = std::fmod(a, 4.0 * A);
+    if (ph <= A) return ph;
+    if (ph <= 3.0 * A) return 2.0 * A - ph;
+    return ph - 4.0 * A;
+}
+
 // frame i of the orbit: camera -> world rotation about y and translation
 inline void orbit_pose(int i, double R[9], double t[3])
 {
-    const double ang = 0.25 * i * M_PI / 180.0, ca = std::cos(ang), sa = std::sin(ang);
+    const double ang = orbit_angle_deg(i) * M_PI / 180.0, ca = std::cos(ang), sa = std::sin(ang);
     const double Rr[9] = { ca, 0, sa, 0, 1, 0, -sa, 0, ca };
     for (int k = 0; k < 9; ++k) R[k] = Rr[k];
     t[0] = -sa * 1.2; t[1] = 0.0; t[2] = 1.2 - ca * 1.2;      // orbit about a pivot 1.2 m ahead

@@ -150,44 +150,60 @@ def hbm_stream_copy(device, gib=1.0, reps=10):
     return 2.0 * n * 4 / (ms * 1e-3) / 1e9
 
 
-def cpu_run(frames, params_kw, n, omp):
-    """One timed run of the oracle over frames 0..n-1 from a fresh context (frame 0 takes the
-    integrate-only path, the rest track); returns seconds."""
+def cpu_run(frames, params_kw, first, n, omp, start=None):
+    """One timed run of the oracle over frames first..first+n-1: from `start`'s state (an oracle
+    context that already ran frames 0..first-1, copied in untimed) or from a fresh context;
+    returns seconds."""
     from oracle import oracle as O
     o = O.Oracle(O.default_params(**params_kw), omp=omp)
+    if start is not None:
+        o.copy_state_from(start)
     t0 = time.perf_counter()
-    for k in range(n):
+    for k in range(first, first + n):
         o(frames[k])
     return time.perf_counter() - t0
 
 
-def cpu_baseline_protocol(frames, params_kw, seconds, nt):
-    """BASELINE.md CPU protocol on the GPU box's host: for the OpenMP build (nt threads) and the
-    serial build, one warm-up run, then the median of 5 timed runs of a bounded sample of the
-    same stream (each run a fresh context over frames 0..n-1, n sized so the 5 runs take about
-    `seconds` / 2 per build); plus C1 (the frame-0 integrate-only path on frame 0, median of 5
-    after a warm-up) as ms/frame."""
+def cpu_baseline_protocol(frames, first, params_kw, seconds, nt):
+    """BASELINE.md CPU protocol on the GPU box's host, on the frames the GPU times: the OpenMP
+    build (nt threads) runs frames 0..first-1 untimed (the GPU's warm-up frames), and from a
+    copy of that state each timed run processes frames first..first+n-1 -- the first n frames of
+    the GPU's timed region, with the same scene, pose history and resets.  For the OpenMP build
+    and the serial build (from the same state): one warm-up run, then the median of 5 timed runs
+    (n sized so the 5 runs take about `seconds` / 2 per build).  Plus C1 (the frame-0
+    integrate-only path on frame 0 of a fresh context, median of 5 after a warm-up) as ms/frame."""
+    from oracle import oracle as O
+    t_w0 = time.perf_counter()
+    state = O.Oracle(O.default_params(**params_kw), omp=True)
+    for k in range(first):
+        state(frames[k])
+    t_state = time.perf_counter() - t_w0
+    avail = len(frames) - first
     res = {}
     for name, omp in (("omp", True), ("serial", False)):
-        t_warm = cpu_run(frames, params_kw, 2, omp)                 # warm-up (also sizes the sample)
+        t_warm = cpu_run(frames, params_kw, first, 2, omp, state)         # warm-up (also sizes the sample)
         per = max(t_warm / 2, 1e-3)
-        n = int(max(3, min(len(frames), seconds / 2 / 5 / per)))
-        runs = sorted(cpu_run(frames, params_kw, n, omp) for _ in range(5))
-        c1 = sorted(cpu_run(frames, params_kw, 1, omp) for _ in range(6))[1:]   # first = warm-up
+        n = int(max(3, min(avail, seconds / 2 / 5 / per)))
+        runs = sorted(cpu_run(frames, params_kw, first, n, omp, state) for _ in range(5))
+        c1 = sorted(cpu_run(frames, params_kw, 0, 1, omp) for _ in range(6))[1:]   # first = warm-up
         res[name] = {"fps": n / runs[2], "n": n, "runs_s": [round(r, 3) for r in runs],
                      "c1_ms": 1000.0 * sorted(c1)[2]}
     o, s1 = res["omp"], res["serial"]
     model, nproc = cpu_model()
     return {"value": round(o["fps"], 4), "unit": "frames/s", "cores": nt, "kind": "port",
             "sample": f"oracle (C restatement, OpenMP build: per-pixel / per-CTA / per-block loops on {nt} threads, "
-                      f"allocation serial), frames 0..{o['n'] - 1} of the same stream from a fresh context; "
-                      f"median of 5 runs after 1 warm-up ({o['runs_s']} s); host CPU of the GPU box",
+                      f"allocation serial) on frames {first}..{first + o['n'] - 1} -- the first {o['n']} frames of the "
+                      f"GPU's timed region -- from the state after frames 0..{first - 1} (run untimed by the OpenMP "
+                      f"build, {t_state:.1f} s); median of 5 runs after 1 warm-up ({o['runs_s']} s); host CPU of the "
+                      "GPU box",
+            "frames": [first, first + o["n"]],
             "c1_ms_per_frame": round(o["c1_ms"], 3),
             "single_thread": {"value": round(s1["fps"], 4), "cores": 1,
-                              "sample": f"serial oracle, frames 0..{s1['n'] - 1}, median of 5 runs after 1 warm-up "
-                                        f"({s1['runs_s']} s)",
+                              "sample": f"serial oracle, frames {first}..{first + s1['n'] - 1} from the same state, "
+                                        f"median of 5 runs after 1 warm-up ({s1['runs_s']} s)",
                               "c1_ms_per_frame": round(s1["c1_ms"], 3)},
-            "cpu_model": model, "nproc": nproc}
+            "cpu_model": model, "nproc": nproc, "affinity_cpus": len(os.sched_getaffinity(0)),
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
 def combine_ranks(elapsed, frames, device, world):
@@ -207,7 +223,9 @@ def combine_ranks(elapsed, frames, device, world):
 def c3_scene():
     """The C3 HBM-scale scene (~2 M active blocks): 2^21 - 1 voxel blocks
     (4 GiB of voxels) fill the 1280x960 frustum in layers from 0.3 m on (to ~2.8 m), every one in
-    the visible list, uploaded as the hash + visible list; dists of a wall at 1.5 m."""
+    the visible list, uploaded as a valid hash table (synth.build_hash) + visible list; dists of a
+    wall at 1.5 m.  Returns (context, params, W, H, voxel size, block count, visible ids,
+    lastFreeExcessListId)."""
     import torch
     from topfusion_amd import TopFu, default_params, synth
     from topfusion_amd import _lib as L
@@ -230,17 +248,17 @@ def c3_scene():
         z = (bz + 1) * bs + 1e-6
     pos = np.concatenate(blocks)[:nb]
     tf = TopFu(p, device=0)
-    h = np.zeros(tf.nbytes(L.TF_BUF_HASH) // HASH_DTYPE.itemsize, HASH_DTYPE)
-    h["ptr"] = -2
-    h["x"][:nb], h["y"][:nb], h["z"][:nb] = pos[:, 0], pos[:, 1], pos[:, 2]
-    h["ptr"][:nb] = np.arange(nb)
+    # a valid hash (every block at its bucket or in its bucket's excess chain, as allocation lays
+    # them out), so hash walks, the block grid and the oracle all find the same blocks
+    h, entry, last_free_excess = synth.build_hash(pos, p.n_buckets, p.n_excess, HASH_DTYPE)
+    assert len(h) == tf.nbytes(L.TF_BUF_HASH) // HASH_DTYPE.itemsize
     tf.upload(L.TF_BUF_HASH, h)
     ids = np.zeros(tf.nbytes(L.TF_BUF_VISIBLE_IDS) // 4, np.int32)
-    ids[:nb] = np.arange(nb)
+    ids[:nb] = entry                                       # visible list: the blocks, near to far
     tf.upload(L.TF_BUF_VISIBLE_IDS, ids)
-    tf.set_counters(-1, p.n_excess - 1, nb)
+    tf.set_counters(-1, last_free_excess, nb)
     tf.stage_preprocess(np.full((H, W), 1500, np.uint16))   # dists of a wall at 1.5 m
-    return tf, p, W, H, vox, nb
+    return tf, p, W, H, vox, nb, entry, last_free_excess
 
 
 def _pmc(config, stage):
@@ -261,7 +279,7 @@ def c3_integrate(args):
     update: a depth and eta >= -mu) and per lane written (those that changed), counted on the
     device; the reference's pass reads and writes every voxel (Nvis x 4096 B), reported beside
     as the reference-equivalent rate."""
-    tf, p, W, H, vox, nb = c3_scene()
+    tf, p, W, H, vox, nb = c3_scene()[:6]
     I = np.eye(4, dtype=np.float32)[:3]
     tf.time_stage("integrate", I, 2)                        # warm-up
     tf.reset_totals()
@@ -299,7 +317,7 @@ def c3_raycast(args):
     image + 4 grey image) + 2 x B x 2064, B = the blocks the ICP-map raycast reads (its
     castRay<true> visibility marks, counted after the run)."""
     from topfusion_amd import _lib as L
-    tf, p, W, H, vox, nb = c3_scene()
+    tf, p, W, H, vox, nb = c3_scene()[:6]
     I = np.eye(4, dtype=np.float32)[:3]
     tf.time_stage("integrate", I, 4)                        # the surface at 1.5 m
     rng = np.empty((H, W, 2), np.float32)
@@ -333,14 +351,16 @@ def c3_raycast(args):
 
 def orbit_frames(n, W, H, seed, device):
     """C2/C3 input: n frames of the synthetic orbit (room + sphere, 0.25 deg per frame
-    around a pivot 1.2 m ahead, 1 mm noise), rendered on the GPU in batches straight into HBM
-    (synth.render_depth_torch -- the host renderer's geometry, torch's noise generator)."""
+    around a pivot 1.2 m ahead, swinging +-25 deg so the camera stays inside the room for any n;
+    1 mm noise), rendered on the GPU in batches straight into HBM (synth.render_depth_torch -- the
+    host renderer's geometry, torch's noise generator)."""
     import torch
     from topfusion_amd import synth
     R = np.empty((n, 3, 3))
     t = np.empty((n, 3))
     for k in range(n):
         R[k], t[k] = synth.orbit_pose(k)
+        assert synth.orbit_in_room(R[k], t[k]), f"orbit frame {k}: camera outside the room"
     dev = torch.empty((n, H, W), dtype=torch.int16, device=device)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
@@ -569,9 +589,10 @@ def main():
             # all cores: the OpenMP build of the oracle; 1 thread: the serial build (reported
             # beside); BASELINE.md protocol: one warm-up frame, then the median of 5 repeats of a
             # bounded sample of the same stream
-            frames = dev[:min(n_frames, 64)].cpu().numpy().view(np.uint16)
+            first = args.warmup * F
+            frames = dev[:min(n_frames, first + 128)].cpu().numpy().view(np.uint16)
             nt = omp_threads()
-            cpu = cpu_baseline_protocol(frames, pkw, args.cpu_seconds, nt)
+            cpu = cpu_baseline_protocol(frames, first, pkw, args.cpu_seconds, nt)
         out = {
             "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame"
                       + (" (swapping scene)" if args.swapping else ""),
@@ -611,6 +632,13 @@ def main():
             "frames_ok": int(ok.sum()), "resets": int(tot["resets"]),
             "ok_frames_per_sec": round(int(ok.sum()) * (total_frames / total_steps_frames) / elapsed_max, 2),
             "visible_blocks_mean": round(nvis_mean, 1),
+            "visible_blocks_mean_is": "visible-list length per frame that integrated (tracked frames and frame-0 "
+                                      "frames after a reset), timed region",
+            "workload_check": None if cfg["walk"] else {
+                "camera_inside_room": "every generated frame (asserted in orbit_frames, >= 0.2 m from every wall)",
+                "orbit_deg_timed": [round(min(synth.orbit_angle_deg(k) for k in range(args.warmup * F, n_frames)), 2),
+                                    round(max(synth.orbit_angle_deg(k) for k in range(args.warmup * F, n_frames)), 2)],
+                "timed_frames": [args.warmup * F, n_frames]},
             "render_tiles_mean": round(tot["tiles_sum"] / max(1, tot["frames_tracked"]), 1),
             "visible_blocks_last": st["noVisibleEntries"],
             "allocated_blocks_last": int(tf.params().n_blocks - 1 - st["lastFreeBlockId"]),

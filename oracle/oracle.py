@@ -82,8 +82,10 @@ def lib(omp=False):
         L.tfo_create.argtypes = [ctypes.POINTER(Params)]; L.tfo_create.restype = P
         L.tfo_destroy.argtypes = [P]
         L.tfo_reset.argtypes = [P]
+        L.tfo_copy_state.argtypes = [P, P]; L.tfo_copy_state.restype = ctypes.c_int
         L.tfo_process_frame.argtypes = [P, P]; L.tfo_process_frame.restype = ctypes.c_int
         L.tfo_get_counters.argtypes = [P, ctypes.POINTER(Counters)]
+        L.tfo_set_counters.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.tfo_get_pose.argtypes = [P, P]
         L.tfo_alloc.argtypes = [P, P, P]
         L.tfo_alloc_ex.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int]
@@ -267,6 +269,10 @@ class Oracle:
     def reset(self):
         self.L.tfo_reset(self.ctx)
 
+    def copy_state_from(self, other):
+        """This context's whole state := other's (same params; either build may be the source)."""
+        assert self.L.tfo_copy_state(self.ctx, other.ctx) == 0, "tfo_copy_state: params differ"
+
     def counters(self):
         c = Counters()
         self.L.tfo_get_counters(self.ctx, ctypes.byref(c))
@@ -284,6 +290,20 @@ class Oracle:
 
     def hash(self):
         return self._view(self.L.tfo_hash(self.ctx), HASH_DTYPE, self.n_total).copy()
+
+    def upload_hash(self, h):
+        """Write a whole hash table (HASH_DTYPE, n_total entries) into the context."""
+        h = np.ascontiguousarray(h, HASH_DTYPE)
+        assert h.shape == (self.n_total,)
+        self._view(self.L.tfo_hash(self.ctx), HASH_DTYPE, self.n_total)[:] = h
+
+    def upload_visible_ids(self, ids):
+        ids = np.ascontiguousarray(ids, np.int32)
+        assert ids.size <= self.params.vis_capacity
+        self._view(self.L.tfo_visible_ids(self.ctx), np.int32, self.params.vis_capacity)[:ids.size] = ids
+
+    def set_counters(self, lastFreeBlockId, lastFreeExcessListId, noVisibleEntries):
+        self.L.tfo_set_counters(self.ctx, lastFreeBlockId, lastFreeExcessListId, noVisibleEntries)
 
     def vba(self):
         return self._view(self.L.tfo_vba(self.ctx), VOXEL_DTYPE, self.params.n_blocks * 512).copy()

@@ -638,6 +638,49 @@ void tfo_destroy(tfo_ctx* c)
     free(c);
 }
 
+/* Deep copy of a context's whole state (scene, render state, pyramids, pose, counters) into
+   another created with the same params: a benchmark sample starts at frame k of a stream
+   without re-running frames 0..k-1.  Not a reference function.  The serial and OpenMP builds
+   compile this same struct, so one build's context may be the source of the other's copy. */
+int tfo_copy_state(tfo_ctx* d, const tfo_ctx* s)
+{
+    if (!d || !s || memcmp(&d->p, &s->p, sizeof(tfo_params)) != 0) return -1;
+    const size_t nt = (size_t)s->n_total, nb = (size_t)s->p.n_blocks, npx = (size_t)s->p.cols * s->p.rows;
+    memcpy(d->hash, s->hash, sizeof(tfo_hash_entry) * nt);
+    memcpy(d->excessList, s->excessList, sizeof(int) * (size_t)s->p.n_excess);
+    memcpy(d->vba, s->vba, sizeof(tfo_voxel) * nb * BLK3);
+    memcpy(d->allocList, s->allocList, sizeof(int) * nb);
+    memcpy(d->allocType, s->allocType, nt);
+    memcpy(d->blockCoords, s->blockCoords, sizeof(int16_t) * nt * 4);
+    memcpy(d->visibleIds, s->visibleIds, sizeof(int) * (size_t)s->p.vis_capacity);
+    memcpy(d->visType, s->visType, nt);
+    memcpy(d->range, s->range, sizeof(float) * 2 * npx);
+    memcpy(d->raycast, s->raycast, sizeof(float) * 4 * npx);
+    memcpy(d->dists, s->dists, sizeof(float) * npx);
+    memcpy(d->frame_grey, s->frame_grey, 4 * npx);
+    for (int l = 0; l < 3; ++l) {
+        const size_t n = (size_t)s->lvl_w[l] * s->lvl_h[l];
+        memcpy(d->depth_pyr[l], s->depth_pyr[l], sizeof(uint16_t) * n);
+        memcpy(d->curr_pts[l], s->curr_pts[l], sizeof(float) * 4 * n);
+        memcpy(d->curr_nrm[l], s->curr_nrm[l], sizeof(float) * 4 * n);
+        memcpy(d->prev_pts[l], s->prev_pts[l], sizeof(float) * 4 * n);
+        memcpy(d->prev_nrm[l], s->prev_nrm[l], sizeof(float) * 4 * n);
+    }
+    if (s->p.use_swapping) {
+        memcpy(d->swapState, s->swapState, nt);
+        memcpy(d->hasStored, s->hasStored, nt);
+        memcpy(d->stored, s->stored, sizeof(tfo_voxel) * nt * BLK3);
+    }
+    if (s->p.voxel_rgb) memcpy(d->vba_rgb, s->vba_rgb, sizeof(uint32_t) * nb * BLK3);
+    d->lastFreeBlockId = s->lastFreeBlockId; d->lastFreeExcessListId = s->lastFreeExcessListId;
+    d->noVisibleEntries = s->noVisibleEntries; d->noTotalBlocks = s->noTotalBlocks;
+    d->frame_counter = s->frame_counter;
+    memcpy(d->pose, s->pose, sizeof(d->pose));
+    d->icp_iterations = s->icp_iterations; d->icp_ok = s->icp_ok; d->n_resets = s->n_resets;
+    memcpy(d->swap_counts, s->swap_counts, sizeof(d->swap_counts));
+    return 0;
+}
+
 void tfo_reset(tfo_ctx* c)
 {   /* TopFu::reset, topfu.cpp:141-152 (render state is NOT cleared) */
     if (c->frame_counter) c->n_resets++;
@@ -1730,6 +1773,14 @@ void tfo_get_counters(const tfo_ctx* c, tfo_counters* o)
 }
 
 void tfo_get_pose(const tfo_ctx* c, float rt[12]) { memcpy(rt, c->pose, sizeof(float) * 12); }
+
+/* the counters of a scene written in place (tfo_hash / tfo_visible_ids), as tf_set_counters */
+void tfo_set_counters(tfo_ctx* c, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries)
+{
+    c->lastFreeBlockId = lastFreeBlockId;
+    c->lastFreeExcessListId = lastFreeExcessListId;
+    c->noVisibleEntries = noVisibleEntries;
+}
 tfo_hash_entry* tfo_hash(tfo_ctx* c) { return c->hash; }
 tfo_voxel* tfo_vba(tfo_ctx* c) { return c->vba; }
 uint32_t* tfo_vba_rgb(tfo_ctx* c) { return c->vba_rgb; }

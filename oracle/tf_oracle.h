@@ -130,11 +130,13 @@ typedef struct tfo_ctx tfo_ctx;
 tfo_ctx* tfo_create(const tfo_params* p);
 void tfo_destroy(tfo_ctx* c);
 void tfo_reset(tfo_ctx* c);                                   /* TopFu::reset */
+int tfo_copy_state(tfo_ctx* dst, const tfo_ctx* src);        /* whole state, same params (bench samples) */
 int  tfo_process_frame(tfo_ctx* c, const uint16_t* depth);    /* TopFu::operator() */
 /* TopFu::operator()(depth, image): the frame's uchar4 RGB image (pitch bytes per row, 0: cols * 4)
    integrated into the Voxel_s_rgb colour (voxel_rgb) */
 int  tfo_process_frame_rgb(tfo_ctx* c, const uint16_t* depth, const uint8_t* rgb, size_t pitch);
 void tfo_get_counters(const tfo_ctx* c, tfo_counters* out);
+void tfo_set_counters(tfo_ctx* c, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries);
 void tfo_get_pose(const tfo_ctx* c, float rt[12]);            /* getCameraPose(): [R|t] row-major */
 /* stage-level entry points on the context */
 void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists);      /* AllocateSceneFromDepth */

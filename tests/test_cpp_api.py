@@ -83,13 +83,17 @@ def test_colour_api_matches_topfu():
 
 
 @pytest.mark.gpu
-def test_engine_api_matches_topfu():
+@pytest.mark.parametrize("wait", ["wait", "nowait"])
+def test_engine_api_matches_topfu(wait):
     """apps/engine_check: TopFu::operator() against the same frames spelled out over the L4
     engine API (imgproc functions, a stand-alone ProjectiveICP, the reconstruction and
     visualisation engines) -- bool, pose, counters and renderImage bit-exact every frame, ICP
-    maps at the end; 40 frames include ICP-failure resets."""
+    maps at the end; 40 frames include ICP-failure resets.  "nowait" leaves out the
+    cuda::waitAllDefaultStream() between the imgproc calls (asynchronous, legacy default
+    stream) and the engines: AllocateSceneFromDepth right after computeDists, estimateTransform
+    right after computePointNormals -- the entry points order themselves after stream 0."""
     exe = _build("engine_check")
-    r = subprocess.run([exe, "40", "320", "240"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe, "40", "320", "240", wait], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     m = re.search(r"engine_check frames (\d+) ok (\d+) resets (\d+): MATCH", r.stdout)
     assert m and int(m.group(1)) == 40 and int(m.group(3)) >= 1, r.stdout

@@ -149,6 +149,7 @@ static void ctx_free(tf_ctx* c)
         icp_order_register(c, -1);
         (void)hipEventDestroy(c->icp_ev);
     }
+    if (c->caller_ev) (void)hipEventDestroy(c->caller_ev);
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
@@ -227,6 +228,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     c->dist2_thres = pin->icp_dist_thres * pin->icp_dist_thres;
 #define ALLOC(ptr, bytes) do { e = dalloc(&(ptr), (bytes)); if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); } } while (0)
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->caller_ev, hipEventDisableTiming);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     ALLOC(c->hash, sizeof(TfHashEntry) * (size_t)c->n_total);
     ALLOC(c->excessList, sizeof(int) * (size_t)pin->n_excess);
@@ -936,6 +938,17 @@ extern "C" tf_status tf_icp_get_params(tf_ctx* c, float* dist_thres, float* angl
     return TF_OK;
 }
 
+// The context stream is non-blocking, so it does not wait for the legacy default stream on
+// which the reference-shaped callers produce their inputs (cuda:: imgproc wrappers with
+// stream 0, asynchronous uploads): in the reference everything runs on the default stream and
+// that order is implicit.  Entry points that read caller device buffers therefore make the
+// context stream wait for all work already enqueued on stream 0 before their first read.
+static hipError_t order_after_caller(tf_ctx* c)
+{
+    hipError_t e = hipEventRecord(c->caller_ev, nullptr);
+    return e == hipSuccess ? hipStreamWaitEvent(c->stream, c->caller_ev, 0) : e;
+}
+
 // caller pitched float4 map -> the context's packed level buffer
 static hipError_t copy_map_in(tf_ctx* c, float4* dst, int l, const void* src, size_t step)
 {
@@ -952,6 +965,7 @@ extern "C" tf_status tf_icp_estimate(tf_ctx* c, const float intr[4], const tf_ma
     if (used > levels) return TF_INVALID_ARG;
     for (int l = 0; l < levels; ++l)
         if (!curr[l].points || !curr[l].normals || !prev[l].points || !prev[l].normals) return TF_INVALID_ARG;
+    TF_CHECK(order_after_caller(c));
     for (int l = 0; l < levels; ++l) {
         TF_CHECK(copy_map_in(c, c->curr_pts[l], l, curr[l].points, curr[l].points_step));
         TF_CHECK(copy_map_in(c, c->curr_nrm[l], l, curr[l].normals, curr[l].normals_step));
@@ -973,6 +987,7 @@ extern "C" tf_status tf_scene_alloc(tf_ctx* c, const float intr[4], const float 
                                    size_t dists_step, int only_update_visible_list, int reset_visible_list)
 {
     if (!c || !pose_rt || !dists) return TF_INVALID_ARG;
+    TF_CHECK(order_after_caller(c));
     TF_CHECK(copy_dists_in(c, dists, dists_step));
     IntrScope is(c, intr);
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
@@ -991,6 +1006,7 @@ extern "C" tf_status tf_scene_integrate(tf_ctx* c, const float intr[4], const fl
                                        size_t dists_step)
 {
     if (!c || !pose_rt || !dists) return TF_INVALID_ARG;
+    TF_CHECK(order_after_caller(c));
     TF_CHECK(copy_dists_in(c, dists, dists_step));
     IntrScope is(c, intr);
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
@@ -1091,6 +1107,7 @@ extern "C" tf_status tf_vis_render_image(tf_ctx* c, const float intr[4], const f
     if (new_raycast) TF_CHECK(tfk_raycast(c, 0));        // RENDER_FROM_NEW_RAYCAST (VisualisationEngine_CUDA.cu:227-240)
     TF_CHECK(tfk_render_type(c, type));
     if (dev_rgba) {
+        TF_CHECK(order_after_caller(c));                  // the caller may still read the image on stream 0
         const size_t row = (size_t)c->W * 4;
         TF_CHECK(hipMemcpy2DAsync(dev_rgba, step ? step : row, c->grey, row, row, c->H, hipMemcpyDeviceToDevice, c->stream));
     }
@@ -1108,6 +1125,7 @@ extern "C" tf_status tf_vis_icp_maps(tf_ctx* c, const float intr[4], const float
     TF_CHECK(tfk_raycast(c, 1));                          // castRay<true> (VisualisationEngine_CUDA.cu:340-345)
     TF_CHECK(tfk_icp_maps(c));                            // renderICP (:347-359) + the context's resized levels
     const size_t row = sizeof(float4) * (size_t)c->W;
+    if (points || normals) TF_CHECK(order_after_caller(c));
     if (points)
         TF_CHECK(hipMemcpy2DAsync(points, points_step ? points_step : row, c->prev_pts[0], row, row, c->H,
                                   hipMemcpyDeviceToDevice, c->stream));

@@ -341,6 +341,9 @@ struct tf_ctx {
     hipEvent_t ev_start, ev_stop;
     // persistent-ICP ordering among the contexts of one device (tf_icp_order_*, tf_capi.hip)
     hipEvent_t icp_ev;
+    // engine entry points over caller buffers: orders the context stream after the legacy
+    // default stream the caller's producers (cuda:: imgproc, uploads) run on (order_after_caller)
+    hipEvent_t caller_ev;
     double prof_ms[TF_NUM_STAGES];
     long long prof_count[TF_NUM_STAGES];
 };

@@ -7,8 +7,9 @@ apps/demo.cpp:93-97), so every workload is rendered analytically:
   down), left wall x = -0.8 m; pose = identity; optional 1 mm noise and 1 %
   holes (seed 42).
 * C2  orbit: the camera starts at the identity and orbits a pivot 1.2 m ahead
-  about the vertical axis at 0.25 deg/frame (~5 mm/frame); room + sphere
-  r = 0.3 m (seed 7 + stream index).
+  about the vertical axis at 0.25 deg/frame (~5 mm/frame), swinging +-25 deg so it
+  stays inside the room for any stream length; room + sphere r = 0.3 m (seed 7 +
+  stream index).
 * C3  1280x960 with intrinsics x2, same scene.
 
 Depth is uint16 millimetres (the reference's cuda::Depth, types.hpp:62).
@@ -113,13 +114,46 @@ def room_corner(cols=640, rows=480, noise_mm=1.0, holes=0.01, seed=42):
     return render_depth(np.eye(3), np.zeros(3), cols, rows, sphere=False, noise_mm=noise_mm, holes=holes, seed=seed)
 
 
-def orbit_pose(k, deg_per_frame=0.25, pivot_dist=1.2):
-    """Ground-truth camera->world pose of frame k of the C2 orbit."""
-    a = np.deg2rad(deg_per_frame * k)
+ORBIT_AMPLITUDE_DEG = 25.0
+# the walls of render_depth's room (x, y, z extents); the sphere sits inside
+ROOM_WALLS_LO = np.array([-0.8, -0.9, -0.6])
+ROOM_WALLS_HI = np.array([1.1, 0.6, 1.8])
+
+
+def orbit_angle_deg(k, deg_per_frame=0.25, amplitude_deg=ORBIT_AMPLITUDE_DEG):
+    """Orbit angle of frame k: a ping-pong (triangle wave) at deg_per_frame between
+    -amplitude and +amplitude, starting at 0 and swinging to +amplitude first.  The first
+    amplitude/deg_per_frame frames equal a plain orbit, and the camera never
+    leaves the room however long the stream is (a plain orbit at 0.25 deg/frame crosses the
+    left wall at 42 deg, frame 168).  amplitude_deg=None gives the plain, unbounded orbit."""
+    if amplitude_deg is None:
+        return deg_per_frame * k
+    a = deg_per_frame * k
+    period = 4.0 * amplitude_deg
+    ph = a % period
+    if ph <= amplitude_deg:
+        return ph
+    if ph <= 3.0 * amplitude_deg:
+        return 2.0 * amplitude_deg - ph
+    return ph - period
+
+
+def orbit_pose(k, deg_per_frame=0.25, pivot_dist=1.2, amplitude_deg=ORBIT_AMPLITUDE_DEG):
+    """Ground-truth camera->world pose of frame k of the C2 orbit: a rotation about the vertical
+    axis through a pivot pivot_dist ahead of the start (0.25 deg ~ 5 mm per frame), swinging
+    +-amplitude_deg (orbit_angle_deg).  With the defaults the camera centre stays >= 0.29 m
+    inside every wall (orbit_in_room)."""
+    a = np.deg2rad(orbit_angle_deg(k, deg_per_frame, amplitude_deg))
     R = _rot_y(a)
     pivot = np.array([0.0, 0.0, pivot_dist])
     t = pivot - R @ pivot
     return R, t
+
+
+def orbit_in_room(R, t, margin=0.2):
+    """True if the camera centre t lies inside the room's walls with `margin` metres to spare."""
+    t = np.asarray(t, np.float64)
+    return bool(np.all(t > ROOM_WALLS_LO + margin) and np.all(t < ROOM_WALLS_HI - margin))
 
 
 def orbit_sequence(n, cols=640, rows=480, seed=7, noise_mm=1.0, holes=0.0, deg_per_frame=0.25):
@@ -127,6 +161,7 @@ def orbit_sequence(n, cols=640, rows=480, seed=7, noise_mm=1.0, holes=0.0, deg_p
     out = np.empty((n, rows, cols), np.uint16)
     for k in range(n):
         R, t = orbit_pose(k, deg_per_frame)
+        assert orbit_in_room(R, t), f"orbit frame {k}: camera outside the room"
         out[k] = render_depth(R, t, cols, rows, sphere=True, noise_mm=noise_mm, holes=holes, seed=seed * 100003 + k)
     return out
 
@@ -205,3 +240,56 @@ def render_depth_torch(R, t, cols=640, rows=480, noise_mm=1.0, generator=None, d
         mm = mm + noise_mm * torch.randn(mm.shape, dtype=torch.float64, device=device, generator=generator)
     mm = torch.where(torch.isfinite(mm), torch.round(mm), torch.zeros_like(mm))
     return torch.clamp(mm, 0, 65535).to(torch.int32).to(torch.int16)
+
+
+# ----------------------------------------------------------------------------------------
+# A voxel-block hash built directly from a list of block positions (the C3 HBM-scale scene)
+# ----------------------------------------------------------------------------------------
+def hash_index(x, y, z, n_buckets):
+    """hashIndex (VoxelBlockHash.hpp / tf_internal.h): ((x*73856093) ^ (y*19349669) ^
+    (z*83492791)) & (n_buckets - 1) in uint32 arithmetic, vectorised."""
+    x = np.asarray(x).astype(np.int64).astype(np.uint32)
+    y = np.asarray(y).astype(np.int64).astype(np.uint32)
+    z = np.asarray(z).astype(np.int64).astype(np.uint32)
+    with np.errstate(over="ignore"):
+        h = (x * np.uint32(73856093)) ^ (y * np.uint32(19349669)) ^ (z * np.uint32(83492791))
+    return (h & np.uint32(n_buckets - 1)).astype(np.int64)
+
+
+def build_hash(pos, n_buckets, n_excess, dtype):
+    """A valid hash table holding the blocks `pos` (int (n, 3)), as the reference's allocation
+    would lay them out (SceneReconstructionEngine_host.cu allocateVoxelBlocksList): the first
+    block of a bucket in the bucket entry, the others in excess entries taken from the top of
+    the excess free list (excessList[lastFreeExcessListId--]) and chained through `offset`
+    (excess id + 1); block i gets VBA block ptr i.  Returns (hash, entry index of each block,
+    lastFreeExcessListId)."""
+    pos = np.asarray(pos, np.int64)
+    n = len(pos)
+    hidx = hash_index(pos[:, 0], pos[:, 1], pos[:, 2], n_buckets)
+    order = np.lexsort((np.arange(n), hidx))            # by bucket, then by block index
+    hs = hidx[order]
+    first = np.ones(n, bool)
+    first[1:] = hs[1:] != hs[:-1]
+    n_ex = int((~first).sum())
+    if n_ex > n_excess:
+        raise ValueError(f"{n_ex} colliding blocks exceed the {n_excess}-entry excess list")
+    ex_id = np.full(n, -1, np.int64)
+    ex_id[~first] = n_excess - 1 - np.arange(n_ex)
+    entry_sorted = np.where(first, hs, n_buckets + ex_id)
+    # offset of each entry: the next block of the same bucket's excess id + 1, else 0
+    nxt = np.zeros(n, np.int64)
+    same_next = np.zeros(n, bool)
+    same_next[:-1] = ~first[1:]
+    nxt[:-1] = ex_id[1:] + 1
+    offset_sorted = np.where(same_next, nxt, 0)
+    h = np.zeros(n_buckets + n_excess, dtype)
+    h["ptr"] = -2
+    blk = order
+    h["x"][entry_sorted] = pos[blk, 0]
+    h["y"][entry_sorted] = pos[blk, 1]
+    h["z"][entry_sorted] = pos[blk, 2]
+    h["offset"][entry_sorted] = offset_sorted
+    h["ptr"][entry_sorted] = blk
+    entry = np.empty(n, np.int64)
+    entry[blk] = entry_sorted
+    return h, entry.astype(np.int32), n_excess - 1 - n_ex
