@@ -644,7 +644,11 @@ def main():
             "allocated_blocks_last": int(tf.params().n_blocks - 1 - st["lastFreeBlockId"]),
             "last_frame_ok": bool(ok[-1]),
             "swapped_out_per_frame": round(tot["swapped_out"] / max(1, tot["frames"]), 2) if args.swapping else None,
-            "swapped_in_per_frame": round(tot["swapped_in"] / max(1, tot["frames"]), 2) if args.swapping else None,
+            "swapped_in_merged_per_frame": round(tot["swapped_in_merged"] / max(1, tot["frames"]), 2) if args.swapping else None,
+            "swap_state_1to2_per_frame": round(tot["swapped_in"] / max(1, tot["frames"]), 2) if args.swapping else None,
+            "swap_counts_are": ("swapped_out: blocks copied VBA -> GlobalCache and freed; swapped_in_merged: GlobalCache "
+                                "-> VBA merges of stored blocks; swap_state_1to2: IntegrateGlobalIntoLocal state "
+                                "transitions, most of them new blocks with nothing stored") if args.swapping else None,
             "roofline": roof,
             "hbm_stream_copy_GBs": stream_gbs,
             "roofline_stages": roof_all,

@@ -332,10 +332,12 @@ typedef struct tf_totals {
     long long resets;               /* ICP failures -> reset (topfu.cpp:263-264) */
     long long visible_sum;          /* noVisibleEntries summed over the frames that integrated */
     long long tiles_sum;            /* noTotalBlocks summed over the tracked frames */
-    long long swapped_in;           /* blocks swapped in (use_swapping) */
-    long long swapped_out;          /* blocks swapped out (use_swapping) */
+    long long swapped_in;           /* swap-ins (use_swapping): state-1 entries with a block set to state 2,
+                                       whether or not the GlobalCache held data for them */
+    long long swapped_out;          /* blocks swapped out: each one copied VBA -> GlobalCache and freed */
     long long integrate_lanes_read;     /* 16-B voxel lanes (4 voxels) integration read: those with an update */
     long long integrate_lanes_written;  /* ... and wrote back: those whose value changed */
+    long long swapped_in_merged;    /* the swap-ins whose entry held stored data: GlobalCache -> VBA transfers */
 } tf_totals;
 tf_status tf_get_totals(tf_ctx* ctx, tf_totals* totals);
 tf_status tf_reset_totals(tf_ctx* ctx);

@@ -82,6 +82,8 @@ def lib(omp=False):
         L.tfo_create.argtypes = [ctypes.POINTER(Params)]; L.tfo_create.restype = P
         L.tfo_destroy.argtypes = [P]
         L.tfo_reset.argtypes = [P]
+        L.tfo_reset_scene.argtypes = [P]
+        L.tfo_swap_merged_total.argtypes = [P]; L.tfo_swap_merged_total.restype = ctypes.c_longlong
         L.tfo_copy_state.argtypes = [P, P]; L.tfo_copy_state.restype = ctypes.c_int
         L.tfo_process_frame.argtypes = [P, P]; L.tfo_process_frame.restype = ctypes.c_int
         L.tfo_get_counters.argtypes = [P, ctypes.POINTER(Counters)]
@@ -268,6 +270,14 @@ class Oracle:
 
     def reset(self):
         self.L.tfo_reset(self.ctx)
+
+    def swap_merged_total(self):
+        """Swap-ins that merged stored data (GlobalCache -> VBA transfers) since creation."""
+        return int(self.L.tfo_swap_merged_total(self.ctx))
+
+    def reset_scene(self):
+        """SceneReconstructionEngine::ResetScene (the GlobalCache stays)."""
+        self.L.tfo_reset_scene(self.ctx)
 
     def copy_state_from(self, other):
         """This context's whole state := other's (same params; either build may be the source)."""

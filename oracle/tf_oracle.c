@@ -556,6 +556,7 @@ struct tfo_ctx {
     uint8_t* hasStored;       /* hasStoredData */
     tfo_voxel* stored;        /* storedVoxelBlocks, 512 voxels per entry */
     int swap_counts[3];       /* last frame: swapped in, swapped out, reallocated */
+    long long swap_merged_total;  /* swap-ins that merged stored data (GlobalCache -> VBA), since creation */
     /* colour (voxel_rgb): Voxel_s_rgb's clr + w_color per voxel, r | g << 8 | b << 16 | w << 24,
        beside the Voxel_s plane (VoxelTypes.hpp:39-67); the frame's RGB image while integrating */
     uint32_t* vba_rgb;
@@ -565,8 +566,9 @@ struct tfo_ctx {
 
 static const float k_identity_rt[12] = { 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0 };
 
-/* ResetScene, SceneReconstructionEngine_host.cu:51-73 */
-static void reset_scene(tfo_ctx* c)
+/* ResetScene, SceneReconstructionEngine_host.cu:51-73; clear_cache: the TopFu-level resets also
+   empty the GlobalCache (see below), the engine's ResetScene (tfo_reset_scene) keeps it */
+static void reset_scene_ex(tfo_ctx* c, int clear_cache)
 {
     for (size_t i = 0; i < (size_t)c->p.n_blocks * BLK3; ++i) { c->vba[i].sdf = 32767; c->vba[i].w = 0; c->vba[i].pad = 0; }
     for (int i = 0; i < c->p.n_blocks; ++i) c->allocList[i] = i;
@@ -575,15 +577,23 @@ static void reset_scene(tfo_ctx* c)
     for (int i = 0; i < c->n_total; ++i) c->hash[i].ptr = -2;
     for (int i = 0; i < c->p.n_excess; ++i) c->excessList[i] = i;
     c->lastFreeExcessListId = c->p.n_excess - 1;
-    /* the reference's ResetScene leaves a GlobalCache alone (its swapping is never enabled);
-       here a reset also empties it, so no block of the old scene is swapped into the new one */
+    /* the reference's ResetScene leaves a GlobalCache alone (its swapping is never enabled), and so
+       does tfo_reset_scene; the TopFu-level resets (construction, TopFu::reset, the ICP-failure
+       reset) also empty it, so no block of the old scene is swapped into the new one */
     if (c->vba_rgb) memset(c->vba_rgb, 0, sizeof(uint32_t) * (size_t)c->p.n_blocks * BLK3);   /* Voxel_s_rgb(): clr 0, w 0 */
     memset(c->swap_counts, 0, sizeof(c->swap_counts));   /* a reset transfers nothing */
-    if (c->p.use_swapping) {
+    if (c->p.use_swapping && clear_cache) {
         memset(c->swapState, 0, (size_t)c->n_total);
         memset(c->hasStored, 0, (size_t)c->n_total);
     }
 }
+
+static void reset_scene(tfo_ctx* c) { reset_scene_ex(c, 1); }
+
+/* SceneReconstructionEngine::ResetScene as an engine call: the GlobalCache stays */
+void tfo_reset_scene(tfo_ctx* c) { reset_scene_ex(c, 0); }
+
+long long tfo_swap_merged_total(const tfo_ctx* c) { return c->swap_merged_total; }
 
 tfo_ctx* tfo_create(const tfo_params* p)
 {
@@ -678,6 +688,7 @@ int tfo_copy_state(tfo_ctx* d, const tfo_ctx* s)
     memcpy(d->pose, s->pose, sizeof(d->pose));
     d->icp_iterations = s->icp_iterations; d->icp_ok = s->icp_ok; d->n_resets = s->n_resets;
     memcpy(d->swap_counts, s->swap_counts, sizeof(d->swap_counts));
+    d->swap_merged_total = s->swap_merged_total;
     return 0;
 }
 
@@ -975,6 +986,7 @@ void tfo_swap_in(tfo_ctx* c)                                            /* Integ
             tfo_voxel* dst = c->vba + (size_t)c->hash[t].ptr * BLK3;
             const tfo_voxel* src = c->stored + (size_t)t * BLK3;
             for (int v = 0; v < BLK3; ++v) combine_voxel(&src[v], &dst[v], c->p.maxW);
+            c->swap_merged_total++;
         }
         c->swapState[t] = 2;
         n_in++;

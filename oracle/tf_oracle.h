@@ -139,6 +139,7 @@ void tfo_get_counters(const tfo_ctx* c, tfo_counters* out);
 void tfo_set_counters(tfo_ctx* c, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries);
 void tfo_get_pose(const tfo_ctx* c, float rt[12]);            /* getCameraPose(): [R|t] row-major */
 /* stage-level entry points on the context */
+void tfo_reset_scene(tfo_ctx* c);                                             /* ResetScene (keeps the GlobalCache) */
 void tfo_alloc(tfo_ctx* c, const float pose_rt[12], const float* dists);      /* AllocateSceneFromDepth */
 void tfo_alloc_ex(tfo_ctx* c, const float pose_rt[12], const float* dists, int only_update_visible, int reset_visible);
 void tfo_integrate(tfo_ctx* c, const float pose_rt[12], const float* dists);  /* IntegrateIntoScene */
@@ -154,6 +155,7 @@ void tfo_render_image(tfo_ctx* c, uint8_t* rgba);                              /
 void tfo_swap(tfo_ctx* c);                          /* IntegrateGlobalIntoLocal + SaveToGlobalMemory */
 void tfo_swap_in(tfo_ctx* c);                       /* IntegrateGlobalIntoLocal */
 void tfo_swap_out(tfo_ctx* c);                      /* SaveToGlobalMemory */
+long long tfo_swap_merged_total(const tfo_ctx* c);  /* swap-ins that merged stored data, since creation */
 void tfo_swap_counts(const tfo_ctx* c, int out[3]);  /* last frame: swapped in, swapped out, reallocated */
 uint8_t* tfo_swap_state(tfo_ctx* c);                /* HashSwapState::state per entry */
 uint8_t* tfo_swap_stored_flags(tfo_ctx* c);         /* GlobalCache hasStoredData per entry */

@@ -103,5 +103,6 @@ def test_c5_bench_frames_640x480(oracle_mod, swapping):
     if swapping:
         assert swapped_out > 0                          # blocks left the enlarged frustum and were evicted
         assert g.totals()["swapped_out"] == swapped_out
+        assert g.totals()["swapped_in_merged"] == o.swap_merged_total()
     g.close()
     del dev

@@ -226,4 +226,30 @@ def test_swapping_c5_random_walk(oracle_mod):
     assert outs > 0 and o.counters()["n_resets"] >= 1
     tg = g.totals()
     assert tg["swapped_out"] == outs, (tg, outs)
+    assert tg["swapped_in_merged"] == o.swap_merged_total(), (tg, o.swap_merged_total())
+    g.close()
+
+
+def test_engine_reset_scene_keeps_global_cache(oracle_mod):
+    """SceneReconstructionEngine::ResetScene (SceneReconstructionEngine_host.cu:51-73) clears the
+    hash, the VBA and the free lists but leaves the GlobalCache alone, as the reference's does
+    (the TopFu-level resets -- construction, TopFu::reset, the ICP-failure reset -- empty it so no
+    block of the old scene is swapped into the new one).  After evictions, the engine reset keeps
+    every stored flag and block, bit-exact with the oracle, and the frames after it still match."""
+    W, H = 320, 240
+    g, o = _pair(oracle_mod, W, H, voxelSize=0.01, n_blocks=2048, swap_transfer_blocks=256,
+                 n_buckets=0x10000, n_excess=0x4000)
+    seq = synth.random_walk_sequence(22, W, H, seed=13)
+    for k in range(16):
+        assert g(seq[k]) == o(seq[k]), k
+    stored_before = o.swap_stored_flags().copy()
+    g.stage_reset_scene()
+    o.reset_scene()
+    _compare(g, o, "after engine ResetScene", stored=True)
+    assert stored_before.sum() > 0
+    assert_bit_exact("stored flags kept", g.swap_stored_flags(), stored_before)
+    assert g.stats()["lastFreeBlockId"] == 2047
+    for k in range(16, 22):
+        assert g(seq[k]) == o(seq[k]), k
+    _compare(g, o, "frames after the reset", stored=True)
     g.close()

@@ -49,7 +49,7 @@ class TfStats(ctypes.Structure):
 class TfTotals(ctypes.Structure):
     _fields_ = [(n, ctypes.c_longlong) for n in ("frames", "frames_tracked", "resets", "visible_sum", "tiles_sum",
                                                  "swapped_in", "swapped_out", "integrate_lanes_read",
-                                                 "integrate_lanes_written")]
+                                                 "integrate_lanes_written", "swapped_in_merged")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

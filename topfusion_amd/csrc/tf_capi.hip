@@ -403,8 +403,12 @@ static void swap_pyramids(tf_ctx* c)
         const bool ext_ = timed_ && stage_single(c, id);                                      \
         if (ext_) { c->ev_start = prof_event(c, slot, 2 * (id)); c->ev_stop = prof_event(c, slot, 2 * (id) + 1); } \
         else if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id)), (strm)));     \
-        TF_CHECK(expr);                                                                       \
-        if (ext_ && c->ev_start) { c->ev_start = c->ev_stop = nullptr; return TF_HIP_ERROR; } \
+        const hipError_t se_ = (expr);                                                        \
+        /* the launcher consumes the events in tf_launch; on every other exit they are dropped */ \
+        const bool unused_ = ext_ && c->ev_start;                                             \
+        c->ev_start = c->ev_stop = nullptr;                                                   \
+        TF_CHECK(se_);                                                                        \
+        if (unused_) return TF_HIP_ERROR;                                                     \
         if (timed_ && !ext_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id) + 1), (strm))); \
     } while (0)
 #define STAGE(id, expr) STAGE_ON(c->stream, id, expr)
@@ -887,9 +891,9 @@ extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12]
 }
 
 extern "C" tf_status tf_stage_reset_scene(tf_ctx* c)
-{
+{   // SceneReconstructionEngine::ResetScene: the GlobalCache stays (SceneReconstructionEngine_host.cu:51-73)
     if (!c) return TF_INVALID_ARG;
-    TF_CHECK(tfk_reset_scene(c));
+    TF_CHECK(tfk_reset_scene(c, 0));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
 }
@@ -1240,6 +1244,7 @@ extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)
     t->frames = d->tot_frames; t->frames_tracked = d->tot_tracked; t->resets = d->tot_resets;
     t->visible_sum = d->tot_visible; t->tiles_sum = d->tot_tiles;
     t->swapped_in = d->tot_swap_in; t->swapped_out = d->tot_swap_out;
+    t->swapped_in_merged = d->tot_swap_merged;
     t->integrate_lanes_read = t->integrate_lanes_written = 0;
     std::vector<long long> h(2 * TF_INTEG_WG);
     TF_CHECK(hipMemcpyAsync(h.data(), c->integ_cnt, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, c->stream));
@@ -1251,7 +1256,7 @@ extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)
 extern "C" tf_status tf_reset_totals(tf_ctx* c)
 {
     if (!c) return TF_INVALID_ARG;
-    const size_t b = offsetof(TfDevState, tot_frames), e = offsetof(TfDevState, tot_pad_) + sizeof(long long);
+    const size_t b = offsetof(TfDevState, tot_frames), e = offsetof(TfDevState, tot_swap_merged) + sizeof(long long);
     TF_CHECK(hipMemsetAsync((char*)c->st + b, 0, e - b, c->stream));
     TF_CHECK(hipMemsetAsync(c->integ_cnt, 0, sizeof(long long) * 2 * TF_INTEG_WG, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));

@@ -79,7 +79,8 @@ struct TfDevState {
     // swap-in launch to the swap-out launch
     int swap_in, swap_out, swap_realloc, swap_free0;
     // totals since creation / tf_reset_totals, accumulated by the frame end (tf_totals)
-    long long tot_frames, tot_tracked, tot_resets, tot_visible, tot_tiles, tot_swap_in, tot_swap_out, tot_pad_;
+    long long tot_frames, tot_tracked, tot_resets, tot_visible, tot_tiles, tot_swap_in, tot_swap_out,
+        tot_swap_merged;         // swap-ins whose entry held stored data (a real GlobalCache -> VBA transfer)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -377,7 +378,8 @@ hipError_t tf_icp_order_before(tf_ctx* c);
 hipError_t tf_icp_order_after(tf_ctx* c);   // frame_begin: frame path (tf_frame_begin)
 int tfk_icp_persistent_ok(tf_ctx* c);      // k_icp_frame fits (co-residency, slot count)
 hipError_t tfk_pose_from_input(tf_ctx* c, int mode);   // pose_in -> alloc / raycast matrices
-hipError_t tfk_reset_scene(tf_ctx* c);
+// clear_cache: also empty the GlobalCache (TopFu-level resets); 0 = the engine's ResetScene
+hipError_t tfk_reset_scene(tf_ctx* c, int clear_cache = 1);
 hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot);   // frame end + ResetScene if ICP failed
 hipError_t tfk_grid_rebuild(tf_ctx* c);   // block grid from the hash (after a hash upload)
 hipError_t tfk_grid_clear(tf_ctx* c);     // every cell (-1, TF_VOFF_NONE)

@@ -985,7 +985,7 @@ hipError_t tfk_icp_maps_end(tf_ctx* c, int slot)
     for (int l = 0; l < TF_LEVELS; ++l) { a.pts[l] = c->prev_pts[l]; a.nrm[l] = c->prev_nrm[l]; }
     a.W = c->W; a.H = c->H; a.voxelSize = c->p.voxelSize;
     ResetArgs r;
-    tf_reset_args(c, &r, 1, slot);
+    tf_reset_args(c, &r, 1, slot, 1);
     const int gx = (c->W + 31) / 32, nmaps = gx * ((c->H + 31) / 32);
     tf_launch(c, k_icp_maps_end, dim3(nmaps + TF_END_BLOCKS), dim3(256), 0, a, r, gx, nmaps);
     return hipGetLastError();

@@ -128,4 +128,4 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
 
 
 // on_failure = 0: ResetScene now (full); 1: the frame end of batch slot `slot`
-void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot);
+void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot, int clear_cache);

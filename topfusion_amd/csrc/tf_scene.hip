@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(256) k_reset_scene(ResetArgs r)
     reset_scene_block(r, blockIdx.x, gridDim.x);
 }
 
-void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot)
+void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot, int clear_cache)
 {
     r->vba = c->vba; r->n_vox = (size_t)c->p.n_blocks * TF_BLK3;
     r->allocList = c->allocList; r->n_blocks = c->p.n_blocks;
@@ -51,18 +51,20 @@ void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot)
     r->slot = on_failure ? slot : 0;
     r->full = on_failure ? 0 : 1;       // (+ st->scene_external, read on the device)
     // swapping: swap-outs push blocks back onto the free list in any order, so its identity (which
-    // the clear-what-was-written reset relies on) no longer holds -- every reset is full, and
-    // also empties the GlobalCache (swap states, stored flags)
-    r->swapState = c->p.use_swapping ? c->swapState : nullptr;
-    r->swapFlags = c->p.use_swapping ? c->swapFlags : nullptr;
+    // the clear-what-was-written reset relies on) no longer holds -- every reset is full.  The
+    // TopFu-level resets (construction, TopFu::reset, the ICP-failure frame end) also empty the
+    // GlobalCache (swap states, stored flags), so no block of the old scene is swapped into the
+    // new one; the engine's ResetScene keeps it, as the reference's does (clear_cache = 0)
+    r->swapState = c->p.use_swapping && clear_cache ? c->swapState : nullptr;
+    r->swapFlags = c->p.use_swapping && clear_cache ? c->swapFlags : nullptr;
     r->vba_rgb = c->p.voxel_rgb ? c->vba_rgb : nullptr;
     if (c->p.use_swapping) r->full = 1;
 }
 
-hipError_t tfk_reset_scene(tf_ctx* c)
+hipError_t tfk_reset_scene(tf_ctx* c, int clear_cache)
 {
     ResetArgs r;
-    tf_reset_args(c, &r, 0, 0);
+    tf_reset_args(c, &r, 0, 0, clear_cache);
     hipLaunchKernelGGL(k_reset_scene, dim3(2048), dim3(256), 0, c->stream, r);
     return hipGetLastError();
 }
@@ -73,7 +75,7 @@ hipError_t tfk_reset_scene(tf_ctx* c)
 hipError_t tfk_reset_scene_on_failure(tf_ctx* c, int slot)
 {
     ResetArgs r;
-    tf_reset_args(c, &r, 1, slot);
+    tf_reset_args(c, &r, 1, slot, 1);
     hipLaunchKernelGGL(k_reset_scene, dim3(TF_END_BLOCKS), dim3(256), 0, c->stream, r);
     return hipGetLastError();
 }

@@ -179,6 +179,7 @@ k_swap_in(TfDevState* __restrict__ st, unsigned char* __restrict__ swapState, co
             if (flags & (1 << i)) { if (r < take) list[r] = base + i; ++r; }
     }
     __syncthreads();
+    int merged = 0;
     for (int k = 0; k < take; ++k) {
         const int id = list[k];
         if (swapFlags[id]) {
@@ -186,9 +187,11 @@ k_swap_in(TfDevState* __restrict__ st, unsigned char* __restrict__ swapState, co
             uint2* dst = (uint2*)(vba + (size_t)hash[id].ptr * TF_BLK3);
             const uint2 s2 = src[threadIdx.x], d2 = dst[threadIdx.x];
             dst[threadIdx.x] = make_uint2(sw_combine(s2.x, d2.x, maxW), sw_combine(s2.y, d2.y, maxW));
+            ++merged;
         }
         if (threadIdx.x == 0) swapState[id] = 2;
     }
+    if (threadIdx.x == 0 && merged) atomicAdd((unsigned long long*)&st->tot_swap_merged, (unsigned long long)merged);
     __syncthreads();
     // swap-out candidates of the chunk: state 2 (after the swap-ins above), a block, not visible
     int c = 0;
