@@ -36,9 +36,6 @@ struct RCache { int bx, by, bz; };
 // reference's serial corner order.  Values, the IndexCache state and vmIndex are exactly
 // those of the reference's serial reads (RepresentationAccess.hpp:73-199).
 // ---------------------------------------------------------------------------------------
-#ifndef TF_RAY_SPEC
-#define TF_RAY_SPEC 1
-#endif
 __device__ __forceinline__ int vblk(int p) { return p >> 3; }   // floor(p / 8) (:9-17), arithmetic shift
 __device__ __forceinline__ int vlin(int x, int y, int z) { return (x & 7) + ((y & 7) << 3) + ((z & 7) << 6); }
 
@@ -84,12 +81,21 @@ __device__ __forceinline__ void blk_load8(const SceneView& s, const unsigned (&o
 // the rare case (a block outside the grid, i.e. beyond +-128 blocks): cell or hash walk per corner.
 // Callers take it for the whole wave, so the common path's loads stay unbranched and in flight
 // together.
+// (one rolled loop with a single walk in it: eight inlined walk loops in the ray march's hot
+// loop cost it registers and code size for a path the C2 / C3 scenes never take)
 __device__ __forceinline__ void blk_lookup_slow(const SceneView& s, const int (&X)[2], const int (&Y)[2], const int (&Z)[2],
                                              int2 (&g)[8])
 {
+    int x0 = X[0], x1 = X[1], y0 = Y[0], y1 = Y[1], z0 = Z[0], z1 = Z[1];
+    // (kept in VGPRs: left alone the optimiser turns the selects below into a private array in scratch)
+    asm volatile("" : "+v"(x0), "+v"(x1), "+v"(y0), "+v"(y1), "+v"(z0), "+v"(z1));
+#pragma unroll 1
     for (int c = 0; c < 8; ++c) {
-        const int bx = X[c & 1], by = Y[(c >> 1) & 1], bz = Z[c >> 2];
-        g[c] = tf_grid_in(bx, by, bz) ? s.grid[tf_grid_cell(bx, by, bz)] : blk_walk(s, bx, by, bz);
+        const int bx = (c & 1) ? x1 : x0, by = (c & 2) ? y1 : y0, bz = (c & 4) ? z1 : z0;
+        const int2 r = tf_grid_in(bx, by, bz) ? s.grid[tf_grid_cell(bx, by, bz)] : blk_walk(s, bx, by, bz);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (k == c) g[k] = r;
     }
 }
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
@@ -121,21 +127,6 @@ __device__ __forceinline__ int lin_y(int y) { return (y & 7) << 3; }
 __device__ __forceinline__ int lin_zg(int z) { return ((z & 7) << 6) + TF_BLK3; }
 __device__ __forceinline__ float raw_sdf(unsigned r) { return (float)(short)(r & 0xffffu); }
 __device__ __forceinline__ float raw_w(unsigned r) { return (float)((r >> 16) & 0xffu); }
-
-// v[i] for a runtime i as a chain of v_cndmask (the empty asm keeps each element in a VGPR;
-// without it the optimiser turns the chain into a dynamically indexed private array)
-__device__ __forceinline__ int sel8(const int (&v)[8], int i)
-{
-    int r = v[0];
-    asm volatile("" : "+v"(r));
-#pragma unroll
-    for (int o = 1; o < 8; ++o) {
-        int t = v[o];
-        asm volatile("" : "+v"(t));
-        r = (i == o) ? t : r;
-    }
-    return r;
-}
 
 // v[ux + 2uy + 4uz] for per-axis bits: a 3-level select tree (7 selects on 3 shared conditions)
 // (the empty asm keeps the selects as selects: left alone the optimiser rebuilds the tree
@@ -214,11 +205,6 @@ __device__ __forceinline__ void corners_lookup(const SceneView& s, const float* 
     else blk_load8(s, o, g);
     corners_blocks(q, g);
 }
-__device__ __forceinline__ void corners_fetch(const SceneView& s, const float* pt, Corners& q)
-{
-    corners_lookup(s, pt, q);
-    corners_vox(s, q);
-}
 // the IndexCache after the 8 serial corner reads: the block of the last corner whose block exists
 __device__ __forceinline__ void corners_cache(const Corners& q, RCache* k)
 {
@@ -275,10 +261,8 @@ struct RayArgs {
     float oneOverVoxelSize, mu;
 };
 
-// castRay (VisualisationEngine_Shared.hpp:99-172), split into init / step / finish so that two
-// rays can be marched interleaved.  One step = the uninterpolated read at ROUND(pt) and, in the
-// band, the interpolated read at pt.  ROUND(pt) is one of the eight interpolation corners, so a
-// step fetches the corners once (speculatively): one grid round trip + one voxel round trip.
+// castRay's state (VisualisationEngine_Shared.hpp:99-172): ray_init, the march loop
+// (ray_march_lite), ray_refine at the surface.
 struct Ray {
     float pt[3], dir[3];
     float totalLength, totalLengthMax, sdfValue;
@@ -312,45 +296,8 @@ __device__ __forceinline__ void ray_init(const RayArgs& a, const float* invM, in
     R.active = R.totalLength < R.totalLengthMax;
 }
 
-// one pass of castRay's loop body on the fetched corners of R.pt
-// (q.raw is only read when ROUND(pt)'s block exists: a step in unallocated space needs no voxel)
-template <bool MARK>
-__device__ __forceinline__ void ray_step(const RayArgs& a, Ray& R, const Corners& q)
-{
-    const float stepScale = a.mu * a.oneOverVoxelSize;
-    // uninterpolated read at ROUND(pt) (readFromSDF_float_uninterpolated, :129-135)
-    const int ux = q.cu & 1, uy = (q.cu >> 1) & 1, uz = q.cu >> 2;
-    int vmIndex = 0;
-    const bool found = (q.valid >> q.cu) & 1u;
-    if (found) {
-        const int Ubx = q.bx + (ux & q.sx), Uby = q.by + (uy & q.sy), Ubz = q.bz + (uz & q.sz);
-        const bool hit = Ubx == R.k.bx && Uby == R.k.by && Ubz == R.k.bz;
-        vmIndex = hit ? 1 : q.hU + 1;
-        R.k.bx = Ubx; R.k.by = Uby; R.k.bz = Ubz;
-    }
-    // a missing block reads Voxel_s(): 32767 / 32767 = 1
-    float sdfValue = found ? tf_short_to_float((short)(sel_tree(q.raw, ux != 0, uy != 0, uz != 0) & 0xffffu)) : 1.0f;
-    if (MARK && vmIndex) a.visType[vmIndex - 1] = 1;
-    float stepLength;
-    if (!vmIndex) {
-        stepLength = (float)TF_BLK;
-    } else {
-        if ((sdfValue <= 0.1f) && (sdfValue >= -0.5f)) {
-            sdfValue = interp_sdf(q);
-            corners_cache(q, &R.k);
-        }
-        if (sdfValue <= 0.0f) { R.sdfValue = sdfValue; R.active = false; return; }   // the loop's break
-        float qq = sdfValue * stepScale;
-        stepLength = (qq < 1.0f) ? 1.0f : qq;
-    }
-    R.sdfValue = sdfValue;
-    R.pt[0] += stepLength * R.dir[0]; R.pt[1] += stepLength * R.dir[1]; R.pt[2] += stepLength * R.dir[2];
-    R.totalLength += stepLength;
-    R.active = R.totalLength < R.totalLengthMax;
-}
-
-// castRay's refinement at the surface: the step back onto it; true when there is one (then
-// ray_finish completes it on the fetched corners of R.pt)
+// castRay's refinement at the surface: the step back onto it; true when there is one (then the
+// confidence read at the new pt completes it, ray_march_lite)
 __device__ __forceinline__ bool ray_refine(const RayArgs& a, Ray& R)
 {
     if (!(R.sdfValue <= 0.0f)) return false;
@@ -358,87 +305,128 @@ __device__ __forceinline__ bool ray_refine(const RayArgs& a, Ray& R)
     R.pt[0] += stepLength * R.dir[0]; R.pt[1] += stepLength * R.dir[1]; R.pt[2] += stepLength * R.dir[2];
     return true;
 }
-__device__ __forceinline__ float ray_finish(const RayArgs& a, Ray& R, const Corners& q)
+#ifdef TF_RAY_STATS
+// diagnostic builds only (tools/ray_stats.py): per ray, steps in unallocated space (low 16 bits)
+// and steps that read voxels (high 16 bits), for the two raycasts of the last pair launch
+__device__ unsigned tf_ray_stats_buf[2 * 1280 * 960];
+extern "C" int tf_debug_ray_stats(void* host, size_t bytes)
 {
-    float confidence;
-    const float sdfValue = interp_sdf_conf(q, &confidence);
-    const float stepLength = sdfValue * (a.mu * a.oneOverVoxelSize);
-    R.pt[0] += stepLength * R.dir[0]; R.pt[1] += stepLength * R.dir[1]; R.pt[2] += stepLength * R.dir[2];
-    return confidence + 1.0f;
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tf_ray_stats_buf), bytes < sizeof(tf_ray_stats_buf) ? bytes : sizeof(tf_ray_stats_buf), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
+
+// (hash entry, VBA offset) of one block: its grid cell, or the hash walk outside the grid (the wave
+// takes that branch together; the common path's load stays unbranched)
+__device__ __forceinline__ int2 blk_one(const SceneView& s, int bx, int by, int bz)
+{
+    const bool in = tf_grid_in(bx, by, bz);
+    const unsigned off = in ? (unsigned)tf_grid_cell(bx, by, bz) * 8u : 0u;
+    int2 g = ld_off<int2>(s.grid, off);
+    if (wave_any(!in)) {
+        if (!in) g = blk_walk(s, bx, by, bz);
+    }
+    return g;
+}
+
+// readFromSDF_float_interpolated at pt (RepresentationAccess.hpp:137-162) with the IndexCache
+// update of its eight serial reads; with conf != nullptr readWithConfidenceFromSDF_float_interpolated
+// (:164-199).  One array holds the corners' VBA offsets and then, loaded over them, their voxel
+// words: the register footprint of the band steps is what sets the march's occupancy.
+__device__ __forceinline__ float interp_at(const SceneView& s, const float* pt, RCache* k, float* conf)
+{
+    Corners q;
+    unsigned o[8];
+    const bool in = corners_prep(pt, q, o);
+    int v[8];
+    if (wave_any(!in)) {
+        int2 g[8];
+        corners_slow(s, q, g);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = g[c].y;
+    } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = ld_off<int>(s.grid, o[c] + 4u);
+    }
+    q.valid = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) q.valid |= (v[c] >= 0 ? 1u : 0u) << c;
+    if (k) corners_cache(q, k);
+    const int lx[2] = { lin_x(q.fx), lin_x(q.fx + 1) }, ly[2] = { lin_y(q.fy), lin_y(q.fy + 1) };
+    const int lz[2] = { lin_zg(q.fz), lin_zg(q.fz + 1) };
+#pragma unroll
+    for (int c = 0; c < 8; ++c) q.raw[c] = vox_at(s, v[c], lx[c & 1] + ly[(c >> 1) & 1] + lz[c >> 2]);
+    return conf ? interp_sdf_conf(q, conf) : interp_sdf(q);
+}
+
+// castRay with the uninterpolated read alone on most steps: a step looks up ROUND(pt)'s block
+// (one grid load) and reads its one voxel; only a step whose value lies in the band
+// [-0.5, 0.1] (where castRay switches to the interpolated read, 1-3 steps a ray) fetches the
+// eight interpolation corners.  Against the eight-corner fetch on every step this spends two
+// round trips more per band step, and holds far fewer registers across the loop (the ray state
+// only): more waves resident to hide the dependent loads.  Values, visibility marks and the
+// IndexCache follow castRay's serial reads exactly (VisualisationEngine_Shared.hpp:117-160).
+template <bool MARK>
+__device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* invM, int x, int y, float* pt)
+{
+    Ray R;
+    ray_init(a, invM, x, y, R);
+    const float stepScale = a.mu * a.oneOverVoxelSize;
+#ifdef TF_RAY_STATS
+    unsigned n_free = 0, n_found = 0;
+#endif
+    while (R.active) {
+        const int rx = tf_round(R.pt[0]), ry = tf_round(R.pt[1]), rz = tf_round(R.pt[2]);
+        const int bx = vblk(rx), by = vblk(ry), bz = vblk(rz);
+        const int2 g = blk_one(a.s, bx, by, bz);
+        const bool found = g.y >= 0;
+        int vmIndex = 0;
+        if (found) {
+            const bool hit = bx == R.k.bx && by == R.k.by && bz == R.k.bz;
+            vmIndex = hit ? 1 : g.x + 1;
+            R.k.bx = bx; R.k.by = by; R.k.bz = bz;
+        }
+#ifdef TF_RAY_STATS
+        if (found) ++n_found; else ++n_free;
+#endif
+        unsigned raw = 0;
+        if (wave_any(found)) raw = vox_at(a.s, g.y, lin_x(rx) + lin_y(ry) + lin_zg(rz));
+        // a missing block reads Voxel_s(): 32767 / 32767 = 1
+        float sdfValue = found ? tf_short_to_float((short)(raw & 0xffffu)) : 1.0f;
+        if (MARK && vmIndex) a.visType[vmIndex - 1] = 1;
+        float stepLength;
+        if (!vmIndex) {
+            stepLength = (float)TF_BLK;
+        } else {
+            if ((sdfValue <= 0.1f) && (sdfValue >= -0.5f)) sdfValue = interp_at(a.s, R.pt, &R.k, nullptr);
+            if (sdfValue <= 0.0f) { R.sdfValue = sdfValue; R.active = false; continue; }   // the loop's break
+            const float qq = sdfValue * stepScale;
+            stepLength = (qq < 1.0f) ? 1.0f : qq;
+        }
+        R.sdfValue = sdfValue;
+        R.pt[0] += stepLength * R.dir[0]; R.pt[1] += stepLength * R.dir[1]; R.pt[2] += stepLength * R.dir[2];
+        R.totalLength += stepLength;
+        R.active = R.totalLength < R.totalLengthMax;
+    }
+#ifdef TF_RAY_STATS
+    if (x + y * a.W < 1280 * 960) tf_ray_stats_buf[(MARK ? 0 : 1280 * 960) + x + y * a.W] = n_free | (n_found << 16);
+#endif
+    float w = 0.0f;
+    if (ray_refine(a, R)) {                 // ray_finish on interp_at's confidence read
+        float confidence;
+        const float sdfValue = interp_at(a.s, R.pt, nullptr, &confidence);
+        const float stepLength = sdfValue * (a.mu * a.oneOverVoxelSize);
+        R.pt[0] += stepLength * R.dir[0]; R.pt[1] += stepLength * R.dir[1]; R.pt[2] += stepLength * R.dir[2];
+        w = confidence + 1.0f;
+    }
+    pt[0] = R.pt[0]; pt[1] = R.pt[1]; pt[2] = R.pt[2];
+    return w;
 }
 
 template <bool MARK>
 __device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, int x, int y, float* pt)
 {
-    Ray R;
-    ray_init(a, invM, x, y, R);
-#if TF_RAY_SPEC
-    if (!MARK) {
-        // castRay<false> (renderImage, stand-alone raycasts): speculative block lookups, per lane.
-        // While a step's voxels are in flight, the eight VBA offsets of the position the NEXT step
-        // has if this one is the common kind -- sdf = 1 in an allocated block (step
-        // max(stepScale, 1)) or no block (step SDF_BLOCK_SIZE), computed by ray_step's own
-        // operations -- are loaded too.  A lane whose actual position equals its speculated one
-        // bit for bit starts the next step with its lookups done; a step whose live lanes all hit
-        // skips the grid round trip.  (Without visibility marks only vmIndex != 0 matters, so the
-        // hash index of the ROUND corner is not needed.)
-        const float qq1 = 1.0f * (a.mu * a.oneOverVoxelSize);
-        const float Lsdf1 = (qq1 < 1.0f) ? 1.0f : qq1;
-        bool have = false;
-        int sv[8];
-        while (R.active) {
-            Corners q;
-            unsigned o[8];
-            const bool in = corners_prep(R.pt, q, o);
-            if (wave_any(!have)) {
-                int2 g[8];
-                if (wave_any(!have && !in)) corners_slow(a.s, q, g);
-                else if (!have) blk_load8(a.s, o, g);
-                if (!have) {
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) sv[c] = g[c].y;
-                }
-            }
-            q.valid = 0;
-#pragma unroll
-            for (int c = 0; c < 8; ++c) { q.voff[c] = sv[c]; q.valid |= (sv[c] >= 0 ? 1u : 0u) << c; }
-            q.hU = 0;
-            const bool found = (q.valid >> q.cu) & 1u;
-            if (wave_any(found)) corners_vox(a.s, q);
-            const float L = found ? Lsdf1 : (float)TF_BLK;
-            float ps[3];
-            ps[0] = R.pt[0] + L * R.dir[0]; ps[1] = R.pt[1] + L * R.dir[1]; ps[2] = R.pt[2] + L * R.dir[2];
-            {
-                Corners qs;
-                unsigned os[8];
-                have = corners_prep(ps, qs, os);
-                if (have) {
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) sv[c] = ld_off<int>(a.s.grid, os[c] + 4u);
-                }
-            }
-            ray_step<MARK>(a, R, q);
-            have = have && __float_as_uint(R.pt[0]) == __float_as_uint(ps[0]) &&
-                   __float_as_uint(R.pt[1]) == __float_as_uint(ps[1]) && __float_as_uint(R.pt[2]) == __float_as_uint(ps[2]);
-        }
-    } else
-#endif
-    while (R.active) {
-        Corners q;
-        corners_lookup(a.s, R.pt, q);
-        // the voxel round trip only when some lane's ROUND(pt) block exists (free space
-        // between surfaces is stepped a block at a time on the grid alone)
-        if (wave_any((q.valid >> q.cu) & 1u)) corners_vox(a.s, q);
-        ray_step<MARK>(a, R, q);
-    }
-    float w = 0.0f;
-    if (ray_refine(a, R)) {
-        Corners q;
-        corners_fetch(a.s, R.pt, q);
-        w = ray_finish(a, R, q);
-    }
-    pt[0] = R.pt[0]; pt[1] = R.pt[1]; pt[2] = R.pt[2];
-    return w;
+    return ray_march_lite<MARK>(a, invM, x, y, pt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -449,6 +437,9 @@ __device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, 
 // vtab: this thread's 8-entry slot in LDS (VTAB_STRIDE ints): the 2x2x2 block offsets, so each
 // of the 32 reads finds its block with one LDS load instead of an 8-way select.
 #define VTAB_STRIDE 9
+#ifndef TF_NORMAL_PHASES
+#define TF_NORMAL_PHASES 1
+#endif
 __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret, int* vtab)
 {
     float ffx = floorf(pt[0]), ffy = floorf(pt[1]), ffz = floorf(pt[2]);
@@ -481,6 +472,12 @@ __device__ void sdf_normal(const SceneView& s, const float* pt, float* ret, int*
     t0 = RV(2, 0, 0); t1 = RV(2, 1, 0); t2 = RV(2, 0, 1); t3 = RV(2, 1, 1);
     p2 = t0 * ny * nz + t1 * cy * nz + t2 * ny * cz + t3 * cy * cz;
     ret[0] = tf_div32767(p1 * nx + p2 * cx - v1);
+#if TF_NORMAL_PHASES
+    // the y and z reads after the x derivative: 16 + 16 loads in flight instead of 32, so the
+    // raycast kernels that end in this gradient keep their register budget (one more round trip
+    // per pixel, once, against the march's many)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     p1 = f0 * nx * nz + f1 * cx * nz + b0 * nx * cz + b1 * cx * cz;
     t0 = RV(0, -1, 0); t1 = RV(1, -1, 0); t2 = RV(0, -1, 1); t3 = RV(1, -1, 1);
     p2 = t0 * nx * nz + t1 * cx * nz + t2 * nx * cz + t3 * cx * cz;
