@@ -152,7 +152,7 @@ static void ctx_free(tf_ctx* c)
     if (c->caller_ev) (void)hipEventDestroy(c->caller_ev);
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
-                     c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
+                     c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->edBins, c->edBinCnt, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
                      c->vba_rgb_guard, c->rgb_in, c->integ_cnt };
     for (void* b : bufs) if (b) (void)hipFree(b);
@@ -252,6 +252,8 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->blockOff, sizeof(int) * (size_t)pin->vis_capacity);
     ALLOC(c->edChunk, sizeof(int) * ((size_t)pin->vis_capacity / 256 + 1));
     ALLOC(c->edSpill, sizeof(int2) * (size_t)ed_nrows(c->H));
+    ALLOC(c->edBins, sizeof(uint4) * 2 * (size_t)ed_nrows(c->H) * ED_LDS_MAX_N);
+    ALLOC(c->edBinCnt, sizeof(int) * 2 * (size_t)ed_nrows(c->H));
     ALLOC(c->depth_in, sizeof(uint16_t) * npx);
     ALLOC(c->dists, sizeof(float) * npx);
     {   // each map's three pyramid levels are contiguous in one allocation
@@ -316,6 +318,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipMemsetAsync(c->visType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->visibleIds, 0, sizeof(int) * (size_t)pin->vis_capacity, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->raycast, 0, sizeof(float) * 4 * npx, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->edBinCnt, 0, sizeof(int) * 2 * (size_t)ed_nrows(c->H), c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->grey, 0, sizeof(uchar4) * npx, c->stream);
     for (int l = 0; l < TF_LEVELS && e == hipSuccess; ++l) {
         size_t n = (size_t)c->lw[l] * c->lh[l];
@@ -334,11 +337,18 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         if (e == hipSuccess) e = ed_spill_all(c);       // the first CreateExpectedDepths clears the whole buffer
         if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     }
+    {   // integration grid of the frame path (TFUSION_INTEG_WG_FRAME overrides; A/B)
+        const char* env = getenv("TFUSION_INTEG_WG_FRAME");
+        c->integ_wg_frame = env ? atoi(env) : TF_INTEG_WG_FRAME;
+        if (c->integ_wg_frame < 64 || c->integ_wg_frame > TF_INTEG_WG) c->integ_wg_frame = TF_INTEG_WG;
+    }
     {   // k_ed_fill: LDS rows up to ED_LDS_MAX_N visible entries, device-scope atomics past that
         // (TFUSION_ED_LDS_MAX_N overrides the threshold; the parity tests run both paths)
         const char* env = getenv("TFUSION_ED_LDS_MAX_N");
         c->ed_lds_max_n = env ? atoi(env) : ED_LDS_MAX_N;
         if (c->ed_lds_max_n > ED_LDS_MAX_N) c->ed_lds_max_n = ED_LDS_MAX_N;
+        // the binned boxes hold 12-bit coordinates (tf_ed.h ed_bin_pack)
+        if (c->W > ED_MAX_W || c->H > ED_MAX_W) c->ed_lds_max_n = 0;
     }
     e = tfk_reset_scene(c);                              // topfu.cpp:75
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -868,7 +878,7 @@ extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12]
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, pose_rt, stage == TF_STAGE_INTEGRATE || stage == TF_STAGE_EXPECTED_DEPTHS ? TF_POSE_ALLOC_NOINV : 0);
     if (s != TF_OK) return s;
-    if (stage == TF_STAGE_EXPECTED_DEPTHS) TF_CHECK(tfk_expected_depths(c));    // boxes of the current list
+    if (stage == TF_STAGE_EXPECTED_DEPTHS) TF_CHECK(tfk_expected_depths(c, 0, 1));    // boxes of the current list
     // the pair's renderImage half reads the snapshot of the raycast matrix / range region
     if (stage == TF_STAGE_RAYCAST_RENDER) TF_CHECK(tfk_render_snapshot(c));
     hipEvent_t e0, e1;
@@ -877,12 +887,15 @@ extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12]
     hipError_t e = hipEventRecord(e0, c->stream);
     for (int i = 0; i < iters && e == hipSuccess; ++i)
         e = stage == TF_STAGE_INTEGRATE ? tfk_integrate(c)
-          : stage == TF_STAGE_EXPECTED_DEPTHS ? tfk_expected_depths(c, 1)
+          : stage == TF_STAGE_EXPECTED_DEPTHS ? tfk_expected_depths(c, 1, 1)
           : stage == TF_STAGE_RAYCAST_ICP ? tfk_raycast(c, 1) : tfk_raycast_pair(c);
     if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
     if (e == hipSuccess) e = hipEventSynchronize(e1);
     float ms = 0.f;
     if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    // the repeated fills kept the bins: empty them for the next projection pass
+    if (e == hipSuccess && stage == TF_STAGE_EXPECTED_DEPTHS)
+        e = hipMemsetAsync(c->edBinCnt, 0, sizeof(int) * 2 * (size_t)ed_nrows(c->H), c->stream);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (e != hipSuccess) return tf_from_hip(e);

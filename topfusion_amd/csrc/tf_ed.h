@@ -11,6 +11,10 @@ struct EdArgs {
     uint4* rec;          // per visible entry: ulx | uly << 16, lrx | lry << 16, zmin, zmax bits (x ~0u: none)
     int* tiles; int* off; int* chunk;
     int2* spill;         // per fill row: extent of the pixels the last fill wrote outside the /8 region
+    uint4* bins;         // [2 * nrows][ED_LDS_MAX_N] binned boxes (ed_bin_pack): row r's, then row r's
+                         // share of the boxes reaching below the LDS rows (entry index % nrows == r)
+    int* bin_cnt;        // [2 * nrows] entries in each bin (the fill's workgroup r zeroes its two)
+    int keep_bins;       // the fill leaves the counts (tf_time_stage's repeated fills)
     int W, H;
     int rc, rr;          // the /8 region: (W-1)/8+1 columns, (H-1)/8+1 rows
     int nrows;           // k_ed_fill's LDS rows (ed_nrows: rr + ED_XROWS, at most H)
@@ -21,6 +25,15 @@ struct EdArgs {
 };
 
 #define ED_CHUNK 256     // visible entries per projection chunk (one workgroup pass)
+#define ED_MAX_ROWS 520  // k_ed_fill LDS rows for H <= 4096 (ed_nrows); binning needs W, H <= 4096
+
+// a binned box: its /8 pixel box (12 bits per coordinate), the visible-list index (16 bits, the
+// MAX_RENDERING_BLOCKS check) and the z range -- everything the fill reads in one 16-byte load
+__device__ __forceinline__ uint4 ed_bin_pack(unsigned ulx, unsigned uly, unsigned lrx, unsigned lry, unsigned i,
+                                             unsigned zmin, unsigned zmax)
+{
+    return make_uint4(ulx | uly << 12 | (i & 0xffu) << 24, lrx | lry << 12 | (i >> 8) << 24, zmin, zmax);
+}
 
 // memsetKernel(FAR_AWAY, VERY_CLOSE) + ProjectSingleBlock (VisualisationEngine_Shared.hpp:33-77).
 // Visible entries are processed in chunks of 256 (thread t of a chunk pass = entry
@@ -72,6 +85,16 @@ __device__ __forceinline__ void ed_project_block(const EdArgs& a, const TfDevSta
         }
     }
     __shared__ int wsum[4];
+    // binning (n <= lds_max_n): every valid box goes into the bin of each LDS row it covers, and
+    // into a "below" bin when it reaches past the LDS rows, so the fill's row workgroup reads its
+    // own boxes instead of scanning the whole list.  Counts are aggregated per chunk in LDS (one
+    // device atomic per bin and chunk); the order inside a bin is arbitrary -- the fill reduces
+    // with min / max only, so its result does not depend on it.
+    __shared__ int lcnt[2 * ED_MAX_ROWS], gbase[2 * ED_MAX_ROWS];
+    const bool binning = n <= a.lds_max_n;
+    const int nb2 = 2 * a.nrows;
+    if (binning)
+        for (int r = threadIdx.x; r < nb2; r += 256) lcnt[r] = 0;
     const int nchunks = (n + ED_CHUNK - 1) / ED_CHUNK;
     const float* M = st->M_alloc;          // pose.inv() (topfu.cpp:306)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -117,6 +140,32 @@ __device__ __forceinline__ void ed_project_block(const EdArgs& a, const TfDevSta
                 }
             }
             a.rec[i] = rec; a.tiles[i] = ntiles;
+        }
+        if (binning) {
+            const uint4 rec = i < n ? a.rec[i] : make_uint4(0xffffffffu, 0u, 0u, 0u);   // (this thread's own store)
+            const bool valid = rec.x != 0xffffffffu;
+            const int uly = (int)(rec.x >> 16), lry = (int)(rec.y >> 16);
+            const int r1 = lry < a.nrows - 1 ? lry : a.nrows - 1;
+            const bool below = valid && lry >= a.nrows;
+            const int bb = a.nrows + (i % a.nrows);
+            if (valid)
+                for (int r = uly; r <= r1; ++r) atomicAdd(&lcnt[r], 1);
+            if (below) atomicAdd(&lcnt[bb], 1);
+            __syncthreads();
+            for (int r = threadIdx.x; r < nb2; r += 256) {
+                const int c = lcnt[r];
+                gbase[r] = c ? atomicAdd(&a.bin_cnt[r], c) : 0;
+                lcnt[r] = 0;
+            }
+            __syncthreads();
+            if (valid) {
+                const uint4 e = ed_bin_pack(rec.x & 0xffffu, (unsigned)uly, rec.y & 0xffffu, (unsigned)lry, (unsigned)i,
+                                            rec.z, rec.w);
+                for (int r = uly; r <= r1; ++r) a.bins[(size_t)r * ED_LDS_MAX_N + gbase[r] + atomicAdd(&lcnt[r], 1)] = e;
+                if (below) a.bins[(size_t)bb * ED_LDS_MAX_N + gbase[bb] + atomicAdd(&lcnt[bb], 1)] = e;
+            }
+            __syncthreads();
+            for (int r = threadIdx.x; r < nb2; r += 256) lcnt[r] = 0;
         }
         // exclusive prefix of the tile counts inside the chunk (wave scan + 4 wave totals)
         int incl = ntiles;

@@ -297,9 +297,12 @@ struct tf_ctx {
     int* blockTiles;
     int* blockOff;           // exclusive tile offset inside the entry's 256-entry chunk
     int* edChunk;            // tile total per chunk
+    uint4* edBins;           // k_ed_fill's per-row bins of boxes (tf_ed.h EdArgs::bins)
+    int* edBinCnt;
     int2* edSpill;           // per k_ed_fill row (ed_nrows): extent [0,x) x [0,y) of the pixels k_ed_fill wrote outside
                              // the /8 region (cleared by the next projection pass)
     int ed_lds_max_n;        // k_ed_fill reduces in LDS per /8 row up to this many visible entries
+    int integ_wg_frame;      // integration workgroups in the frame path (<= TF_INTEG_WG)
     // frame buffers
     uint16_t* depth_in;      // staging for host uploads / pitched input
     float* dists;
@@ -404,7 +407,8 @@ hipError_t tfk_render_snapshot(tf_ctx* c);   // render_snapshot as its own launc
 // CreateICPMaps + the frame end (tfk_reset_scene_on_failure) in one grid (the frame path)
 hipError_t tfk_icp_maps_end(tf_ctx* c, int slot);
 #define TF_END_BLOCKS 256        // workgroups of the frame-end / in-frame reset pass
-hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0);
+// keep_bins: the fill leaves the projection's bins in place (repeated fills of tf_time_stage)
+hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0, int keep_bins = 0);
 #define TF_ED_BLOCKS 256         // workgroups of the expected-depth projection pass
 #define ED_MAX_W 4096            // k_ed_fill: columns of a row held in LDS (wider images: atomics past it)
 #define ED_XROWS 8               // k_ed_fill: LDS rows below the /8 region (where boxes spill)
@@ -412,6 +416,7 @@ static inline int ed_nrows(int H) { const int n = (H - 1) / TF_SUBSAMPLE + 1 + E
 #define ED_LDS_MAX_N 16384       // k_ed_fill: per-/8-row LDS reduction up to this many visible entries
 hipError_t ed_spill_all(tf_ctx* c);   // mark the whole range buffer for clearing by the next projection pass
 #define TF_INTEG_WG 2048         // workgroups of the integration pass (grid-stride)
+#define TF_INTEG_WG_FRAME 768    // ... in the frame path (C2-size lists: 3 resident rounds of 256 WGs instead of 2048)
 hipError_t tfk_frame0_matrices(tf_ctx* c);
 // swapping (tf_swap.hip): reallocation of listed swapped-out entries (after the visible list),
 // and IntegrateGlobalIntoLocal + SaveToGlobalMemory (after integration)

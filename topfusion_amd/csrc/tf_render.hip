@@ -1017,8 +1017,8 @@ k_ed_project(EdArgs a, const TfDevState* __restrict__ st)
 #define ED_WIDE 4         // box columns in a row above which a wave fills it (queued)
 #endif
 #define ED_QUEUE 256      // queued segments per workgroup (beyond: filled by their thread)
-#define ED_THREADS 1024   // k_ed_fill workgroup: 8 records in flight per thread cover 8192 entries
-#define ED_INFLIGHT 8     // (16 measured slower: 8.5 vs 7.6 us at 6k entries)
+#define ED_THREADS 256    // k_ed_fill workgroup
+#define ED_INFLIGHT 4     // binned boxes in flight per thread (1024 per workgroup pass)
 // a segment: rows y0 .. y1, columns [x0, x1], z range as ints; lds: the workgroup's LDS row,
 // else the range image with device-scope atomics
 struct EdSeg { int y0, y1, x0, x1, zmin, zmax, lds; };
@@ -1038,20 +1038,16 @@ __global__ void __launch_bounds__(ED_THREADS)
 k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
 {
     // Everything this kernel reads was written by the previous launch, on other XCDs: the state
-    // words, the chunk totals and the first ED_INFLIGHT * ED_THREADS records are requested
-    // together (one round trip, not three dependent ones); entries past the count are discarded.
-    uint4 rec[ED_INFLIGHT];
-#pragma unroll
-    for (int k = 0; k < ED_INFLIGHT; ++k) {
-        const int i = threadIdx.x + k * ED_THREADS;
-        rec[k] = a.rec[i < a.vcap ? i : 0];
-    }
+    // words, the chunk totals and this row's two bin counts are requested together (one round
+    // trip); then the binned boxes (the second).
+    const int row = blockIdx.x, nrow = a.nrows;
     const unsigned cv = threadIdx.x < 64 && (int)threadIdx.x < a.nchunk_max ? (unsigned)a.chunk[threadIdx.x] : 0u;
+    const int cnt_row = a.bin_cnt[row], cnt_below = a.bin_cnt[nrow + row];
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
     const int n = st->noVisibleEntries;
     const int nchunks = (n + ED_CHUNK - 1) / ED_CHUNK;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int row = blockIdx.x, rc = a.rc, rr = a.rr, nrow = a.nrows;
+    const int rc = a.rc, rr = a.rr;
     if (n > a.lds_max_n) {
         // ---- large lists: one wave per block, its lanes over the block's pixel box, device atomics
         __shared__ unsigned red[ED_THREADS / 64];
@@ -1108,45 +1104,46 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
     if (row == 0 && threadIdx.x == 0) st->noTotalBlocks = (int)(capped ? a.cap : total);
     int xt = -1;                                 // last LDS column this thread touched
     int sx = 0, sy = 0;                          // extent of this thread's device-atomic writes
-    for (int i0 = threadIdx.x; i0 < n; i0 += ED_INFLIGHT * ED_THREADS) {
-        if (i0 != (int)threadIdx.x) {
+    // this row's boxes (bin row), then its share of the boxes reaching below the LDS rows
+    // (bin nrow + row); the projection pass binned them (ed_project_block)
+    for (int part = 0; part < 2; ++part) {
+        const int m = part ? cnt_below : cnt_row;
+        const uint4* bin = a.bins + (size_t)(part ? nrow + row : row) * ED_LDS_MAX_N;
+        for (int k0 = threadIdx.x; k0 < m; k0 += ED_INFLIGHT * ED_THREADS) {
+            uint4 e[ED_INFLIGHT];
 #pragma unroll
-            for (int k = 0; k < ED_INFLIGHT; ++k)        // (lists past ED_INFLIGHT * ED_THREADS)
-                rec[k] = a.rec[i0 + k * ED_THREADS < n ? i0 + k * ED_THREADS : i0];
-        }
+            for (int k = 0; k < ED_INFLIGHT; ++k) e[k] = bin[k0 + k * ED_THREADS < m ? k0 + k * ED_THREADS : k0];
 #pragma unroll
-        for (int k = 0; k < ED_INFLIGHT; ++k) {
-            const int i = i0 + k * ED_THREADS;
-            const uint4 r = rec[k];
-            if (i >= n || r.x == 0xffffffffu) continue;
-            const int bx = (int)(r.x & 0xffff), by = (int)(r.x >> 16), bz = (int)(r.y & 0xffff), bw = (int)(r.y >> 16);
-            const bool in_row = by <= row && row <= bw;
-            const bool below = bw >= nrow && i % nrow == row;  // rows past the LDS rows: by entry index
-            if (!in_row && !below) continue;
-            if (capped) {
-                const unsigned need = (unsigned)a.tiles[i], off = cpre[i / ED_CHUNK] + (unsigned)a.off[i];
-                if (!(need && off + need <= a.cap)) continue;
-            }
-            const int zmin = (int)r.z, zmax = (int)r.w;
-            if (in_row) {
-                const int x1 = bz < lw - 1 ? bz : lw - 1;
-                if (x1 >= bx) {
-                    xt = max(xt, x1);
-                    const int slot = x1 - bx + 1 > ED_WIDE ? atomicAdd(&nq, 1) : ED_QUEUE;
-                    if (slot < ED_QUEUE) q[slot] = EdSeg{row, row, bx, x1, zmin, zmax, 1};
-                    else for (int x = bx; x <= x1; ++x) { atomicMin(&lmin[x], zmin); atomicMax(&lmax[x], zmax); }
+            for (int k = 0; k < ED_INFLIGHT; ++k) {
+                if (k0 + k * ED_THREADS >= m) continue;
+                const uint4 r = e[k];
+                const int bx = (int)(r.x & 0xfffu), by = (int)((r.x >> 12) & 0xfffu);
+                const int bz = (int)(r.y & 0xfffu), bw = (int)((r.y >> 12) & 0xfffu);
+                const int i = (int)((r.x >> 24) | ((r.y >> 24) << 8));
+                if (capped) {
+                    const unsigned need = (unsigned)a.tiles[i], off = cpre[i / ED_CHUNK] + (unsigned)a.off[i];
+                    if (!(need && off + need <= a.cap)) continue;
                 }
-                if (bz >= lw) {                  // (images wider than ED_MAX_W)
-                    sx = max(sx, bz + 1); sy = max(sy, row + 1);
-                    ed_fill_global(a, row, row, bx > lw ? bx : lw, bz, zmin, zmax, 0, 1);
+                const int zmin = (int)r.z, zmax = (int)r.w;
+                if (!part) {                     // by <= row <= bw
+                    const int x1 = bz < lw - 1 ? bz : lw - 1;
+                    if (x1 >= bx) {
+                        xt = max(xt, x1);
+                        const int slot = x1 - bx + 1 > ED_WIDE ? atomicAdd(&nq, 1) : ED_QUEUE;
+                        if (slot < ED_QUEUE) q[slot] = EdSeg{row, row, bx, x1, zmin, zmax, 1};
+                        else for (int x = bx; x <= x1; ++x) { atomicMin(&lmin[x], zmin); atomicMax(&lmax[x], zmax); }
+                    }
+                    if (bz >= lw) {              // (images wider than ED_MAX_W)
+                        sx = max(sx, bz + 1); sy = max(sy, row + 1);
+                        ed_fill_global(a, row, row, bx > lw ? bx : lw, bz, zmin, zmax, 0, 1);
+                    }
+                } else {                         // rows past the LDS rows: device atomics
+                    const int y0 = by > nrow ? by : nrow;
+                    sx = max(sx, bz + 1); sy = max(sy, bw + 1);
+                    const int slot = (bz - bx + 1) * (bw - y0 + 1) > 64 ? atomicAdd(&nq, 1) : ED_QUEUE;
+                    if (slot < ED_QUEUE) q[slot] = EdSeg{y0, bw, bx, bz, zmin, zmax, 0};
+                    else ed_fill_global(a, y0, bw, bx, bz, zmin, zmax, 0, 1);
                 }
-            }
-            if (below) {
-                const int y0 = by > nrow ? by : nrow;
-                sx = max(sx, bz + 1); sy = max(sy, bw + 1);
-                const int slot = (bz - bx + 1) * (bw - y0 + 1) > 64 ? atomicAdd(&nq, 1) : ED_QUEUE;
-                if (slot < ED_QUEUE) q[slot] = EdSeg{y0, bw, bx, bz, zmin, zmax, 0};
-                else ed_fill_global(a, y0, bw, bx, bz, zmin, zmax, 0, 1);
             }
         }
     }
@@ -1173,6 +1170,10 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
         int2 e = make_int2(sxy[0], sxy[1]);      // outside the /8 region: this row past rc, or all of it
         if (xend > (row < rr ? rc : 0)) { e.x = max(e.x, xend); e.y = max(e.y, row + 1); }
         a.spill[row] = e;
+        if (!a.keep_bins) {                      // the bins are consumed (every thread read the counts)
+            a.bin_cnt[row] = 0;
+            a.bin_cnt[nrow + row] = 0;
+        }
     }
 }
 
@@ -1191,6 +1192,7 @@ void tf_ed_args(tf_ctx* c, EdArgs* out)
     a.hash = c->hash; a.visibleIds = c->visibleIds; a.range = (float2*)c->range;
     a.rec = c->blockRec; a.tiles = c->blockTiles; a.off = c->blockOff; a.chunk = c->edChunk;
     a.spill = c->edSpill;
+    a.bins = c->edBins; a.bin_cnt = c->edBinCnt; a.keep_bins = 0;
     a.W = c->W; a.H = c->H;
     a.rc = (c->W - 1) / TF_SUBSAMPLE + 1; a.rr = (c->H - 1) / TF_SUBSAMPLE + 1;
     a.nrows = ed_nrows(c->H);
@@ -1202,10 +1204,11 @@ void tf_ed_args(tf_ctx* c, EdArgs* out)
 }
 
 // project_done: k_ed_project's pass already ran in the frame's k_integrate grid (frame path)
-hipError_t tfk_expected_depths(tf_ctx* c, int project_done)
+hipError_t tfk_expected_depths(tf_ctx* c, int project_done, int keep_bins)
 {
     EdArgs a;
     tf_ed_args(c, &a);
+    a.keep_bins = keep_bins;
     if (!project_done) hipLaunchKernelGGL(k_ed_project, dim3(TF_ED_BLOCKS), dim3(256), 0, c->stream, a, c->st);
     // one workgroup per LDS row (the atomic path grid-strides the same grid)
     tf_launch(c, k_ed_fill, dim3(a.nrows), dim3(ED_THREADS), 0, a, c->st);

@@ -1051,7 +1051,7 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
     EdArgs ed = {};
     // 2048 workgroups, 8 per CU (7 are resident at once under the SGPR budget): measured faster
     // on the C3I scene than a grid of exactly the resident count (2.43 vs 2.75 ms)
-    const int nwg = TF_INTEG_WG;
+    const int nwg = frame_path ? c->integ_wg_frame : TF_INTEG_WG;
     long long* count = (frame_path ? c->count_lanes : 1) ? c->integ_cnt : nullptr;
     const dim3 b(256);
     if (with_ed) {
