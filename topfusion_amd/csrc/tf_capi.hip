@@ -152,7 +152,7 @@ static void ctx_free(tf_ctx* c)
     if (c->caller_ev) (void)hipEventDestroy(c->caller_ev);
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
                      c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
-                     c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->edBins, c->edBinCnt, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
+                     c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->edBins, c->edBinCnt, c->edDone, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
                      c->vba_rgb_guard, c->rgb_in, c->integ_cnt };
     for (void* b : bufs) if (b) (void)hipFree(b);
@@ -254,6 +254,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->edSpill, sizeof(int2) * (size_t)ed_nrows(c->H));
     ALLOC(c->edBins, sizeof(uint4) * 2 * (size_t)ed_nrows(c->H) * ED_LDS_MAX_N);
     ALLOC(c->edBinCnt, sizeof(int) * 2 * (size_t)ed_nrows(c->H));
+    ALLOC(c->edDone, 64);
     ALLOC(c->depth_in, sizeof(uint16_t) * npx);
     ALLOC(c->dists, sizeof(float) * npx);
     {   // each map's three pyramid levels are contiguous in one allocation
@@ -319,6 +320,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipMemsetAsync(c->visibleIds, 0, sizeof(int) * (size_t)pin->vis_capacity, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->raycast, 0, sizeof(float) * 4 * npx, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->edBinCnt, 0, sizeof(int) * 2 * (size_t)ed_nrows(c->H), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->edDone, 0, 64, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->grey, 0, sizeof(uchar4) * npx, c->stream);
     for (int l = 0; l < TF_LEVELS && e == hipSuccess; ++l) {
         size_t n = (size_t)c->lw[l] * c->lh[l];
@@ -411,6 +413,7 @@ static void swap_pyramids(tf_ctx* c)
     do {                                                                                      \
         const bool timed_ = c->prof_slot_on[slot] && ((c->prof_mask >> (id)) & 1u);          \
         const bool ext_ = timed_ && stage_single(c, id);                                      \
+        if (timed_) c->prof_slot_stages[slot] |= 1u << (id);                                  \
         if (ext_) { c->ev_start = prof_event(c, slot, 2 * (id)); c->ev_stop = prof_event(c, slot, 2 * (id) + 1); } \
         else if (timed_) TF_CHECK(hipEventRecord(prof_event(c, slot, 2 * (id)), (strm)));     \
         const hipError_t se_ = (expr);                                                        \
@@ -453,6 +456,7 @@ static tf_status prof_collect(tf_ctx* c, int first, int n, const int* ok, const 
     for (int f = 0; f < n; ++f)
         for (int i = 0; i < TF_NUM_STAGES; ++i) {
             if (!c->prof_slot_on[first + f] || !((c->prof_mask >> i) & 1u) || !stage_ran(i, mode[f], ok[f])) continue;
+            if (!((c->prof_slot_stages[first + f] >> i) & 1u)) continue;      // not enqueued as its own stage
             if (i == TF_STAGE_PREPROCESS && !c->prof_slot_pre[first + f]) continue;   // done by the previous frame
             if (i == TF_STAGE_RAYCAST_RENDER) continue;                       // fused into RAYCAST_ICP
             float ms = 0.f;
@@ -506,6 +510,7 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     uint16_t* d0 = plan->d0 ? plan->d0 : c->d0_buf[0];
     c->prof_slot_on[slot] = c->prof_enabled && (c->prof_seq++ % c->prof_period) == 0;
     c->prof_slot_pre[slot] = !plan->pre_done;
+    c->prof_slot_stages[slot] = 0;
     // preprocessing (topfu.cpp:166-197)
     if (!plan->pre_done) STAGE(TF_STAGE_PREPROCESS, tfk_preprocess(c, depth, pitch, c->stream, d0));
     c->depth_pyr[0] = d0;
@@ -517,9 +522,12 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     // (+ CreateExpectedDepths' projection pass in the same grid)
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1, 1));              // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)
     if (c->p.use_swapping) TF_CHECK(tfk_swap(c));                   // swap in / out after integration
-    STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c, 1));     // topfu.cpp:306
+    // CreateExpectedDepths (topfu.cpp:306): its projection ran in k_integrate's grid; its fill runs
+    // in k_raycast_pair's grid when the frame is narrow enough (tfk_ed_fused), else on its own
+    const int fuse_ed = tfk_ed_fused(c);
+    if (!fuse_ed) STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c, 1));
     // CreateICPMaps' raycast + renderImage (topfu.cpp:284-285 + 307) in one launch (snapshot range)
-    STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch));
+    STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch, fuse_ed));
     // renderICP + resizePointsNormals (topfu.cpp:308-309) + the frame end (topfu.cpp:263-264)
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps_end(c, slot));
     return TF_OK;

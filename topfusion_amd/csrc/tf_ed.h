@@ -15,6 +15,7 @@ struct EdArgs {
                          // share of the boxes reaching below the LDS rows (entry index % nrows == r)
     int* bin_cnt;        // [2 * nrows] entries in each bin (the fill's workgroup r zeroes its two)
     int keep_bins;       // the fill leaves the counts (tf_time_stage's repeated fills)
+    unsigned* done;      // fill fused into k_raycast_pair: its atomic path counts finished rows here
     int W, H;
     int rc, rr;          // the /8 region: (W-1)/8+1 columns, (H-1)/8+1 rows
     int nrows;           // k_ed_fill's LDS rows (ed_nrows: rr + ED_XROWS, at most H)

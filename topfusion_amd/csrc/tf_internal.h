@@ -299,6 +299,7 @@ struct tf_ctx {
     int* edChunk;            // tile total per chunk
     uint4* edBins;           // k_ed_fill's per-row bins of boxes (tf_ed.h EdArgs::bins)
     int* edBinCnt;
+    unsigned* edDone;        // the fused fill's atomic path: rows done (k_raycast_pair)
     int2* edSpill;           // per k_ed_fill row (ed_nrows): extent [0,x) x [0,y) of the pixels k_ed_fill wrote outside
                              // the /8 region (cleared by the next projection pass)
     int ed_lds_max_n;        // k_ed_fill reduces in LDS per /8 row up to this many visible entries
@@ -338,6 +339,7 @@ struct tf_ctx {
     long long prof_seq;      // frames enqueued since profiling was configured
     unsigned char prof_slot_on[TF_PROF_RING];   // batch slot carries stage events
     unsigned char prof_slot_pre[TF_PROF_RING];  // batch slot ran its own preprocessing (no lookahead)
+    unsigned prof_slot_stages[TF_PROF_RING];    // batch slot: the stages whose events were recorded
     hipEvent_t prof_ev[2 * TF_NUM_STAGES * TF_PROF_RING];
     // a single-kernel stage being timed: its launch (tf_launch) carries these events, which
     // hipExtLaunchKernelGGL ties to the dispatch's own begin / end (what rocprofv3 reports);
@@ -401,7 +403,10 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0, int with_ed = 0);
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_type(tf_ctx* c, int type);   // RenderImage pixel stage (tf_render_type) on raycast
 // CreateICPMaps raycast + renderImage, one launch (frame path); next: + that frame's dists/pyramid/normals
-hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = TfAhead{}, size_t pitch = 0);   // + dists/pyramid/normals of pyr, bilateral of bil
+// + dists/pyramid/normals of pyr, bilateral of bil; fuse_ed: CreateExpectedDepths' fill in the same
+// grid (frame path, when tfk_ed_fused: then no separate tfk_expected_depths launch)
+hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = TfAhead{}, size_t pitch = 0, int fuse_ed = 0);
+int tfk_ed_fused(const tf_ctx* c);
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_render_snapshot(tf_ctx* c);   // render_snapshot as its own launch
 // CreateICPMaps + the frame end (tfk_reset_scene_on_failure) in one grid (the frame path)

@@ -30,8 +30,16 @@ struct BilArgs {
     uint16_t* dst;                      // level-0 depth (bilateral + truncation)
 };
 
+// the bilateral pass's LDS (a caller-provided block, so a fused kernel can overlay it with the
+// LDS of its other branches)
+struct BilLds {
+    uint16_t tile[PRE_TY + 2 * HALO][PRE_TX + 2 * HALO + 2];
+    float ftile[PRE_TY + 2 * HALO][PRE_TX + 2 * HALO + 2];
+    float sptab[2 * HALO + 1][2 * HALO + 2];      // RN(space2 * ss) by (y-cy+3, x-cx+3)
+};
+
 // tile (bx, by) of k_dists_bilateral; every thread of the workgroup calls it
-__device__ __forceinline__ void bilateral_block(const BilArgs& b, int bx, int by)
+__device__ __forceinline__ void bilateral_block(const BilArgs& b, int bx, int by, BilLds& L)
 {
     const uint16_t* __restrict__ src = b.src;
     const size_t pitch = b.pitch;
@@ -39,9 +47,9 @@ __device__ __forceinline__ void bilateral_block(const BilArgs& b, int bx, int by
     const float ss = b.ss, sd = b.sd;
     float* __restrict__ dists = b.dists;
     uint16_t* __restrict__ dst = b.dst;
-    __shared__ uint16_t tile[PRE_TY + 2 * HALO][PRE_TX + 2 * HALO + 2];
-    __shared__ float ftile[PRE_TY + 2 * HALO][PRE_TX + 2 * HALO + 2];
-    __shared__ float sptab[2 * HALO + 1][2 * HALO + 2];      // RN(space2 * ss) by (y-cy+3, x-cx+3)
+    auto& tile = L.tile;
+    auto& ftile = L.ftile;
+    auto& sptab = L.sptab;
     const int tx = threadIdx.x & (PRE_TX - 1), ty = threadIdx.x / PRE_TX;
     const int x0 = bx * PRE_TX, y0 = by * PRE_TY;
     bool big = false;
@@ -207,11 +215,16 @@ __device__ __forceinline__ void pn_pixel(const T* lds, int ld, int ox, int oy, c
 #define PN_R0 45                       // level-0 staging: [X0-6, X0+39)
 #define PN_R1 21                       // level-1 staging: [X1-2, X1+19)
 #define PN_R2 9                        // level-2 staging: [X2, X2+9)
-__device__ __forceinline__ void pyr_normals_block(const PyrArgs& a, int bx, int by)
+struct PnLds {
+    uint16_t s0[PN_R0 * PN_R0];
+    int s1[PN_R1 * PN_R1];
+    int s2[PN_R2 * PN_R2];
+};
+__device__ __forceinline__ void pyr_normals_block(const PyrArgs& a, int bx, int by, PnLds& L)
 {
-    __shared__ uint16_t s0[PN_R0 * PN_R0];
-    __shared__ int s1[PN_R1 * PN_R1];
-    __shared__ int s2[PN_R2 * PN_R2];
+    uint16_t* s0 = L.s0;
+    int* s1 = L.s1;
+    int* s2 = L.s2;
     const int W0 = a.w[0], H0 = a.h[0], W1 = a.w[1], H1 = a.h[1], W2 = a.w[2], H2 = a.h[2];
     const int X0 = bx * PN_T0, Y0 = by * PN_T0;
     const int X1 = X0 / 2, Y1 = Y0 / 2, X2 = X0 / 4, Y2 = Y0 / 4;

@@ -9,8 +9,16 @@
 // VALU-bound (49 canonical exp per pixel).
 #include "tf_preproc.h"
 
-__global__ void __launch_bounds__(256) k_dists_bilateral(BilArgs b) { bilateral_block(b, blockIdx.x, blockIdx.y); }
-__global__ void __launch_bounds__(256) k_pyr_normals(PyrArgs a) { pyr_normals_block(a, blockIdx.x, blockIdx.y); }
+__global__ void __launch_bounds__(256) k_dists_bilateral(BilArgs b)
+{
+    __shared__ BilLds L;
+    bilateral_block(b, blockIdx.x, blockIdx.y, L);
+}
+__global__ void __launch_bounds__(256) k_pyr_normals(PyrArgs a)
+{
+    __shared__ PnLds L;
+    pyr_normals_block(a, blockIdx.x, blockIdx.y, L);
+}
 
 // the preprocessing arguments of raw frame `depth`; lookahead: the frame-path split in which
 // the bilateral pass leaves dists alone (the current frame's allocation / integration still

@@ -270,10 +270,9 @@ struct Ray {
     bool active;             // inside castRay's while loop
 };
 
-__device__ __forceinline__ void ray_init(const RayArgs& a, const float* invM, int x, int y, Ray& R)
+// vf: the range image at the ray's /8 pixel (renderingRangeImage[locId2], :104-106)
+__device__ __forceinline__ void ray_init(const RayArgs& a, const float* invM, int x, int y, float2 vf, Ray& R)
 {
-    int locId2 = (int)floorf((float)x / TF_SUBSAMPLE) + (int)floorf((float)y / TF_SUBSAMPLE) * a.W;
-    float2 vf = a.range[locId2];
     float r[3], ps[3], pe[3];
     float pz = vf.x;
     float px = pz * (((float)x + a.ncx) * a.invfx);
@@ -367,10 +366,10 @@ __device__ __forceinline__ float interp_at(const SceneView& s, const float* pt, 
 // only): more waves resident to hide the dependent loads.  Values, visibility marks and the
 // IndexCache follow castRay's serial reads exactly (VisualisationEngine_Shared.hpp:117-160).
 template <bool MARK>
-__device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* invM, int x, int y, float* pt)
+__device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* invM, int x, int y, float2 vf, float* pt)
 {
     Ray R;
-    ray_init(a, invM, x, y, R);
+    ray_init(a, invM, x, y, vf, R);
     const float stepScale = a.mu * a.oneOverVoxelSize;
 #ifdef TF_RAY_STATS
     unsigned n_free = 0, n_found = 0;
@@ -424,9 +423,9 @@ __device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* i
 }
 
 template <bool MARK>
-__device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, int x, int y, float* pt)
+__device__ __forceinline__ float ray_march(const RayArgs& a, const float* invM, int x, int y, float2 vf, float* pt)
 {
-    return ray_march_lite<MARK>(a, invM, x, y, pt);
+    return ray_march_lite<MARK>(a, invM, x, y, vf, pt);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -529,22 +528,23 @@ __device__ __forceinline__ int xcd_tile(int bid, int n)
 
 // MODE 0: castRay<false> -> point image; 1: castRay<true> (visibility marks) -> point image
 // (CreateICPMaps); 2: castRay<false> + renderGrey fused (renderImage in the frame path).
-template <int MODE>
-__device__ __forceinline__ void raycast_tile(const RayArgs& a, const TfDevState* __restrict__ st, int bid,
-                                             int tiles_x, int n_tiles)
+// vtab: the caller's LDS for MODE 2's gradient (256 * VTAB_STRIDE ints).  rng (the frame kernel's
+// CreateICPMaps rays with CreateExpectedDepths' fill fused in): the tile's four /8 range pixels,
+// computed by the caller; else the range image is read.
+template <int MODE, bool RNG_LDS = false>
+__device__ __forceinline__ void raycast_tile(const RayArgs& a, const TfDevState* __restrict__ st, int tile,
+                                             int tiles_x, int* vtab, const float2* rng = nullptr)
 {
-    // the frame's renderImage (MODE 2) reads the snapshot render_snapshot took (tf_internal.h)
-    if (MODE == 2 ? !st->render_go : (st->abort || st->mode == 0)) return;   // ICP failed, or frame 0
-    const int tile = xcd_tile(bid, n_tiles);            // grid padded to a multiple of 8
-    if (tile < 0) return;
-    const int x = (tile % tiles_x) * 16 + (threadIdx.x & 15), y = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
+    const int x = tx * 16 + (threadIdx.x & 15), y = ty * 16 + (threadIdx.x >> 4);
     if (x >= a.W || y >= a.H) return;
+    const float2 vf = RNG_LDS ? rng[((y >> 3) - 2 * ty) * 2 + ((x >> 3) - 2 * tx)]
+                              : a.range[(int)floorf((float)x / TF_SUBSAMPLE) + (int)floorf((float)y / TF_SUBSAMPLE) * a.W];
     const float* M = MODE == 2 ? st->M_render : st->M_ray;
     float pt[3];
-    const float w = ray_march<MODE == 1>(a, M, x, y, pt);
+    const float w = ray_march<MODE == 1>(a, M, x, y, vf, pt);
     if (MODE == 2) {
         // renderImage: lightSource = -Vector3f(pose.getColumn(2)) (VisualisationEngine_CUDA.cu:243)
-        __shared__ int vtab[256 * VTAB_STRIDE];
         unsigned char v = 0;
         if (w > 0) v = grey_pixel(a.s, pt, -M[8], -M[9], -M[10], &vtab[threadIdx.x * VTAB_STRIDE]);
         a.grey[x + y * a.W] = make_uchar4(v, v, v, v);
@@ -553,34 +553,23 @@ __device__ __forceinline__ void raycast_tile(const RayArgs& a, const TfDevState*
     }
 }
 
+// the early exits every raycast workgroup takes first (uniform): the frame's renderImage (MODE 2)
+// reads the snapshot render_snapshot took (tf_internal.h); the others run on tracked frames only
+template <int MODE>
+__device__ __forceinline__ bool raycast_go(const TfDevState* __restrict__ st)
+{
+    return MODE == 2 ? st->render_go != 0 : !(st->abort || st->mode == 0);
+}
+
 // Distinct instantiations also give each use its own kernel name in rocprof.
 template <int MODE>
 __global__ void __launch_bounds__(256)
 k_raycast(RayArgs a, const TfDevState* __restrict__ st, int tiles_x, int n_tiles)
 {
-    raycast_tile<MODE>(a, st, blockIdx.x, tiles_x, n_tiles);
-}
-
-// The frame's two raycasts in one launch: the first half of the grid casts CreateICPMaps'
-// rays (castRay<true>, new range image), the second half renderImage's (castRay<false> +
-// grey, range snapshot).  Neither writes what the other reads, and a launch's run time is its
-// slowest waves' ray length: the halves fill each other's tails instead of each kernel
-// draining alone.  (Measured: marching both rays of a pixel interleaved in one thread, sharing
-// each step's round trips, is slower -- 142 VGPRs halve the resident waves.)
-__global__ void __launch_bounds__(256)
-k_raycast_pair(RayArgs ai, RayArgs ar, const TfDevState* __restrict__ st, int tiles_x, int n_tiles, int nb,
-               PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx)
-{
-    const int b = (int)blockIdx.x;
-    if (b < nb) raycast_tile<1>(ai, st, b, tiles_x, n_tiles);
-    else if (b < 2 * nb) raycast_tile<2>(ar, st, b - nb, tiles_x, n_tiles);
-    // Later frames of the batch in this grid's tail, not gated by this frame's abort: the next
-    // frame's computeDists + pyramids + normals (this frame's allocation and integration, the
-    // last readers of dists and of the current maps, are done; its level-0 depth was filtered
-    // a launch or more ago), then the bilateral pass of the frame after it (into the other
-    // level-0 buffer: this frame's, whose last reader was its own pyramid pass)
-    else if (b < 2 * nb + n_pyr) pyr_normals_block(pyr, (b - 2 * nb) % pyr_gx, (b - 2 * nb) / pyr_gx);
-    else bilateral_block(bil, (b - 2 * nb - n_pyr) % bil_gx, (b - 2 * nb - n_pyr) / bil_gx);
+    if (!raycast_go<MODE>(st)) return;
+    const int tile = xcd_tile(blockIdx.x, n_tiles);            // grid padded to a multiple of 8
+    if (tile < 0) return;
+    raycast_tile<MODE>(a, st, tile, tiles_x, nullptr);
 }
 
 static void ray_args(tf_ctx* c, RayArgs& a)
@@ -623,38 +612,6 @@ hipError_t tfk_render_snapshot(tf_ctx* c)
                        (float2*)c->range_render, c->W, c->H);
     return hipGetLastError();
 }
-
-// CreateICPMaps' raycast + the frame's renderImage in one launch (after CreateExpectedDepths):
-// the renderImage half reads the range-image snapshot (render_snapshot)
-hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch)
-{
-    RayArgs ai, ar;
-    ray_args(c, ai);
-    ai.visType = c->visType;
-    ray_args(c, ar);
-    ar.range = (const float2*)c->range_render;
-    ar.grey = c->grey;
-    const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty;
-    const int nb = (n + 7) / 8 * 8;
-    BilArgs bb = BilArgs{}, bx; PyrArgs pp = PyrArgs{}, px;
-    int n_pyr = 0, pyr_gx = 1, n_bil = 0, bil_gx = 1;
-    if (pyr.src) {
-        const hipError_t e = tf_pre_args(c, pyr.src, pitch, 1, pyr.d0, &bx, &pp);
-        if (e != hipSuccess) return e;
-        pyr_gx = tf_div_up(c->W, PN_T0);
-        n_pyr = pyr_gx * tf_div_up(c->H, PN_T0);
-    }
-    if (bil.src) {
-        const hipError_t e = tf_pre_args(c, bil.src, pitch, 1, bil.d0, &bb, &px);
-        if (e != hipSuccess) return e;
-        bil_gx = tf_div_up(c->W, PRE_TX);
-        n_bil = bil_gx * tf_div_up(c->H, PRE_TY);
-    }
-    tf_launch(c, k_raycast_pair, dim3(2 * nb + n_pyr + n_bil), dim3(256), 0, ai, ar, c->st, tx, n, nb,
-                       pp, n_pyr, pyr_gx, bb, bil_gx);
-    return hipGetLastError();
-}
-
 
 // ---------------------------------------------------------------------------------------
 // RenderImage_common's pixel stages (VisualisationEngine_CUDA.cu:254-290) on the raycast image:
@@ -1034,13 +991,29 @@ __device__ __forceinline__ void ed_fill_global(const EdArgs& a, int y0, int y1, 
     }
 }
 
-__global__ void __launch_bounds__(ED_THREADS)
-k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
+// k_ed_fill's workgroup `row` of `nfill` (its own launch, or the leading workgroups of
+// k_raycast_pair in the frame path); LW: LDS columns (wider rows take device atomics past them).
+// own_zero: the workgroup empties its two bins at the end (else the frame end does, after the
+// raycast's ICP tiles have read them too).  With `done` set, the atomic path counts its finished
+// workgroups there (release) for the ICP tiles that wait on the range image.
+template <int LW>
+struct EdLds {
+    int lmin[LW], lmax[LW];
+    unsigned cpre[ED_LDS_MAX_N / ED_CHUNK];      // tiles of chunks before chunk c (nchunks <= 64)
+    EdSeg q[ED_QUEUE];
+    int nq, sxy[3];
+    unsigned total_s;
+    unsigned red[ED_THREADS / 64];
+};
+
+template <int LW>
+__device__ __forceinline__ void ed_fill_block(const EdArgs& a, TfDevState* __restrict__ st, int row, int nfill,
+                                              EdLds<LW>& L, bool own_zero)
 {
-    // Everything this kernel reads was written by the previous launch, on other XCDs: the state
+    // Everything this reads was written by the previous launch, on other XCDs: the state
     // words, the chunk totals and this row's two bin counts are requested together (one round
     // trip); then the binned boxes (the second).
-    const int row = blockIdx.x, nrow = a.nrows;
+    const int nrow = a.nrows;
     const unsigned cv = threadIdx.x < 64 && (int)threadIdx.x < a.nchunk_max ? (unsigned)a.chunk[threadIdx.x] : 0u;
     const int cnt_row = a.bin_cnt[row], cnt_below = a.bin_cnt[nrow + row];
     if (st->abort || st->mode == 0) return;          // ICP failed, or frame 0 (no rendering)
@@ -1050,7 +1023,7 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
     const int rc = a.rc, rr = a.rr;
     if (n > a.lds_max_n) {
         // ---- large lists: one wave per block, its lanes over the block's pixel box, device atomics
-        __shared__ unsigned red[ED_THREADS / 64];
+        unsigned* red = L.red;
         unsigned part = 0;
         for (int c = threadIdx.x; c < nchunks; c += ED_THREADS) part += (unsigned)a.chunk[c];
         for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d, 64);
@@ -1059,11 +1032,11 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
         unsigned total = 0;
         for (int w = 0; w < ED_THREADS / 64; ++w) total += red[w];
         const bool capped = total > a.cap;
-        if (blockIdx.x == 0 && threadIdx.x == 0) st->noTotalBlocks = (int)(capped ? a.cap : total);
+        if (row == 0 && threadIdx.x == 0) st->noTotalBlocks = (int)(capped ? a.cap : total);
         unsigned cprefix = 0;                    // tiles of chunks [0, cdone)
         int cdone = 0;
-        const int nw = gridDim.x * (ED_THREADS / 64);
-        for (int i = blockIdx.x * (ED_THREADS / 64) + wv; i < n; i += nw) {
+        const int nw = nfill * (ED_THREADS / 64);
+        for (int i = row * (ED_THREADS / 64) + wv; i < n; i += nw) {
             const uint4 r = a.rec[i];
             if (r.x == 0xffffffffu) continue;
             if (capped) {
@@ -1076,16 +1049,25 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
                            (int)r.z, (int)r.w, lane, 64);
         }
         // the next projection pass clears the whole buffer (every pixel may have been written)
-        if (threadIdx.x == 0) a.spill[blockIdx.x] = blockIdx.x == 0 ? make_int2(a.W, a.H) : make_int2(0, 0);
+        if (threadIdx.x == 0) a.spill[row] = row == 0 ? make_int2(a.W, a.H) : make_int2(0, 0);
+        if (a.done) {                            // the range image is final once every row has counted
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                atomicAdd(a.done, 1u);
+            }
+        }
         return;
     }
     // ---- one image row per workgroup, reduced in LDS over the full width ----
-    const int lw = a.W < ED_MAX_W ? a.W : ED_MAX_W;    // LDS columns
-    __shared__ int lmin[ED_MAX_W], lmax[ED_MAX_W];
-    __shared__ unsigned cpre[ED_LDS_MAX_N / ED_CHUNK];   // tiles of chunks before chunk c (nchunks <= 64)
-    __shared__ EdSeg q[ED_QUEUE];
-    __shared__ int nq, sxy[3];
-    __shared__ unsigned total_s;
+    const int lw = a.W < LW ? a.W : LW;         // LDS columns
+    int* lmin = L.lmin;
+    int* lmax = L.lmax;
+    unsigned* cpre = L.cpre;
+    EdSeg* q = L.q;
+    int& nq = L.nq;
+    int* sxy = L.sxy;
+    unsigned& total_s = L.total_s;
     for (int x = threadIdx.x; x < lw; x += ED_THREADS) { lmin[x] = __float_as_int(TF_FAR_AWAY); lmax[x] = __float_as_int(TF_VERY_CLOSE); }
     if (threadIdx.x < 64) {                      // wave 0: chunk totals -> tile total + chunk prefix
         const unsigned v = (int)threadIdx.x < nchunks ? cv : 0u;
@@ -1170,11 +1152,18 @@ k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
         int2 e = make_int2(sxy[0], sxy[1]);      // outside the /8 region: this row past rc, or all of it
         if (xend > (row < rr ? rc : 0)) { e.x = max(e.x, xend); e.y = max(e.y, row + 1); }
         a.spill[row] = e;
-        if (!a.keep_bins) {                      // the bins are consumed (every thread read the counts)
+        if (own_zero) {                          // the bins are consumed (every thread read the counts)
             a.bin_cnt[row] = 0;
             a.bin_cnt[nrow + row] = 0;
         }
     }
+}
+
+__global__ void __launch_bounds__(ED_THREADS)
+k_ed_fill(EdArgs a, TfDevState* __restrict__ st)
+{
+    __shared__ EdLds<ED_MAX_W> L;
+    ed_fill_block<ED_MAX_W>(a, st, blockIdx.x, gridDim.x, L, !a.keep_bins);
 }
 
 hipError_t ed_spill_all(tf_ctx* c)
@@ -1192,7 +1181,7 @@ void tf_ed_args(tf_ctx* c, EdArgs* out)
     a.hash = c->hash; a.visibleIds = c->visibleIds; a.range = (float2*)c->range;
     a.rec = c->blockRec; a.tiles = c->blockTiles; a.off = c->blockOff; a.chunk = c->edChunk;
     a.spill = c->edSpill;
-    a.bins = c->edBins; a.bin_cnt = c->edBinCnt; a.keep_bins = 0;
+    a.bins = c->edBins; a.bin_cnt = c->edBinCnt; a.keep_bins = 0; a.done = nullptr;
     a.W = c->W; a.H = c->H;
     a.rc = (c->W - 1) / TF_SUBSAMPLE + 1; a.rr = (c->H - 1) / TF_SUBSAMPLE + 1;
     a.nrows = ed_nrows(c->H);
@@ -1212,5 +1201,213 @@ hipError_t tfk_expected_depths(tf_ctx* c, int project_done, int keep_bins)
     if (!project_done) hipLaunchKernelGGL(k_ed_project, dim3(TF_ED_BLOCKS), dim3(256), 0, c->stream, a, c->st);
     // one workgroup per LDS row (the atomic path grid-strides the same grid)
     tf_launch(c, k_ed_fill, dim3(a.nrows), dim3(ED_THREADS), 0, a, c->st);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// The frame's raycasts in one launch (k_raycast_pair), with CreateExpectedDepths' fill fused in
+// ---------------------------------------------------------------------------------------
+#define ED_PAIR_W 1280   // the fused fill's LDS columns: frames up to 1280 wide (wider: k_ed_fill)
+
+// the four /8 range pixels (2tx..2tx+1, 2ty..2ty+1) under a 16x16 ray tile from the projection's
+// bins: for each, the min / max over the boxes of its row's bin that cover its column and pass
+// the MAX_RENDERING_BLOCKS check -- exactly the value ed_fill_block's LDS row gets (the same
+// boxes, min / max commute), so the tile's rays need not wait for the fill
+struct IrLds {
+    unsigned cpre[ED_LDS_MAX_N / ED_CHUNK];
+    unsigned total;
+    int mn[4][4], mx[4][4];      // [wave][pixel]
+    float2 rng[4];
+};
+__device__ __forceinline__ void ed_tile_range(const EdArgs& a, int X0, int Y0, int n, IrLds& L)
+{
+    const int nchunks = (n + ED_CHUNK - 1) / ED_CHUNK;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // one round trip: the chunk totals and the two bin counts
+    const unsigned cv = threadIdx.x < 64 && (int)threadIdx.x < nchunks ? (unsigned)a.chunk[threadIdx.x] : 0u;
+    const int c0 = a.bin_cnt[Y0], c1 = a.bin_cnt[Y0 + 1];
+    if (threadIdx.x < 64) {                      // chunk totals -> tile total + chunk prefix
+        unsigned incl = cv;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned u = __shfl_up(incl, d, 64);
+            if ((int)threadIdx.x >= d) incl += u;
+        }
+        L.cpre[threadIdx.x] = incl - cv;
+        if (threadIdx.x == 63) L.total = incl;
+    }
+    __syncthreads();
+    const bool capped = L.total > a.cap;
+    int mn[4], mx[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) { mn[p] = __float_as_int(TF_FAR_AWAY); mx[p] = __float_as_int(TF_VERY_CLOSE); }
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+        const int m = part ? c1 : c0;
+        const uint4* bin = a.bins + (size_t)(Y0 + part) * ED_LDS_MAX_N;
+        for (int k0 = threadIdx.x; k0 < m; k0 += 4 * 256) {
+            uint4 e[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) e[k] = bin[k0 + k * 256 < m ? k0 + k * 256 : k0];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k0 + k * 256 >= m) continue;
+                const uint4 r = e[k];
+                const int bx = (int)(r.x & 0xfffu), bz = (int)(r.y & 0xfffu);
+                if (bz < X0 || bx > X0 + 1) continue;
+                if (capped) {
+                    const int i = (int)((r.x >> 24) | ((r.y >> 24) << 8));
+                    const unsigned need = (unsigned)a.tiles[i], off = L.cpre[i / ED_CHUNK] + (unsigned)a.off[i];
+                    if (!(need && off + need <= a.cap)) continue;
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    if (bx <= X0 + c && X0 + c <= bz) {
+                        mn[2 * part + c] = min(mn[2 * part + c], (int)r.z);
+                        mx[2 * part + c] = max(mx[2 * part + c], (int)r.w);
+                    }
+            }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            mn[p] = min(mn[p], __shfl_xor(mn[p], o, 64));
+            mx[p] = max(mx[p], __shfl_xor(mx[p], o, 64));
+        }
+    if (lane == 0)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) { L.mn[wv][p] = mn[p]; L.mx[wv][p] = mx[p]; }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const int p = threadIdx.x;
+        const int a0 = min(min(L.mn[0][p], L.mn[1][p]), min(L.mn[2][p], L.mn[3][p]));
+        const int a1 = max(max(L.mx[0][p], L.mx[1][p]), max(L.mx[2][p], L.mx[3][p]));
+        L.rng[p] = make_float2(__int_as_float(a0), __int_as_float(a1));
+    }
+    __syncthreads();
+}
+
+// every branch's LDS overlaid: the kernel keeps the raycast's occupancy (8 workgroups per CU)
+union PairLds {
+    int vtab[256 * VTAB_STRIDE];
+    IrLds ir;
+    EdLds<ED_PAIR_W> ed;
+    PnLds pn;
+    BilLds bil;
+};
+
+// The frame's two raycasts in one launch: one part of the grid casts CreateICPMaps' rays
+// (castRay<true>, new range image), another renderImage's (castRay<false> + grey, range
+// snapshot).  Neither writes what the other reads, and a launch's run time is its slowest waves'
+// ray length: the halves fill each other's tails instead of each kernel draining alone.
+// (Measured: marching both rays of a pixel interleaved in one thread, sharing each step's round
+// trips, is slower -- 142 VGPRs halve the resident waves.)
+// nfill > 0 (frame path, W <= ED_PAIR_W): the grid starts with CreateExpectedDepths' fill
+// (ed_fill_block, one workgroup per LDS row; it writes the range image for the frames after this
+// one) and the CreateICPMaps tiles take their four range pixels from the projection's bins
+// (ed_tile_range) instead of waiting for it -- one launch and its dependent round trips fewer per
+// frame.  Past lds_max_n visible entries the fill takes its atomic path and the tiles wait for
+// its rows to count done (the fill workgroups come first in dispatch order, and wait on nothing).
+// (8 waves per SIMD: the allocator left alone takes 70 VGPRs over the kernel's branches, each of
+// which fits 64 on its own; held to 64 it spills one 8-byte value once per thread)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
+k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x, int n_tiles, int nb,
+               PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx, EdArgs ed, int nfill, int nfill_pad)
+{
+    __shared__ PairLds L;
+    int b = (int)blockIdx.x;
+    if (b < nfill_pad) {
+        if (b < nfill) ed_fill_block<ED_PAIR_W>(ed, st, b, nfill, L.ed, false);
+        return;
+    }
+    b -= nfill_pad;
+    if (b < nb) {
+        if (!raycast_go<1>(st)) return;
+        const int tile = xcd_tile(b, n_tiles);
+        if (tile < 0) return;
+        const int tx = tile % tiles_x, ty = tile / tiles_x;
+        const int n = st->noVisibleEntries;
+        if (nfill > 0 && n <= ed.lds_max_n) {
+            ed_tile_range(ed, 2 * tx, 2 * ty, n, L.ir);
+        } else {
+            if (nfill > 0 && threadIdx.x == 0) {
+                // the fill's atomic path writes the range image: wait until every row is done
+                unsigned spins = 0;
+                while (__hip_atomic_load(ed.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nfill) {
+                    if (++spins > (1u << 24)) { st->icp_ok = -1; break; }   // the frame end reports a HIP error
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            __syncthreads();
+            if (threadIdx.x < 4) {               // the tile's four /8 pixels of the range image
+                const int X = 2 * tx + (threadIdx.x & 1), Y = 2 * ty + (threadIdx.x >> 1);
+                L.ir.rng[threadIdx.x] = X < ai.W && Y < ai.H ? ai.range[X + Y * ai.W] : make_float2(0.f, 0.f);
+            }
+            __syncthreads();
+        }
+        // (one instance of the march for both sources of the range: a second costs registers)
+        raycast_tile<1, true>(ai, st, tile, tiles_x, nullptr, L.ir.rng);
+        return;
+    }
+    b -= nb;
+    if (b < nb) {
+        if (!raycast_go<2>(st)) return;
+        const int tile = xcd_tile(b, n_tiles);
+        if (tile < 0) return;
+        raycast_tile<2>(ar, st, tile, tiles_x, L.vtab);
+        return;
+    }
+    b -= nb;
+    // Later frames of the batch in this grid's tail, not gated by this frame's abort: the next
+    // frame's computeDists + pyramids + normals (this frame's allocation and integration, the
+    // last readers of dists and of the current maps, are done; its level-0 depth was filtered
+    // a launch or more ago), then the bilateral pass of the frame after it (into the other
+    // level-0 buffer: this frame's, whose last reader was its own pyramid pass)
+    if (b < n_pyr) pyr_normals_block(pyr, b % pyr_gx, b / pyr_gx, L.pn);
+    else bilateral_block(bil, (b - n_pyr) % bil_gx, (b - n_pyr) / bil_gx, L.bil);
+}
+
+// CreateICPMaps' raycast + the frame's renderImage in one launch (after CreateExpectedDepths'
+// projection): the renderImage half reads the range-image snapshot (render_snapshot).
+// fuse_ed: CreateExpectedDepths' fill runs in this grid (frame path; W <= ED_PAIR_W)
+int tfk_ed_fused(const tf_ctx* c) { return c->W <= ED_PAIR_W; }
+
+hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch, int fuse_ed)
+{
+    RayArgs ai, ar;
+    ray_args(c, ai);
+    ai.visType = c->visType;
+    ray_args(c, ar);
+    ar.range = (const float2*)c->range_render;
+    ar.grey = c->grey;
+    const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty;
+    const int nb = (n + 7) / 8 * 8;
+    BilArgs bb = BilArgs{}, bx; PyrArgs pp = PyrArgs{}, px;
+    int n_pyr = 0, pyr_gx = 1, n_bil = 0, bil_gx = 1;
+    if (pyr.src) {
+        const hipError_t e = tf_pre_args(c, pyr.src, pitch, 1, pyr.d0, &bx, &pp);
+        if (e != hipSuccess) return e;
+        pyr_gx = tf_div_up(c->W, PN_T0);
+        n_pyr = pyr_gx * tf_div_up(c->H, PN_T0);
+    }
+    if (bil.src) {
+        const hipError_t e = tf_pre_args(c, bil.src, pitch, 1, bil.d0, &bb, &px);
+        if (e != hipSuccess) return e;
+        bil_gx = tf_div_up(c->W, PRE_TX);
+        n_bil = bil_gx * tf_div_up(c->H, PRE_TY);
+    }
+    EdArgs ed;
+    tf_ed_args(c, &ed);
+    int nfill = 0, nfill_pad = 0;
+    if (fuse_ed && tfk_ed_fused(c)) {
+        nfill = ed.nrows;
+        nfill_pad = (nfill + 7) / 8 * 8;        // keeps the tiles' XCD swizzle aligned
+        ed.done = c->edDone;
+    }
+    tf_launch(c, k_raycast_pair, dim3(nfill_pad + 2 * nb + n_pyr + n_bil), dim3(256), 0, ai, ar, c->st, tx, n, nb,
+              pp, n_pyr, pyr_gx, bb, bil_gx, ed, nfill, nfill_pad);
     return hipGetLastError();
 }

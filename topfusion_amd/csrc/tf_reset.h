@@ -16,6 +16,8 @@ struct ResetArgs {
     unsigned char* swapState;        // swapping: GlobalCache states / stored flags, cleared with a reset
     unsigned char* swapFlags;
     unsigned* vba_rgb;               // voxel_rgb: the colour plane, cleared with its blocks (Voxel_s_rgb(): 0)
+    int* ed_bin_cnt; int ed_nbins;   // frame end: CreateExpectedDepths' bins emptied (the fused fill and the
+    unsigned* ed_done;               // ICP tiles that read them are done), its done counter cleared
 };
 
 // Runs as workgroup `bid` of `nblk` (256 threads): its own launch (k_reset_scene) or the
@@ -47,6 +49,10 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
         if (ok == 1 && mode == 1) { st->tot_tracked++; st->tot_tiles += st->noTotalBlocks; }
         r.frame_ok[r.slot] = ok;
         r.frame_mode[r.slot] = mode;
+    }
+    if (on_failure && bid == 0 && r.ed_bin_cnt) {
+        for (int k = threadIdx.x; k < r.ed_nbins; k += 256) r.ed_bin_cnt[k] = 0;
+        if (threadIdx.x == 0) *r.ed_done = 0u;
     }
     if (on_failure && !(st->mode == 1 && st->icp_ok == 0)) return;   // topfu.cpp:263-264 only
     const size_t tid = (size_t)bid * 256 + threadIdx.x;

@@ -58,6 +58,9 @@ void tf_reset_args(tf_ctx* c, ResetArgs* r, int on_failure, int slot, int clear_
     r->swapState = c->p.use_swapping && clear_cache ? c->swapState : nullptr;
     r->swapFlags = c->p.use_swapping && clear_cache ? c->swapFlags : nullptr;
     r->vba_rgb = c->p.voxel_rgb ? c->vba_rgb : nullptr;
+    r->ed_bin_cnt = on_failure ? c->edBinCnt : nullptr;
+    r->ed_nbins = 2 * ed_nrows(c->H);
+    r->ed_done = c->edDone;
     if (c->p.use_swapping) r->full = 1;
 }
 
@@ -286,7 +289,8 @@ k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEnt
         // frame's raw depth and writes only its level-0 depth buffer; not gated by this
         // frame's abort)
         const int b = (int)blockIdx.x - n_alloc;
-        bilateral_block(next, b % next_gx, b / next_gx);
+        __shared__ BilLds L;
+        bilateral_block(next, b % next_gx, b / next_gx, L);
         return;
     }
     if (st->abort) return;
