@@ -101,9 +101,19 @@ __device__ __forceinline__ void tstep(float* v, int lane)
 
 // rows of 4 pixels per lane with the current-frame point/normal already in registers and both
 // previous-map gathers issued before the dependent tests (defined with the persistent kernel)
-struct IpPix { float vx, vy, vz, nx, ny, nz; };
-__device__ __forceinline__ void ip_rows4(const IcpLevel& L, const float* aff, const IpPix (&px)[4],
-                                         const int (&xy)[4], float (&r)[4][7]);
+typedef float ip_f2 __attribute__((ext_vector_type(2)));   // two pixels' values: v_pk_* arithmetic
+// the current-frame point / normal of a lane's pixel pair (2h, 2h + 1), one packed pair per component
+struct IpPix { ip_f2 vx, vy, vz, nx, ny, nz; };
+// pixel j of the lane: (map index valid, point, normal) -> pair j / 2, element j % 2
+__device__ __forceinline__ void ip_set(IpPix (&px)[2], int j, float4 v, float4 n)
+{
+    IpPix& p = px[j >> 1];
+    if (j & 1) { p.vx.y = v.x; p.vy.y = v.y; p.vz.y = v.z; p.nx.y = n.x; p.ny.y = n.y; p.nz.y = n.z; }
+    else { p.vx.x = v.x; p.vy.x = v.y; p.vz.x = v.z; p.nx.x = n.x; p.ny.x = n.y; p.nz.x = n.z; }
+}
+__device__ __forceinline__ void ip_rows4(const IcpLevel& L, const float* aff, const IpPix (&px)[2],
+                                         const int (&xy)[4], ip_f2 (&r01)[7], ip_f2 (&r23)[7]);
+__device__ __forceinline__ float ip_cta_reduce(const ip_f2 (&r01)[7], const ip_f2 (&r23)[7], int lane);
 
 __global__ void __launch_bounds__(64 * ICP_WAVES)
 k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsigned* __restrict__ ticket,
@@ -124,7 +134,7 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
         const int bx = cta % L.gx, by = cta / L.gx;
         // the CTA's current maps with unconditional loads, then ip_rows4 (the per-pixel
         // per-pixel early returns make every load a branch: ~10 round trips per CTA)
-        IpPix q[4];
+        IpPix q[2];
         int qxy[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -135,30 +145,11 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
             const int pi = in ? y * L.W + x : 0;
             float4 v = L.vcurr[pi], n = L.ncurr[pi];
             if (!in) { v = make_float4(0.f, 0.f, 0.f, 0.f); n = v; }
-            q[j].vx = v.x; q[j].vy = v.y; q[j].vz = v.z; q[j].nx = n.x; q[j].ny = n.y; q[j].nz = n.z;
+            ip_set(q, j, v, n);
         }
-        float r[4][7];
-        ip_rows4(L, aff, q, qxy, r);
-        // steps 128 and 64 of the halving tree in registers (partial_reduce order, proj_icp.cu:137-356)
-        float v[32];
-        int k = 0;
-#pragma unroll
-        for (int a = 0; a < 6; ++a)
-#pragma unroll
-            for (int b = a; b < 7; ++b, ++k) {
-                float a0 = r[0][a] * r[0][b] + r[2][a] * r[2][b];
-                float a1 = r[1][a] * r[1][b] + r[3][a] * r[3][b];
-                v[k] = a0 + a1;
-            }
-#pragma unroll
-        for (int j = 27; j < 32; ++j) v[j] = 0.f;
-        // steps 32..2 transposed, step 1 plain: lane l ends with sum (l >> 1)
-        tstep<32, 32>(v, lane);
-        tstep<16, 16>(v, lane);
-        tstep<8, 8>(v, lane);
-        tstep<4, 4>(v, lane);
-        tstep<2, 2>(v, lane);
-        float tot = v[0] + xor1(v[0]);
+        ip_f2 r01[7], r23[7];
+        ip_rows4(L, aff, q, qxy, r01, r23);
+        const float tot = ip_cta_reduce(r01, r23, lane);    // lane l ends with sum (l >> 1)
         const int sidx = lane >> 1;
         if (!(lane & 1) && sidx < 27) red[s][sidx] = tot;
     }
@@ -402,46 +393,77 @@ __device__ __forceinline__ unsigned ip_xcc_id()
 // the current-frame point/normal in registers and both previous-map loads issued before any of
 // the dependent tests (IpPix is declared above k_icp_iter)
 
-__device__ __forceinline__ void ip_rows4(const IcpLevel& L, const float* aff, const IpPix (&px)[4],
-                                         const int (&xy)[4], float (&r)[4][7])
+// kdot / kcross (tf_internal.h) on two pixels at once: the same operations per element, as
+// v_pk_mul / v_pk_fma / v_pk_add (the rows are VALU-bound: two reference CTAs share a SIMD at
+// level 0, one CTA's rows are ~700 instructions)
+__device__ __forceinline__ ip_f2 ip_bc(float v) { return ip_f2{ v, v }; }
+__device__ __forceinline__ ip_f2 kdot2(ip_f2 ax, ip_f2 ay, ip_f2 az, ip_f2 bx, ip_f2 by, ip_f2 bz)
 {
-    tf3 R0 = mk3(aff[0], aff[1], aff[2]), R1 = mk3(aff[4], aff[5], aff[6]), R2 = mk3(aff[8], aff[9], aff[10]);
-    tf3 s[4];
-    bool ok[4];
-    int idx[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        tf3 v = mk3(px[j].vx, px[j].vy, px[j].vz);
-        ok[j] = xy[j] >= 0 && !isnan(v.x);
-        s[j] = mk3(kdot(R0, v) + aff[3], kdot(R1, v) + aff[7], kdot(R2, v) + aff[11]);
-        float coox = fmaf(L.fx, s[j].x / s[j].z, L.cx);
-        float cooy = fmaf(L.fy, s[j].y / s[j].z, L.cy);
-        ok[j] = ok[j] && !(s[j].z <= 0 || coox < 0 || cooy < 0 || coox >= (float)L.W || cooy >= (float)L.H);
-        idx[j] = ok[j] ? (int)floorf(cooy) * L.W + (int)floorf(coox) : 0;
-    }
-    float4 dp[4], ndp[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { dp[j] = L.vprev[idx[j]]; ndp[j] = L.nprev[idx[j]]; }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        tf3 d = mk3(dp[j].x, dp[j].y, dp[j].z);
-        bool good = ok[j] && !isnan(d.x);
-        tf3 sd = sub3(s[j], d);
-        good = good && !(kdot(sd, sd) > L.dist2);
-        tf3 nc = mk3(px[j].nx, px[j].ny, px[j].nz);
-        tf3 ns = mk3(kdot(R0, nc), kdot(R1, nc), kdot(R2, nc));
-        tf3 nd = mk3(ndp[j].x, ndp[j].y, ndp[j].z);
-        good = good && !(fabsf(kdot(ns, nd)) < L.min_cosine);
-        tf3 cr = kcross(s[j], nd);
-        float b = kdot(nd, sub3(d, s[j]));
-        r[j][0] = good ? cr.x : 0.f; r[j][1] = good ? cr.y : 0.f; r[j][2] = good ? cr.z : 0.f;
-        r[j][3] = good ? nd.x : 0.f; r[j][4] = good ? nd.y : 0.f; r[j][5] = good ? nd.z : 0.f;
-        r[j][6] = good ? b : 0.f;
-    }
+    return __builtin_elementwise_fma(ax, bx, __builtin_elementwise_fma(ay, by, az * bz));
 }
 
-// 256-pixel CTA reduction (partial_reduce order): lane l ends holding sum (l >> 1)
-__device__ __forceinline__ float ip_cta_reduce(const float (&r)[4][7], int lane)
+// a pixel pair: projection into the previous frame (find_coresp's first half)
+__device__ __forceinline__ void ip_project2(const IcpLevel& L, const float* aff, ip_f2 vx, ip_f2 vy, ip_f2 vz,
+                                           int xy0, int xy1, ip_f2& sx, ip_f2& sy, ip_f2& sz, bool& ok0, bool& ok1,
+                                           int& idx0, int& idx1)
+{
+    sx = kdot2(ip_bc(aff[0]), ip_bc(aff[1]), ip_bc(aff[2]), vx, vy, vz) + ip_bc(aff[3]);
+    sy = kdot2(ip_bc(aff[4]), ip_bc(aff[5]), ip_bc(aff[6]), vx, vy, vz) + ip_bc(aff[7]);
+    sz = kdot2(ip_bc(aff[8]), ip_bc(aff[9]), ip_bc(aff[10]), vx, vy, vz) + ip_bc(aff[11]);
+    const ip_f2 qx = { sx.x / sz.x, sx.y / sz.y }, qy = { sy.x / sz.x, sy.y / sz.y };
+    const ip_f2 coox = __builtin_elementwise_fma(ip_bc(L.fx), qx, ip_bc(L.cx));
+    const ip_f2 cooy = __builtin_elementwise_fma(ip_bc(L.fy), qy, ip_bc(L.cy));
+    ok0 = xy0 >= 0 && !isnan(vx.x) &&
+          !(sz.x <= 0 || coox.x < 0 || cooy.x < 0 || coox.x >= (float)L.W || cooy.x >= (float)L.H);
+    ok1 = xy1 >= 0 && !isnan(vx.y) &&
+          !(sz.y <= 0 || coox.y < 0 || cooy.y < 0 || coox.y >= (float)L.W || cooy.y >= (float)L.H);
+    idx0 = ok0 ? (int)floorf(cooy.x) * L.W + (int)floorf(coox.x) : 0;
+    idx1 = ok1 ? (int)floorf(cooy.y) * L.W + (int)floorf(coox.y) : 0;
+}
+
+// a pixel pair: the correspondence tests and the row (find_coresp's second half, the
+// row of proj_icp.cu:365-377), zero where a test fails
+__device__ __forceinline__ void ip_row2(const IcpLevel& L, const float* aff, ip_f2 ncx, ip_f2 ncy, ip_f2 ncz,
+                                       ip_f2 sx, ip_f2 sy, ip_f2 sz, bool ok0, bool ok1, float4 dp0, float4 dp1,
+                                       float4 ndp0, float4 ndp1, ip_f2 (&r)[7])
+{
+    const ip_f2 dx = { dp0.x, dp1.x }, dy = { dp0.y, dp1.y }, dz = { dp0.z, dp1.z };
+    const ip_f2 ex = sx - dx, ey = sy - dy, ez = sz - dz;              // sd = s - d
+    const ip_f2 dd = kdot2(ex, ey, ez, ex, ey, ez);
+    const ip_f2 nsx = kdot2(ip_bc(aff[0]), ip_bc(aff[1]), ip_bc(aff[2]), ncx, ncy, ncz);
+    const ip_f2 nsy = kdot2(ip_bc(aff[4]), ip_bc(aff[5]), ip_bc(aff[6]), ncx, ncy, ncz);
+    const ip_f2 nsz = kdot2(ip_bc(aff[8]), ip_bc(aff[9]), ip_bc(aff[10]), ncx, ncy, ncz);
+    const ip_f2 ndx = { ndp0.x, ndp1.x }, ndy = { ndp0.y, ndp1.y }, ndz = { ndp0.z, ndp1.z };
+    const ip_f2 cs = kdot2(nsx, nsy, nsz, ndx, ndy, ndz);
+    // kcross(s, nd), kdot(nd, d - s)
+    const ip_f2 crx = sy * ndz - sz * ndy, cry = sz * ndx - sx * ndz, crz = sx * ndy - sy * ndx;
+    const ip_f2 b = kdot2(ndx, ndy, ndz, dx - sx, dy - sy, dz - sz);
+    const bool g0 = ok0 && !isnan(dx.x) && !(dd.x > L.dist2) && !(fabsf(cs.x) < L.min_cosine);
+    const bool g1 = ok1 && !isnan(dx.y) && !(dd.y > L.dist2) && !(fabsf(cs.y) < L.min_cosine);
+    auto sel = [g0, g1](ip_f2 v) { return ip_f2{ g0 ? v.x : 0.f, g1 ? v.y : 0.f }; };
+    r[0] = sel(crx); r[1] = sel(cry); r[2] = sel(crz);
+    r[3] = sel(ndx); r[4] = sel(ndy); r[5] = sel(ndz); r[6] = sel(b);
+}
+
+__device__ __forceinline__ void ip_rows4(const IcpLevel& L, const float* aff, const IpPix (&px)[2],
+                                         const int (&xy)[4], ip_f2 (&r01)[7], ip_f2 (&r23)[7])
+{
+    ip_f2 sx0, sy0, sz0, sx1, sy1, sz1;
+    bool ok0, ok1, ok2, ok3;
+    int i0, i1, i2, i3;
+    ip_project2(L, aff, px[0].vx, px[0].vy, px[0].vz, xy[0], xy[1], sx0, sy0, sz0, ok0, ok1, i0, i1);
+    ip_project2(L, aff, px[1].vx, px[1].vy, px[1].vz, xy[2], xy[3], sx1, sy1, sz1, ok2, ok3, i2, i3);
+    // both previous-map gathers of all four pixels issued before any dependent test
+    const float4 d0 = L.vprev[i0], d1 = L.vprev[i1], d2 = L.vprev[i2], d3 = L.vprev[i3];
+    const float4 n0 = L.nprev[i0], n1 = L.nprev[i1], n2 = L.nprev[i2], n3 = L.nprev[i3];
+    ip_row2(L, aff, px[0].nx, px[0].ny, px[0].nz, sx0, sy0, sz0, ok0, ok1, d0, d1, n0, n1, r01);
+    ip_row2(L, aff, px[1].nx, px[1].ny, px[1].nz, sx1, sy1, sz1, ok2, ok3, d2, d3, n2, n3, r23);
+}
+
+// 256-pixel CTA reduction (partial_reduce order): lane l ends holding sum (l >> 1).  Steps 128
+// and 64 in registers: (r0a r0b + r2a r2b) + (r1a r1b + r3a r3b), the first two pairs as one
+// v_pk_mul each over the pixel pairs and one v_pk_add.
+__device__ __forceinline__ float ip_cta_reduce(const ip_f2 (&r01)[7], const ip_f2 (&r23)[7], int lane)
 {
     float v[32];
     int k = 0;
@@ -449,9 +471,8 @@ __device__ __forceinline__ float ip_cta_reduce(const float (&r)[4][7], int lane)
     for (int a = 0; a < 6; ++a)
 #pragma unroll
         for (int b = a; b < 7; ++b, ++k) {
-            float a0 = r[0][a] * r[0][b] + r[2][a] * r[2][b];
-            float a1 = r[1][a] * r[1][b] + r[3][a] * r[3][b];
-            v[k] = a0 + a1;
+            const ip_f2 s = r01[a] * r01[b] + r23[a] * r23[b];      // (a0, a1)
+            v[k] = s.x + s.y;
         }
 #pragma unroll
     for (int j = 27; j < 32; ++j) v[j] = 0.f;
@@ -555,7 +576,7 @@ k_icp_frame(IcpFrameArgs a)
         const IcpLevel L = li == 0 ? a.lv[0] : (li == 1 ? a.lv[1] : a.lv[2]);
         const int slots = li == 0 ? a.slots[0] : (li == 1 ? a.slots[1] : a.slots[2]);
         // current-frame maps of my CTA slots -> registers (constant over the level)
-        IpPix px[IP_SREG][4];
+        IpPix px[IP_SREG][2];
         int xy[IP_SREG][4];
 #pragma unroll
         for (int rr = 0; rr < IP_SREG; ++rr) {
@@ -574,8 +595,7 @@ k_icp_frame(IcpFrameArgs a)
                 const int pi = in ? y * L.W + x : 0;
                 float4 v = L.vcurr[pi], n = L.ncurr[pi];
                 if (!in) { v = make_float4(0.f, 0.f, 0.f, 0.f); n = v; }
-                px[rr][j].vx = v.x; px[rr][j].vy = v.y; px[rr][j].vz = v.z;
-                px[rr][j].nx = n.x; px[rr][j].ny = n.y; px[rr][j].nz = n.z;
+                ip_set(px[rr], j, v, n);
             }
         }
         const int iters = li == 0 ? a.iters[0] : (li == 1 ? a.iters[1] : a.iters[2]);
@@ -595,9 +615,9 @@ k_icp_frame(IcpFrameArgs a)
             for (int rr = 0; rr < IP_SREG; ++rr) {
                 const int sl = wave + IP_WAVES * rr;
                 if (sl < slots && wg + ICP_NWG * sl < L.nct) {
-                    float r[4][7];
-                    ip_rows4(L, aff, px[rr], xy[rr], r);
-                    const float tot = ip_cta_reduce(r, lane);
+                    ip_f2 r01[7], r23[7];
+                    ip_rows4(L, aff, px[rr], xy[rr], r01, r23);
+                    const float tot = ip_cta_reduce(r01, r23, lane);
                     if (!(lane & 1) && (lane >> 1) < 27) red[sl][lane >> 1] = tot;
                 }
             }
@@ -606,7 +626,7 @@ k_icp_frame(IcpFrameArgs a)
             for (int sl = wave + IP_WAVES * IP_SREG; sl < slots; sl += IP_WAVES) {
                 const int cta = wg + ICP_NWG * sl;
                 if (cta >= L.nct) break;
-                IpPix q[4];
+                IpPix q[2];
                 int qxy[4];
                 const int bx = cta % L.gx, by = cta / L.gx;
 #pragma unroll
@@ -618,11 +638,11 @@ k_icp_frame(IcpFrameArgs a)
                     const int pi = in ? y * L.W + x : 0;                 // unconditional loads
                     float4 v = L.vcurr[pi], n = L.ncurr[pi];
                     if (!in) { v = make_float4(0.f, 0.f, 0.f, 0.f); n = v; }
-                    q[j].vx = v.x; q[j].vy = v.y; q[j].vz = v.z; q[j].nx = n.x; q[j].ny = n.y; q[j].nz = n.z;
+                    ip_set(q, j, v, n);
                 }
-                float r[4][7];
-                ip_rows4(L, aff, q, qxy, r);
-                const float tot = ip_cta_reduce(r, lane);
+                ip_f2 r01[7], r23[7];
+                ip_rows4(L, aff, q, qxy, r01, r23);
+                const float tot = ip_cta_reduce(r01, r23, lane);
                 if (!(lane & 1) && (lane >> 1) < 27) red[sl][lane >> 1] = tot;
             }
             __syncthreads();
