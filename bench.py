@@ -84,26 +84,46 @@ def parse():
 
 
 def stage_bytes(stage, p, nvis, W, H, lanes=None):
-    """Algorithmic HBM bytes of ONE launch of a stage.  integrate: the visible
-    entries, the depth image and the voxel bytes the update needs -- the 16-B lanes (4 voxels)
-    with an update read, those whose value changed written (`lanes` = (read, written) per
-    launch, counted on the device); without counts every voxel read and written."""
+    """Algorithmic HBM bytes of ONE launch of a stage's frame-path kernel (plus the
+    work the frame path fuses into that kernel's grid), batched path (two-frame lookahead).
+      icp:         sum over levels of iters x W_l x H_l x 64 B.
+      raycast_icp: k_raycast_pair -- both raycasts (float4 point image + uchar4 grey image out,
+                   every visible block read once per raycast, 2064 B each), the fused
+                   CreateExpectedDepths fill (the /8 range region written, the binned boxes read
+                   once: 2 x 16 B per box), and the lookahead it carries: frame j+1's computeDists
+                   (raw 2 B in, 4 B out), pyramid (level 0 in, levels 1-2 out) and points + normals
+                   of three levels (32 B per level pixel), frame j+2's bilateral pass (2 B in, 2 B out).
+      integrate:   k_integrate<true> -- the visible entries (id + hash entry, 20 B), the depth image,
+                   16 B per voxel lane read (those with an update) and per lane written (those that
+                   changed), counted on the device (`lanes` = (read, written) per launch; without
+                   counts every voxel read and written), plus CreateExpectedDepths' projection in
+                   its leading workgroups (entries read again, 24 B record + tiles + offset out,
+                   2 x 16 B binned per box)."""
+    npx = W * H
     if stage == "raycast_icp":
-        # both raycasts in one launch: float4 ray image + uchar4 grey image out, every visible
-        # block read once per raycast
-        return W * H * (16 + 4) + 2 * nvis * (2048 + 16)
+        rc, rr = (W - 1) // 8 + 1, (H - 1) // 8 + 1
+        pre = npx * (2 + 4) + npx * 2 + (npx // 4 + npx // 16) * 2 + (npx + npx // 4 + npx // 16) * 32 + npx * (2 + 2)
+        return npx * (16 + 4) + 2 * nvis * (2048 + 16) + rc * rr * 8 + nvis * 32 + pre
     if stage == "integrate":
+        ed = nvis * (20 + 24 + 32)
         if lanes is not None:
-            return nvis * 20 + W * H * 4 + 16 * (lanes[0] + lanes[1])
-        return nvis * (4096 + 20) + W * H * 4           # voxel R+W + entry/id + depth image
+            return nvis * 20 + npx * 4 + 16 * (lanes[0] + lanes[1]) + ed
+        return nvis * (4096 + 20) + npx * 4 + ed           # voxel R+W + entry/id + depth image
     if stage == "grey":
-        return W * H * (16 + 4) + nvis * (2048 + 16)
+        return npx * (16 + 4) + nvis * (2048 + 16)
     if stage == "icp":
         tot = 0
         for l in range(3):
             tot += p.icp_iter_num[l] * (W >> l) * (H >> l) * 64
         return tot
     return None
+
+
+def pmc_tracked_bytes(pmc, stage):
+    """HBM-side bytes per launch of a stage's kernel on the timed frames' tracked frames
+    (profiles/pmc_traffic.json, tools/pmc_frames_summary.py), else the older per-launch figure."""
+    e = pmc.get(stage) or {}
+    return (e.get("tracked") or {}).get("bytes", e.get("bytes_per_launch"))
 
 
 def omp_threads():
@@ -567,7 +587,7 @@ def main():
                 ach = b / (ms * 1e-3) / 1e9
                 roof_all[k] = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                "frac": round(ach / PEAK_HBM_GBS, 5),
-                               "traffic": (pmc.get(k) or {}).get("bytes_per_launch"),
+                               "traffic": pmc_tracked_bytes(pmc, k),
                                "kernel": KERNEL_OF_STAGE[k], "algorithmic_bytes_per_launch": int(b),
                                "avg_launch_ms": round(ms, 5),
                                "timing": (f"HIP events tied to the dispatch of every {args.profile_every}-th launch of the "

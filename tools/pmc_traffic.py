@@ -11,8 +11,7 @@ The output holds one entry per bench config (C2, C3); an existing file is update
 import csv, glob, json, os, sys
 from collections import defaultdict
 
-STAGE_OF = [("k_icp_frame", "icp"), ("k_raycast<2>", "raycast_render"), ("k_raycast_pair", "raycast_icp"),
-            ("k_integrate", "integrate")]
+STAGE_OF = [("k_icp_frame", "icp"), ("k_raycast_pair", "raycast_icp"), ("k_integrate", "integrate")]
 
 
 def per_kernel(root, counter):
@@ -54,8 +53,6 @@ def main():
     allcfg = {}
     if os.path.exists(out):
         allcfg = json.load(open(out))
-        if allcfg and "C2" not in allcfg and "C3" not in allcfg:     # old flat layout
-            allcfg = {}
     allcfg[config] = res
     json.dump(allcfg, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
