@@ -12,12 +12,12 @@
 __global__ void __launch_bounds__(256) k_dists_bilateral(BilArgs b)
 {
     __shared__ BilLds L;
-    bilateral_block(b, blockIdx.x, blockIdx.y, L);
+    bilateral_block<true>(b, blockIdx.x, blockIdx.y, L);
 }
-__global__ void __launch_bounds__(256) k_pyr_normals(PyrArgs a)
+__global__ void __launch_bounds__(1024) k_pyr_normals(PyrArgs a)
 {
     __shared__ PnLds L;
-    pyr_normals_block(a, blockIdx.x, blockIdx.y, L);
+    pyr_normals_block<1024>(a, blockIdx.x, blockIdx.y, L);
 }
 
 // the preprocessing arguments of raw frame `depth`; lookahead: the frame-path split in which
@@ -54,6 +54,6 @@ hipError_t tfk_preprocess(tf_ctx* c, const uint16_t* depth, size_t pitch, hipStr
     hipError_t e = tf_pre_args(c, depth, pitch, 0, d0, &b, &a);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_dists_bilateral, dim3(tf_div_up(c->W, PRE_TX), tf_div_up(c->H, PRE_TY)), dim3(256), 0, strm, b);
-    hipLaunchKernelGGL(k_pyr_normals, dim3(tf_div_up(c->W, PN_T0), tf_div_up(c->H, PN_T0)), dim3(256), 0, strm, a);
+    hipLaunchKernelGGL(k_pyr_normals, dim3(tf_div_up(c->W, PN_T0), tf_div_up(c->H, PN_T0)), dim3(1024), 0, strm, a);
     return hipGetLastError();
 }

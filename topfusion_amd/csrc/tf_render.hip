@@ -1366,8 +1366,8 @@ k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
     // last readers of dists and of the current maps, are done; its level-0 depth was filtered
     // a launch or more ago), then the bilateral pass of the frame after it (into the other
     // level-0 buffer: this frame's, whose last reader was its own pyramid pass)
-    if (b < n_pyr) pyr_normals_block(pyr, b % pyr_gx, b / pyr_gx, L.pn);
-    else bilateral_block(bil, (b - n_pyr) % bil_gx, (b - n_pyr) / bil_gx, L.bil);
+    if (b < n_pyr) pyr_normals_block<256>(pyr, b % pyr_gx, b / pyr_gx, L.pn);
+    else bilateral_block<false>(bil, (b - n_pyr) % bil_gx, (b - n_pyr) / bil_gx, L.bil);
 }
 
 // CreateICPMaps' raycast + the frame's renderImage in one launch (after CreateExpectedDepths'

@@ -290,7 +290,7 @@ k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEnt
         // frame's abort)
         const int b = (int)blockIdx.x - n_alloc;
         __shared__ BilLds L;
-        bilateral_block(next, b % next_gx, b / next_gx, L);
+        bilateral_block<false>(next, b % next_gx, b / next_gx, L);
         return;
     }
     if (st->abort) return;

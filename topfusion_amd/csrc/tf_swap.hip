@@ -23,8 +23,8 @@
 // trip and no staging buffer; hipMemcpy moves it to / from a file (tf_swap_save / _load).
 // Three launches per frame after integration, over 4096-entry chunks like the allocation scans:
 // count swap-in candidates; swap in (ordered by a chunk prefix) + count swap-out candidates;
-// swap out.  The reallocation of listed swapped-out entries is one workgroup over the visible
-// list (ascending, so its serial free-list order is a block prefix sum).
+// swap out.  The reallocation of listed swapped-out entries is the same count + prefix pattern
+// over the visible list (ascending, so its serial free-list order is a prefix sum).
 #include "tf_internal.h"
 
 #define SW_CHUNK 4096          // entries per workgroup (256 threads x 16)
@@ -64,44 +64,93 @@ __device__ __forceinline__ int sw_excl_scan(int v, int* total)
 // ---------------------------------------------------------------------------------------
 // reAllocateSwappedOutVoxelBlocks_device (SceneReconstructionEngine_host.cu:417-432): entries of
 // visible type > 0 whose block was swapped out (ptr == -1) take blocks from the free list in
-// ascending index order; once it is empty the rest keep ptr -1.  One workgroup over the visible
-// list (ascending, so its serial free-list order is a block prefix sum); when the list is full
-// (noVisibleEntries == cap: entries past the capacity may be of type > 0 without being listed,
-// and the reference's pass covers every entry) it walks visType over the whole table instead.
+// ascending index order; once it is empty the rest keep ptr -1.  The candidates are the visible
+// list's entries (ascending, so the serial free-list order is a prefix sum over the list); when
+// the list is full (noVisibleEntries == cap: entries past the capacity may be of type > 0
+// without being listed, and the reference's pass covers every entry) every hash entry with
+// visType > 0.  Two launches over 4096-candidate chunks, as the swap-in / swap-out passes:
+// count per chunk, then each chunk assigns allocList[v - prefix - rank].
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
-k_swap_realloc(TfDevState* __restrict__ st, TfHashEntry* __restrict__ hash, const int* __restrict__ visibleIds,
-               const unsigned char* __restrict__ visType, const int* __restrict__ allocList, int2* __restrict__ grid,
-               int cap, int n_total)
+__device__ __forceinline__ int sw_realloc_flags(const TfDevState* st, const TfHashEntry* __restrict__ hash,
+                                                const int* __restrict__ visibleIds, const unsigned char* __restrict__ visType,
+                                                int cap, int n_total, int* ids)
 {
-    if (st->abort) return;
     const int nv = st->noVisibleEntries;
     const bool full = nv >= cap;
     const int n = full ? n_total : nv;
-    int v = st->lastFreeBlockId;                // uniform: every thread reads it before any write
-    int done = 0;
-    for (int i0 = 0; i0 < n; i0 += 256) {
-        const int i = i0 + threadIdx.x;
-        int id = -1;
-        bool need = false;
-        if (i < n) {
-            id = full ? i : visibleIds[i];
-            need = (!full || visType[id] > 0) && hash[id].ptr == -1;
+    const int base = blockIdx.x * SW_CHUNK + threadIdx.x * 16;
+    int flags = 0;
+    if (base >= n) return 0;
+    if (full) {
+        if (base + 16 <= n_total) {
+            unsigned long long vlo, vhi;
+            sw_load16(visType + base, &vlo, &vhi);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) ids[i] = sw_byte(vlo, vhi, i) > 0 ? base + i : -1;
+        } else {
+            for (int i = 0; i < 16; ++i) ids[i] = base + i < n_total && visType[base + i] > 0 ? base + i : -1;
         }
-        int cnt;
-        const int r = sw_excl_scan(need ? 1 : 0, &cnt);
-        if (need && v - r >= 0) {
-            TfHashEntry e = hash[id];
-            e.ptr = allocList[v - r];
-            hash[id].ptr = e.ptr;
-            grid_set(grid, e, id);
-        }
-        const int got = cnt < v + 1 ? cnt : (v + 1 > 0 ? v + 1 : 0);
-        v -= got;
-        done += got;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ids[i] = base + i < n ? visibleIds[base + i] : -1;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) { st->lastFreeBlockId = v; st->swap_realloc = done; }
+    int ptr[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ptr[i] = ids[i] >= 0 ? hash[ids[i]].ptr : 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) if (ptr[i] == -1) flags |= 1 << i;
+    return flags;
+}
+
+__global__ void __launch_bounds__(256)
+k_swap_realloc_count(TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash, const int* __restrict__ visibleIds,
+                     const unsigned char* __restrict__ visType, int* __restrict__ counts, int cap, int n_total)
+{
+    if (st->abort) return;
+    int ids[16];
+    const int flags = sw_realloc_flags(st, hash, visibleIds, visType, cap, n_total, ids);
+    int tot;
+    sw_excl_scan(__popc(flags), &tot);
+    if (threadIdx.x == 0) counts[2 * blockIdx.x] = tot;
+    if (blockIdx.x == 0 && threadIdx.x == 0) counts[1] = st->lastFreeBlockId;   // the free-list top both passes use
+}
+
+__global__ void __launch_bounds__(256)
+k_swap_realloc(TfDevState* __restrict__ st, TfHashEntry* __restrict__ hash, const int* __restrict__ visibleIds,
+               const unsigned char* __restrict__ visType, const int* __restrict__ allocList, int2* __restrict__ grid,
+               const int* __restrict__ counts, int n_chunks, int cap, int n_total)
+{
+    if (st->abort) return;
+    int pre = 0, all = 0;
+    for (int h = threadIdx.x; h < n_chunks; h += 256) {
+        const int c = counts[2 * h];
+        all += c;
+        if (h < (int)blockIdx.x) pre += c;
+    }
+    sw_excl_scan(pre, &pre);
+    sw_excl_scan(all, &all);
+    const int v = counts[1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int got = all < v + 1 ? all : (v + 1 > 0 ? v + 1 : 0);
+        st->lastFreeBlockId = v - got;
+        st->swap_realloc = got;
+    }
+    int ids[16];
+    const int flags = sw_realloc_flags(st, hash, visibleIds, visType, cap, n_total, ids);
+    int nchunk;
+    int r = pre + sw_excl_scan(__popc(flags), &nchunk);
+    if (!flags) return;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (!(flags & (1 << i))) continue;
+        if (v - r >= 0) {
+            TfHashEntry e = hash[ids[i]];
+            e.ptr = allocList[v - r];
+            hash[ids[i]].ptr = e.ptr;
+            grid_set(grid, e, ids[i]);
+        }
+        ++r;
+    }
 }
 
 // swap-in candidates of a chunk: state 1 with a block
@@ -297,8 +346,12 @@ k_swap_out(TfDevState* __restrict__ st, unsigned char* __restrict__ swapState, u
 
 hipError_t tfk_swap_realloc(tf_ctx* c)
 {
-    hipLaunchKernelGGL(k_swap_realloc, dim3(1), dim3(256), 0, c->stream, c->st, c->hash, c->visibleIds, c->visType,
-                       c->allocList, c->bgrid, c->p.vis_capacity, c->n_total);
+    // chunks over the table: the visible list never holds more than n_total entries
+    const int nch = (c->n_total + SW_CHUNK - 1) / SW_CHUNK;
+    hipLaunchKernelGGL(k_swap_realloc_count, dim3(nch), dim3(256), 0, c->stream, c->st, c->hash, c->visibleIds, c->visType,
+                       c->swapCounts, c->p.vis_capacity, c->n_total);
+    hipLaunchKernelGGL(k_swap_realloc, dim3(nch), dim3(256), 0, c->stream, c->st, c->hash, c->visibleIds, c->visType,
+                       c->allocList, c->bgrid, c->swapCounts, nch, c->p.vis_capacity, c->n_total);
     return hipGetLastError();
 }
 
