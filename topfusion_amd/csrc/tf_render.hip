@@ -536,7 +536,12 @@ __device__ __forceinline__ void raycast_tile(const RayArgs& a, const TfDevState*
                                              int tiles_x, int* vtab, const float2* rng = nullptr)
 {
     const int tx = tile % tiles_x, ty = tile / tiles_x;
-    const int x = tx * 16 + (threadIdx.x & 15), y = ty * 16 + (threadIdx.x >> 4);
+    // wave w casts the tile's 8x8 quadrant (w & 1, w >> 1): exactly one /8 pixel of the range
+    // image, so the wave's rays start and end on the same range (similar lengths, the wave waits
+    // on fewer stragglers), and a load of the wave touches a more compact footprint of voxels
+    // (C2: raycast pair 80 -> 73 us against 4x16-pixel waves)
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int x = tx * 16 + (wv & 1) * 8 + (ln & 7), y = ty * 16 + (wv >> 1) * 8 + (ln >> 3);
     if (x >= a.W || y >= a.H) return;
     const float2 vf = RNG_LDS ? rng[((y >> 3) - 2 * ty) * 2 + ((x >> 3) - 2 * tx)]
                               : a.range[(int)floorf((float)x / TF_SUBSAMPLE) + (int)floorf((float)y / TF_SUBSAMPLE) * a.W];
