@@ -197,11 +197,11 @@ namespace tfusion
         bool frame(const cuda::Depth& depth, const cuda::image4u* rgba)
         {
             float rt[12];
-            tf_stats st;
+            // no tf_stats: the call returns once the frame's result is known (stats() waits for the rest)
             const tf_status s = rgba && !rgba->empty()
                 ? tf_process_frame_rgb(ctx_, depth.ptr(), depth.step(), reinterpret_cast<const uint8_t*>(rgba->ptr()),
-                                       rgba->step(), rt, &st)
-                : tf_process_frame(ctx_, depth.ptr(), depth.step(), rt, &st);
+                                       rgba->step(), rt, nullptr)
+                : tf_process_frame(ctx_, depth.ptr(), depth.step(), rt, nullptr);
             if (s == TF_ICP_FAIL) {                   // reset(), return false (topfu.cpp:263-264)
                 frame_counter_ = 0;
                 poses_.clear();

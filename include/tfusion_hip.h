@@ -119,9 +119,13 @@ void      tf_destroy(tf_ctx* ctx);
 /* TopFu::reset (tfusion/src/topfu.cpp:141-152) */
 tf_status tf_reset(tf_ctx* ctx);
 /* TopFu::operator()(const cuda::Depth&) (tfusion/src/topfu.cpp:161-330).
- * dev_depth: uint16 millimetres, rows x cols, row pitch in bytes.  Synchronous.
+ * dev_depth: uint16 millimetres, rows x cols, row pitch in bytes.
  * Returns TF_OK (true) or TF_ICP_FAIL (false, scene reset).  pose_out (optional):
- * getCameraPose() as a row-major 3x4 [R|t]. */
+ * getCameraPose() as a row-major 3x4 [R|t].  Returns as soon as the frame's result is known
+ * (after its ICP), with its allocation, integration and raycasts still running on the context
+ * stream -- the reference likewise returns with its last kernels in flight (topfu.cpp:307-329);
+ * every later call that reads the state is ordered after them.  dev_depth has been consumed by
+ * then.  stats (optional) waits for the whole frame; so do RGB frames and profiled contexts. */
 tf_status tf_process_frame(tf_ctx* ctx, const uint16_t* dev_depth, size_t pitch_bytes,
                            float pose_out[12], tf_stats* stats);
 /* same, host depth (cuda::Depth::upload, device_array.hpp; demo.cpp:100) */

@@ -162,6 +162,7 @@ static void ctx_free(tf_ctx* c)
     for (int l = 1; l < TF_LEVELS; ++l) if (c->depth_pyr[l]) (void)hipFree(c->depth_pyr[l]);
     for (int k = 0; k < 2; ++k) if (c->d0_buf[k]) (void)hipFree(c->d0_buf[k]);
     if (c->st_host) (void)hipHostFree(c->st_host);
+    if (c->verdict_host) (void)hipHostFree(c->verdict_host);
     for (int i = 0; i < 2 * TF_NUM_STAGES * TF_PROF_RING; ++i) if (c->prof_ev[i]) (void)hipEventDestroy(c->prof_ev[i]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -300,7 +301,17 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     }
 #undef ALLOC
     e = hipHostMalloc((void**)&c->st_host, TF_ST_BYTES, hipHostMallocDefault);
+    // per-call frames: the verdict record in fine-grained host memory (written by the ICP launch
+    // with system-scope stores)
+    if (e == hipSuccess)
+        e = hipHostMalloc((void**)&c->verdict_host, sizeof(unsigned long long) * TF_VERDICT_WORDS, hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->verdict_dev, c->verdict_host, 0);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    memset(c->verdict_host, 0, sizeof(unsigned long long) * TF_VERDICT_WORDS);
+    {   // TFUSION_PERCALL_EARLY=0: per-call frames wait for the whole frame (A/B)
+        const char* env = getenv("TFUSION_PERCALL_EARLY");
+        c->percall_early = !(env && env[0] == '0');
+    }
     // initial device state
     TfDevState s0;
     memset(&s0, 0, sizeof(s0));
@@ -616,11 +627,80 @@ static void fill_stats(tf_ctx* c, tf_stats* st)
     st->n_resets = c->n_resets;
 }
 
+// A per-call frame returns on its verdict (early) when nothing the caller asked for needs the
+// whole frame: no stats, no stage timing, no RGB image (k_integrate reads the caller's image
+// directly, so the call must not return before the integration has run), and the persistent
+// ICP (the per-iteration fallback writes no verdict).
+static bool percall_early(const tf_ctx* c, const tf_stats* stats)
+{
+    return c->percall_early && c->icp_persistent && !c->prof_enabled && !stats && !c->rgb_cur;
+}
+
+// TopFu::operator() returning on its verdict.  Enqueues the whole frame, then waits only until
+// the persistent ICP launch has written the frame's verdict (topfu.cpp:209 / 263-264 / 329:
+// frame-0 path, reset + false, true; and poses_.back()) into host memory.  The allocation,
+// integration, raycasts and frame end are still running on the context stream when it returns;
+// everything that reads their results later (tf_download, tf_render_image, tf_get_*) is ordered
+// after them on that stream, and the next frame's launches queue behind them, so the device does
+// not wait for the host between frames.  The frame's preprocessing has read the depth by then.
+// host_depth: the tf_process_frame_host form.
+static tf_status process_frame_early(tf_ctx* c, const uint16_t* depth, size_t pitch, const uint16_t* host_depth,
+                                     float pose_out[12])
+{
+    if (host_depth) {
+        TF_CHECK(hipMemcpy2DAsync(c->depth_in, (size_t)c->W * 2, host_depth, pitch, (size_t)c->W * 2, c->H,
+                                  hipMemcpyHostToDevice, c->stream));
+        depth = c->depth_in;
+        pitch = (size_t)c->W * 2;
+    }
+    if (++c->verdict_gen == 0) c->verdict_gen = 1;
+    const unsigned gen = c->verdict_gen;
+    c->verdict_arm = 1;
+    tf_status s = enqueue_frame(c, depth, pitch, 0);
+    c->verdict_arm = 0;
+    if (s != TF_OK) return s;
+    // wait for the verdict: every word tagged with this generation
+    volatile unsigned long long* v = c->verdict_host;
+    unsigned long long w[13];
+    bool drained = false;
+    for (unsigned spins = 0;; ++spins) {
+        int k = 0;
+        for (; k < 13; ++k) {
+            w[k] = v[k];
+            if ((unsigned)(w[k] >> 32) != gen) break;
+        }
+        if (k == 13) break;
+        if (drained) return TF_HIP_ERROR;        // the stream finished without writing it
+        if ((spins & 1023u) == 1023u) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess) drained = true;   // read the record once more, then give up
+            else if (q != hipErrorNotReady) return tf_from_hip(q);
+        }
+        __builtin_ia32_pause();
+    }
+    const int mode = (int)(w[0] & 15u), ok = (int)((w[0] >> 4) & 15u) - 1;
+    if (ok < 0) {                                 // a lost peer in the persistent ICP
+        (void)hipStreamSynchronize(c->stream);
+        return TF_HIP_ERROR;
+    }
+    // host mirrors of the counters the frame end writes (tf_reset.h)
+    if (mode == 0) c->frame_counter = 1;
+    else if (ok) c->frame_counter++;
+    else { c->frame_counter = 0; c->n_resets++; }
+    if (pose_out)
+        for (int i = 0; i < 12; ++i) {
+            const unsigned bits = (unsigned)w[1 + i];
+            memcpy(&pose_out[i], &bits, sizeof(float));
+        }
+    return ok ? TF_OK : TF_ICP_FAIL;
+}
+
 extern "C" tf_status tf_process_frame(tf_ctx* c, const uint16_t* dev_depth, size_t pitch, float pose_out[12],
                                       tf_stats* stats)
 {
     if (!c || !dev_depth) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
+    if (percall_early(c, stats)) return process_frame_early(c, dev_depth, pitch, nullptr, pose_out);
     tf_status s = enqueue_frame(c, dev_depth, pitch, 0);
     if (s != TF_OK) return s;
     s = finish_frames(c, 0, 1, nullptr);
@@ -660,6 +740,7 @@ extern "C" tf_status tf_process_frame_host(tf_ctx* c, const uint16_t* host_depth
 {
     if (!c || !host_depth) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
+    if (percall_early(c, stats)) return process_frame_early(c, nullptr, pitch, host_depth, pose_out);
     TF_CHECK(hipMemcpy2DAsync(c->depth_in, (size_t)c->W * 2, host_depth, pitch, (size_t)c->W * 2, c->H,
                               hipMemcpyHostToDevice, c->stream));
     return tf_process_frame(c, c->depth_in, (size_t)c->W * 2, pose_out, stats);

@@ -320,7 +320,25 @@ struct IcpFrameArgs {
     unsigned char* visType;
     const float2* range;
     float2* snap;
+    // per-call frames (tf_process_frame): the frame's verdict -- TopFu::operator()'s return value
+    // and poses_.back() -- written to host memory as soon as it is known, so the host returns
+    // while the rest of the frame runs (tf_verdict_*, tf_capi.hip); nullptr: not requested
+    unsigned long long* verdict;
+    unsigned verdict_gen;
 };
+
+// the verdict record: TF_VERDICT_WORDS 64-bit words, each (generation << 32 | payload), written
+// with system-scope stores into fine-grained host memory; the host accepts the record once every
+// word carries the generation it armed.  Word 0: mode | (ok + 1) << 4 | iterations << 8;
+// words 1..12: the pose's float bits.
+static __device__ void icp_verdict(const IcpFrameArgs& a, int mode, int ok, int iters, const float* pose)
+{
+    const unsigned long long g = (unsigned long long)a.verdict_gen << 32;
+    for (int i = 0; i < 12; ++i)
+        __hip_atomic_store(&a.verdict[1 + i], g | __float_as_uint(pose[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.verdict[0], g | (unsigned)(mode | (ok + 1) << 4 | iters << 8), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // k_set_type3's work (render_snapshot + set_type3_pass) in every workgroup of the persistent
 // ICP grid after its last iteration: pose0 = poses_.back() read at launch (only workgroup 0
@@ -546,6 +564,11 @@ k_icp_frame(IcpFrameArgs a)
         const bool frame0 = st->frame_counter == 0;
         if (wg == 0 && tid == 0) tf_frame_begin(st);
         if (frame0) {
+            if (a.verdict && wg == 0 && tid == 0) {             // return ++frame_counter_, true (topfu.cpp:209)
+                float pose[12];
+                for (int i = 0; i < 12; ++i) pose[i] = st->pose[i];
+                icp_verdict(a, 0, 1, 0, pose);
+            }
             if (a.fold_t3) {
                 __syncthreads();
                 icp_fold_t3(a, pose0_s, nullptr, 0, 1);
@@ -810,6 +833,12 @@ k_icp_frame(IcpFrameArgs a)
                 tf_rigid_mul(pose, aff, pose);
                 for (int i = 0; i < 12; ++i) st->pose[i] = pose[i];
                 tf_set_pose_matrices(st, pose, 1);
+                if (a.verdict) icp_verdict(a, 1, 1, done, pose);
+            } else if (a.verdict) {
+                // failure: the frame end resets the pose history to [I] (topfu.cpp:263-264, reset())
+                float pose[12];
+                for (int i = 0; i < 12; ++i) pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+                icp_verdict(a, 1, status == 1 ? 1 : (status == 0 ? 0 : -1), done, pose);
             }
         }
     }
@@ -924,6 +953,10 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
             a.vis.enlarged = c->p.use_swapping ? 1 : 0;
             a.hash = c->hash; a.visibleIds = c->visibleIds; a.visType = c->visType;
             a.range = (const float2*)c->range; a.snap = (float2*)c->range_render;
+        }
+        if (c->verdict_arm && pose_update && frame_begin) {     // tf_process_frame's early return
+            a.verdict = c->verdict_dev;
+            a.verdict_gen = c->verdict_gen;
         }
         // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
         // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up

@@ -352,7 +352,17 @@ struct tf_ctx {
     hipEvent_t caller_ev;
     double prof_ms[TF_NUM_STAGES];
     long long prof_count[TF_NUM_STAGES];
+    // per-call frames (tf_process_frame, TopFu::operator()): the persistent ICP launch writes the
+    // frame's verdict (return value, pose) into fine-grained host memory and the call returns on
+    // it, with the rest of the frame still running on the stream -- as the reference returns with
+    // its CreateICPMaps / resize kernels in flight (topfu.cpp:307-329)
+    unsigned long long* verdict_host;    // TF_VERDICT_WORDS words (hipHostMallocCoherent)
+    unsigned long long* verdict_dev;     // the same memory as the device addresses it
+    unsigned verdict_gen;                // generation of the record being armed
+    int verdict_arm;                     // the frame being enqueued writes the verdict
+    int percall_early;                   // TFUSION_PERCALL_EARLY (default 1)
 };
+#define TF_VERDICT_WORDS 16
 
 // the launch of a stage's single kernel: timed by the dispatch's own timestamps when the
 // stage is being timed (c->ev_start set by STAGE_ON, consumed here), plain otherwise

@@ -405,6 +405,24 @@ __device__ __forceinline__ int block_sum(int v)
     return tot;
 }
 
+// four block sums at once (one LDS exchange instead of four)
+__device__ __forceinline__ int4 block_sum4(int4 v)
+{
+    __shared__ int4 wsum4[4];
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        v.x += __shfl_xor(v.x, o, 64); v.y += __shfl_xor(v.y, o, 64);
+        v.z += __shfl_xor(v.z, o, 64); v.w += __shfl_xor(v.w, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) wsum4[wave] = v;
+    __syncthreads();
+    int4 t = wsum4[0];
+    for (int w = 1; w < 4; ++w) { const int4 u = wsum4[w]; t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w; }
+    __syncthreads();
+    return t;
+}
+
 // ---------------------------------------------------------------------------------------
 // allocateVoxelBlocksList_device (SceneReconstructionEngine_host.cu:350-415), ordered
 // ---------------------------------------------------------------------------------------
@@ -474,7 +492,10 @@ k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int*
         a12 += c12; a2 += c2;
         if (h < (int)blockIdx.x) { p12 += c12; p2 += c2; }
     }
-    p12 = block_sum(p12); p2 = block_sum(p2); a12 = block_sum(a12); a2 = block_sum(a2);
+    {
+        const int4 t = block_sum4(make_int4(p12, p2, a12, a2));
+        p12 = t.x; p2 = t.y; a12 = t.z; a2 = t.w;
+    }
     const int v0 = st->lastFreeBlockId, e0 = st->lastFreeExcessListId;
     const bool exhausted = (a12 > v0 + 1) || (a2 > e0 + 1);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -484,35 +505,53 @@ k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int*
     int l12 = 0, l2 = 0;
     if (base < n_total)
         for (int i = 0; i < 16; ++i) { unsigned t = byte16(lo, hi, i); l12 += t != 0; l2 += t == 2; }
-    int tmp;
-    int r12 = p12 + block_excl_scan(l12, &tmp);
-    int r2 = p2 + block_excl_scan(l2, &tmp);
-    const float* invM = st->invM_alloc;
-    for (int i = 0; i < 16 && l12; ++i) {
-        int t = (int)byte16(lo, hi, i);
-        if (!t) continue;
-        int idx = base + i;
-        if (exhausted) requestList[r12] = idx;
-        else {
-            short pos[3];
-            alloc_block_from_key(a, invM, winnerKey[idx], pos);
-            TfHashEntry e; e.x = pos[0]; e.y = pos[1]; e.z = pos[2]; e.pad = 0; e.offset = 0;
-            e.ptr = allocList[v0 - r12];
-            if (t == 1) {
-                hash[idx] = e;
-                grid_set(a.grid, e, idx);
-            } else {
-                int exlOffset = excessList[e0 - r2];
-                hash[idx].offset = exlOffset + 1;
-                hash[a.n_buckets + exlOffset] = e;
-                grid_set(a.grid, e, a.n_buckets + exlOffset);
-                visType[a.n_buckets + exlOffset] = 1;
+    int wg12, tmp;
+    const int o12 = block_excl_scan(l12, &wg12);          // this thread's first request in the workgroup
+    const int r2_0 = p2 + block_excl_scan(l2, &tmp);
+    if (exhausted) {
+        int r12 = p12 + o12;
+        for (int i = 0; i < 16 && l12; ++i)
+            if (byte16(lo, hi, i)) requestList[r12++] = base + i;
+    } else if (wg12) {
+        // The workgroup's requests one per thread, in index order (request k takes free-list slot
+        // v0 - (p12 + k), its excess slot e0 - r2): the winner key, the free block and the excess
+        // slot are loaded together, then the key's depth sample; a thread holding several
+        // requests would chain those round trips.
+        __shared__ int rq_idx[256], rq_r2[256];
+        const float* invM = st->invM_alloc;
+        for (int k0 = 0; k0 < wg12; k0 += 256) {
+            int k = o12, q2 = r2_0;
+            for (int i = 0; i < 16 && l12; ++i) {
+                const unsigned t = byte16(lo, hi, i);
+                if (!t) continue;
+                if (k >= k0 && k < k0 + 256) { rq_idx[k - k0] = base + i; rq_r2[k - k0] = t == 2 ? q2 : -1; }
+                ++k;
+                if (t == 2) ++q2;
             }
-            allocType[idx] = 0;
-            winnerKey[idx] = -1;
+            __syncthreads();
+            if (k0 + (int)threadIdx.x < wg12) {
+                const int idx = rq_idx[threadIdx.x], q = rq_r2[threadIdx.x];
+                const int key = winnerKey[idx];
+                const int ptr = allocList[v0 - (p12 + k0 + (int)threadIdx.x)];
+                const int exlOffset = q >= 0 ? excessList[e0 - q] : 0;
+                short pos[3];
+                alloc_block_from_key(a, invM, key, pos);
+                TfHashEntry e; e.x = pos[0]; e.y = pos[1]; e.z = pos[2]; e.pad = 0; e.offset = 0;
+                e.ptr = ptr;
+                if (q < 0) {
+                    hash[idx] = e;
+                    grid_set(a.grid, e, idx);
+                } else {
+                    hash[idx].offset = exlOffset + 1;
+                    hash[a.n_buckets + exlOffset] = e;
+                    grid_set(a.grid, e, a.n_buckets + exlOffset);
+                    visType[a.n_buckets + exlOffset] = 1;
+                }
+                allocType[idx] = 0;
+                winnerKey[idx] = -1;
+            }
+            __syncthreads();
         }
-        r12++;
-        if (t == 2) r2++;
     }
     // Without exhaustion the counters drop by the totals (k_vis_count, next launch: every
     // workgroup here has read them).  With it, the workgroup that finishes last takes the

@@ -51,7 +51,7 @@ class TopFu:
         self._h = h
         self.W, self.H = self.params_.cols, self.params_.rows
         self.n_total = self.params_.n_buckets + self.params_.n_excess
-        self.last_stats = None
+        self._framed = False
 
     def close(self):
         if getattr(self, "_h", None):
@@ -73,26 +73,25 @@ class TopFu:
         reset).  rgb (voxel_rgb contexts): the frame's uchar4 (rows, cols, 4) image -- a host array
         with a host depth, a device pointer with a device depth."""
         lib = L.load()
-        stats = L.TfStats()
         pose = np.zeros(12, np.float32)
         if isinstance(depth, int):
             if rgb is None:
-                s = lib.tf_process_frame(self._h, ctypes.c_void_p(depth), pitch, _ptr(pose), ctypes.byref(stats))
+                s = lib.tf_process_frame(self._h, ctypes.c_void_p(depth), pitch, _ptr(pose), None)
             else:
                 s = lib.tf_process_frame_rgb(self._h, ctypes.c_void_p(depth), pitch, ctypes.c_void_p(int(rgb)), 0,
-                                             _ptr(pose), ctypes.byref(stats))
+                                             _ptr(pose), None)
         else:
             d = np.ascontiguousarray(depth, np.uint16)
             assert d.shape == (self.H, self.W), d.shape
             if rgb is None:
-                s = lib.tf_process_frame_host(self._h, _ptr(d), self.W * 2, _ptr(pose), ctypes.byref(stats))
+                s = lib.tf_process_frame_host(self._h, _ptr(d), self.W * 2, _ptr(pose), None)
             else:
                 c = np.ascontiguousarray(rgb, np.uint8)
                 assert c.shape == (self.H, self.W, 4), c.shape
                 s = lib.tf_process_frame_rgb_host(self._h, _ptr(d), self.W * 2, _ptr(c), self.W * 4, _ptr(pose),
-                                                  ctypes.byref(stats))
+                                                  None)
         L.check(s, "tf_process_frame", allow=(L.TF_OK, L.TF_ICP_FAIL))
-        self.last_stats = stats.as_dict()
+        self._framed = True
         return s == L.TF_OK
 
     def process_frames(self, dev_frames, n, stride=None, rgb_frames=None, rgb_stride=None):
@@ -131,6 +130,12 @@ class TopFu:
 
     def reset(self):
         L.check(L.load().tf_reset(self._h), "tf_reset")
+
+    @property
+    def last_stats(self):
+        """The counters after the last frame (tf_get_stats: waits for the frame's remaining work --
+        a frame call returns once its result is known, with its later stages still running)."""
+        return self.stats() if self._framed else None
 
     def stats(self):
         s = L.TfStats()
