@@ -3,10 +3,12 @@ with no host synchronisation between them, as demo.cpp's loop and bench.py's per
 
 A per-call frame returns once its verdict -- the bool and poses_.back() -- is known (the persistent
 ICP launch writes it into host memory), with its allocation, integration, raycasts and frame end
-still running, so the next call's launches queue behind them (DESIGN §6 "Per-call rate").  Every
-frame's bool and pose, and the whole state at the end, must be bit-exact with the oracle run frame
-by frame -- with the early return and without it (TFUSION_PERCALL_EARLY=0), and with a batch,
-renders and host-depth frames mixed in between.
+still running, so the next call's launches queue behind them; its last two launches are enqueued by
+the next call with that frame's preprocessing in their grid tails, or by any other entry point
+first (DESIGN §6 "Per-call rate").  Every frame's bool and pose, and the whole state at the end,
+must be bit-exact with the oracle run frame by frame -- with and without the early return
+(TFUSION_PERCALL_EARLY) and the deferred launches (TFUSION_PERCALL_DEFER), with a batch, renders
+and host-depth frames mixed in between.
 """
 import ctypes
 
@@ -19,12 +21,13 @@ from topfusion_amd import synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("early", ["1", "0"])
-def test_per_call_back_to_back(oracle_mod, monkeypatch, early):
+@pytest.mark.parametrize("early,defer", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_per_call_back_to_back(oracle_mod, monkeypatch, early, defer):
     from test_gpu_parity import _compare_frame_state, compare_scene
     from topfusion_amd import TopFu, default_params
     from topfusion_amd import _lib as L
     monkeypatch.setenv("TFUSION_PERCALL_EARLY", early)
+    monkeypatch.setenv("TFUSION_PERCALL_DEFER", defer)
     W, H, n = 640, 480, 48
     fx, fy, cx, cy = synth.intrinsics(W, H)
     args = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy)

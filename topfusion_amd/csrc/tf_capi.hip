@@ -174,6 +174,21 @@ static hipError_t dalloc(T** p, size_t bytes)
     return hipMalloc((void**)p, bytes < 16 ? 16 : bytes);
 }
 
+// A deferred per-call frame's last two launches (TfFramePlan::defer_tail): CreateICPMaps' raycast
+// + renderImage (+ CreateExpectedDepths' fill), then CreateICPMaps + the frame end.  nxt: the next
+// frame, whose bilateral pass joins the first grid and whose dists / pyramid / normals pass the
+// second (the batch's lookahead, enqueue_frame); none when flushed for another entry point.
+static tf_status flush_tail(tf_ctx* c, TfAhead nxt = TfAhead{}, size_t pitch = 0)
+{
+    if (!c->tail_pending) return TF_OK;
+    c->tail_pending = 0;
+    TF_CHECK(tfk_raycast_pair(c, TfAhead{}, nxt, pitch, c->tail_fuse_ed));
+    TF_CHECK(tfk_icp_maps_end(c, 0, nxt, pitch));
+    return TF_OK;
+}
+// every entry point but the per-call frame itself first completes a deferred frame's launches
+#define TF_FLUSH(c) do { if (c) { const tf_status fs_ = flush_tail(c); if (fs_ != TF_OK) return fs_; } } while (0)
+
 static tf_status sync_state(tf_ctx* c)
 {
     TF_CHECK(hipMemcpyAsync(c->st_host, c->st, sizeof(TfDevState), hipMemcpyDeviceToHost, c->stream));
@@ -308,9 +323,12 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->verdict_dev, c->verdict_host, 0);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     memset(c->verdict_host, 0, sizeof(unsigned long long) * TF_VERDICT_WORDS);
-    {   // TFUSION_PERCALL_EARLY=0: per-call frames wait for the whole frame (A/B)
+    {   // TFUSION_PERCALL_EARLY=0: per-call frames wait for the whole frame; TFUSION_PERCALL_DEFER=0:
+        // they enqueue all their launches (A/B)
         const char* env = getenv("TFUSION_PERCALL_EARLY");
         c->percall_early = !(env && env[0] == '0');
+        env = getenv("TFUSION_PERCALL_DEFER");
+        c->percall_defer = !(env && env[0] == '0');
     }
     // initial device state
     TfDevState s0;
@@ -390,6 +408,7 @@ extern "C" void tf_destroy(tf_ctx* c)
 
 extern "C" tf_status tf_reset(tf_ctx* c)
 {
+    TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
     return ctx_reset(c);
 }
@@ -500,6 +519,7 @@ struct TfFramePlan {
     int pre_done;            // this frame's preprocessing ran in earlier launches
     uint16_t* d0;            // this frame's level-0 depth buffer
     TfAhead alloc_bil, pair_pyr, pair_bil;
+    int defer_tail;          // leave k_raycast_pair + k_icp_maps_end to the next call (flush_tail)
 };
 
 // the view's RGB image for the integrations enqueued while in scope (voxel_rgb)
@@ -516,7 +536,7 @@ struct RgbScope {
 static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, int slot,
                                const TfFramePlan* plan = nullptr)
 {
-    static const TfFramePlan none = { 0, nullptr, {}, {}, {} };
+    static const TfFramePlan none = { 0, nullptr, {}, {}, {}, 0 };
     if (!plan) plan = &none;
     uint16_t* d0 = plan->d0 ? plan->d0 : c->d0_buf[0];
     c->prof_slot_on[slot] = c->prof_enabled && (c->prof_seq++ % c->prof_period) == 0;
@@ -537,12 +557,18 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     // in k_raycast_pair's grid when the frame is narrow enough (tfk_ed_fused), else on its own
     const int fuse_ed = tfk_ed_fused(c);
     if (!fuse_ed) STAGE(TF_STAGE_EXPECTED_DEPTHS, tfk_expected_depths(c, 1));
+    if (plan->defer_tail) {                   // per-call frame: the last two launches wait for the next call
+        c->tail_pending = 1;
+        c->tail_fuse_ed = fuse_ed;
+        return TF_OK;
+    }
     // CreateICPMaps' raycast + renderImage (topfu.cpp:284-285 + 307) in one launch (snapshot range)
     STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch, fuse_ed));
     // renderICP + resizePointsNormals (topfu.cpp:308-309) + the frame end (topfu.cpp:263-264)
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps_end(c, slot));
     return TF_OK;
 }
+
 
 // sync, read back slots [first, first+n) and the state; ok_out gets 1/0 per frame
 static tf_status finish_frames(tf_ctx* c, int first, int n, int* ok_out)
@@ -653,10 +679,19 @@ static tf_status process_frame_early(tf_ctx* c, const uint16_t* depth, size_t pi
         depth = c->depth_in;
         pitch = (size_t)c->W * 2;
     }
+    // the previous frame's deferred launches carry this frame's preprocessing in their grid tails
+    TfFramePlan plan = { 0, nullptr, {}, {}, {}, c->percall_defer };
+    if (c->tail_pending) {
+        const TfAhead nxt = { depth, c->d0_buf[0] };
+        tf_status fs = flush_tail(c, nxt, pitch);
+        if (fs != TF_OK) return fs;
+        plan.pre_done = 1;
+        plan.d0 = c->d0_buf[0];
+    }
     if (++c->verdict_gen == 0) c->verdict_gen = 1;
     const unsigned gen = c->verdict_gen;
     c->verdict_arm = 1;
-    tf_status s = enqueue_frame(c, depth, pitch, 0);
+    tf_status s = enqueue_frame(c, depth, pitch, 0, &plan);
     c->verdict_arm = 0;
     if (s != TF_OK) return s;
     // wait for the verdict: every word tagged with this generation
@@ -701,6 +736,7 @@ extern "C" tf_status tf_process_frame(tf_ctx* c, const uint16_t* dev_depth, size
     if (!c || !dev_depth) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
     if (percall_early(c, stats)) return process_frame_early(c, dev_depth, pitch, nullptr, pose_out);
+    TF_FLUSH(c);
     tf_status s = enqueue_frame(c, dev_depth, pitch, 0);
     if (s != TF_OK) return s;
     s = finish_frames(c, 0, 1, nullptr);
@@ -713,6 +749,7 @@ extern "C" tf_status tf_process_frame(tf_ctx* c, const uint16_t* dev_depth, size
 extern "C" tf_status tf_process_frame_rgb(tf_ctx* c, const uint16_t* dev_depth, size_t pitch, const uint8_t* dev_rgb,
                                           size_t rgb_pitch, float pose_out[12], tf_stats* stats)
 {
+    TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
     if (dev_rgb && !c->p.voxel_rgb) return TF_INVALID_ARG;
     RgbScope rs(c, dev_rgb, rgb_pitch);
@@ -722,6 +759,7 @@ extern "C" tf_status tf_process_frame_rgb(tf_ctx* c, const uint16_t* dev_depth, 
 extern "C" tf_status tf_process_frame_rgb_host(tf_ctx* c, const uint16_t* host_depth, size_t pitch, const uint8_t* host_rgb,
                                                size_t rgb_pitch, float pose_out[12], tf_stats* stats)
 {
+    TF_FLUSH(c);
     if (!c || !host_depth) return TF_INVALID_ARG;
     if (host_rgb && !c->p.voxel_rgb) return TF_INVALID_ARG;
     if (!host_rgb) return tf_process_frame_host(c, host_depth, pitch, pose_out, stats);
@@ -741,6 +779,7 @@ extern "C" tf_status tf_process_frame_host(tf_ctx* c, const uint16_t* host_depth
     if (!c || !host_depth) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
     if (percall_early(c, stats)) return process_frame_early(c, nullptr, pitch, host_depth, pose_out);
+    TF_FLUSH(c);
     TF_CHECK(hipMemcpy2DAsync(c->depth_in, (size_t)c->W * 2, host_depth, pitch, (size_t)c->W * 2, c->H,
                               hipMemcpyHostToDevice, c->stream));
     return tf_process_frame(c, c->depth_in, (size_t)c->W * 2, pose_out, stats);
@@ -753,12 +792,14 @@ static tf_status process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t st
 
 extern "C" tf_status tf_process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t stride, int n, int* ok_out)
 {
+    TF_FLUSH(c);
     return process_frames(c, dev_frames, stride, nullptr, 0, n, ok_out);
 }
 
 extern "C" tf_status tf_process_frames_rgb(tf_ctx* c, const uint16_t* dev_frames, size_t stride, const uint8_t* rgb_frames,
                                           size_t rgb_stride, int n, int* ok_out)
 {
+    TF_FLUSH(c);
     if (c && rgb_frames && !c->p.voxel_rgb) return TF_INVALID_ARG;
     return process_frames(c, dev_frames, stride, rgb_frames, rgb_stride, n, ok_out);
 }
@@ -775,7 +816,7 @@ static tf_status process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t st
             const int j = first + i;
             // two-frame lookahead (enqueue_frame): frame j+1's pyramid pass and frame j+2's
             // bilateral pass run in frame j's grid tails
-            TfFramePlan p = { j > 0, c->d0_buf[j & 1], {}, {}, {} };
+            TfFramePlan p = { j > 0, c->d0_buf[j & 1], {}, {}, {}, 0 };
             if (j + 1 < n) {
                 TfAhead next = { frame(j + 1), c->d0_buf[(j + 1) & 1] };
                 p.pair_pyr = next;
@@ -794,11 +835,13 @@ static tf_status process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t st
 
 extern "C" tf_status tf_render_image(tf_ctx* c, uint8_t* dev_rgba, size_t pitch)
 {   // TopFu::renderImage: raycast from poses_.back() with the current range image + grey
+    TF_FLUSH(c);
     return tf_render_image_type(c, TF_RENDER_SHADED_GREYSCALE, dev_rgba, pitch);
 }
 
 extern "C" tf_status tf_render_image_type(tf_ctx* c, int type, uint8_t* dev_rgba, size_t pitch)
 {   // VisualisationEngine_CUDA::RenderImage(..., type, RENDER_FROM_NEW_RAYCAST) from poses_.back()
+    TF_FLUSH(c);
     if (!c || type < TF_RENDER_SHADED_GREYSCALE || type > TF_RENDER_COLOUR_FROM_CONFIDENCE) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));
     TF_CHECK(hipMemcpyAsync(c->st->pose_in, c->st->pose, sizeof(float) * 12, hipMemcpyDeviceToDevice, c->stream));
@@ -816,6 +859,7 @@ extern "C" tf_status tf_render_image_type(tf_ctx* c, int type, uint8_t* dev_rgba
 
 extern "C" tf_status tf_get_pose(tf_ctx* c, float rt[12])
 {
+    TF_FLUSH(c);
     if (!c || !rt) return TF_INVALID_ARG;
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
@@ -825,6 +869,7 @@ extern "C" tf_status tf_get_pose(tf_ctx* c, float rt[12])
 
 extern "C" tf_status tf_get_stats(tf_ctx* c, tf_stats* stats)
 {
+    TF_FLUSH(c);
     if (!c || !stats) return TF_INVALID_ARG;
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
@@ -839,7 +884,11 @@ extern "C" tf_status tf_get_params(tf_ctx* c, tf_params* p)
     return TF_OK;
 }
 
-extern "C" void* tf_get_stream(tf_ctx* c) { return c ? (void*)c->stream : nullptr; }
+extern "C" void* tf_get_stream(tf_ctx* c)
+{   // (a caller that synchronises the stream itself sees every frame complete)
+    if (c) (void)flush_tail(c);
+    return c ? (void*)c->stream : nullptr;
+}
 
 extern "C" tf_status tf_get_schedule(tf_ctx* c, int* icp_persistent)
 {
@@ -859,6 +908,7 @@ static tf_status set_pose_in(tf_ctx* c, const float* rt, int mode)
 
 extern "C" tf_status tf_stage_preprocess(tf_ctx* c, const uint16_t* dev_depth, size_t pitch)
 {
+    TF_FLUSH(c);
     if (!c || !dev_depth) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
     TF_CHECK(clear_abort(c));
@@ -870,6 +920,7 @@ extern "C" tf_status tf_stage_preprocess(tf_ctx* c, const uint16_t* dev_depth, s
 
 extern "C" tf_status tf_stage_preprocess_host(tf_ctx* c, const uint16_t* host_depth, size_t pitch)
 {
+    TF_FLUSH(c);
     if (!c || !host_depth) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
     TF_CHECK(hipMemcpy2DAsync(c->depth_in, (size_t)c->W * 2, host_depth, pitch, (size_t)c->W * 2, c->H,
@@ -879,6 +930,7 @@ extern "C" tf_status tf_stage_preprocess_host(tf_ctx* c, const uint16_t* host_de
 
 extern "C" tf_status tf_stage_icp(tf_ctx* c, float affine_rt[12], int* ok, int* iterations)
 {
+    TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     TF_CHECK(tfk_icp(c, 0));
@@ -894,6 +946,7 @@ extern "C" tf_status tf_stage_icp(tf_ctx* c, float affine_rt[12], int* ok, int* 
 
 extern "C" tf_status tf_stage_alloc(tf_ctx* c, const float pose_rt[12])
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
@@ -905,6 +958,7 @@ extern "C" tf_status tf_stage_alloc(tf_ctx* c, const float pose_rt[12])
 
 extern "C" tf_status tf_stage_integrate(tf_ctx* c, const float pose_rt[12])
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
@@ -916,6 +970,7 @@ extern "C" tf_status tf_stage_integrate(tf_ctx* c, const float pose_rt[12])
 
 extern "C" tf_status tf_stage_expected_depths(tf_ctx* c, const float pose_rt[12])
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
@@ -927,6 +982,7 @@ extern "C" tf_status tf_stage_expected_depths(tf_ctx* c, const float pose_rt[12]
 
 extern "C" tf_status tf_stage_raycast(tf_ctx* c, const float invM_rt[12], int update_visible)
 {
+    TF_FLUSH(c);
     if (!c || !invM_rt) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, invM_rt, 0);
@@ -938,6 +994,7 @@ extern "C" tf_status tf_stage_raycast(tf_ctx* c, const float invM_rt[12], int up
 
 extern "C" tf_status tf_stage_icp_maps(tf_ctx* c, const float invM_rt[12])
 {
+    TF_FLUSH(c);
     if (!c || !invM_rt) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, invM_rt, 0);
@@ -949,6 +1006,7 @@ extern "C" tf_status tf_stage_icp_maps(tf_ctx* c, const float invM_rt[12])
 
 extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
 {
+    TF_FLUSH(c);
     if (!c || !invM_rt) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));                      // tracking-path kernels run (st->mode = 1)
     tf_status s = set_pose_in(c, invM_rt, 0);
@@ -960,6 +1018,7 @@ extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
 
 extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12], int iters, float* ms_per_iter)
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt || iters <= 0 || !ms_per_iter) return TF_INVALID_ARG;
     if (stage != TF_STAGE_INTEGRATE && stage != TF_STAGE_RAYCAST_ICP && stage != TF_STAGE_RAYCAST_RENDER &&
         stage != TF_STAGE_EXPECTED_DEPTHS)
@@ -994,6 +1053,7 @@ extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12]
 
 extern "C" tf_status tf_stage_reset_scene(tf_ctx* c)
 {   // SceneReconstructionEngine::ResetScene: the GlobalCache stays (SceneReconstructionEngine_host.cu:51-73)
+    TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
     TF_CHECK(tfk_reset_scene(c, 0));
     TF_CHECK(hipStreamSynchronize(c->stream));
@@ -1002,6 +1062,7 @@ extern "C" tf_status tf_stage_reset_scene(tf_ctx* c)
 
 extern "C" tf_status tf_stage_swap_pyramids(tf_ctx* c)
 {
+    TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
     swap_pyramids(c);
     return TF_OK;
@@ -1023,6 +1084,7 @@ struct IntrScope {
 
 extern "C" tf_status tf_icp_set_params(tf_ctx* c, float dist_thres, float angle_thres, const int iters[4])
 {
+    TF_FLUSH(c);
     if (!c || !iters || !(dist_thres >= 0) || !(angle_thres >= 0)) return TF_INVALID_ARG;
     if (iters[3] != 0) return TF_INVALID_ARG;            // three pyramid levels (TF_LEVELS)
     for (int l = 0; l < 4; ++l) if (iters[l] < 0) return TF_INVALID_ARG;
@@ -1037,6 +1099,7 @@ extern "C" tf_status tf_icp_set_params(tf_ctx* c, float dist_thres, float angle_
 
 extern "C" tf_status tf_icp_get_params(tf_ctx* c, float* dist_thres, float* angle_thres, int iters[4])
 {
+    TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
     if (dist_thres) *dist_thres = c->p.icp_dist_thres;
     if (angle_thres) *angle_thres = c->p.icp_angle_thres;
@@ -1065,6 +1128,7 @@ static hipError_t copy_map_in(tf_ctx* c, float4* dst, int l, const void* src, si
 extern "C" tf_status tf_icp_estimate(tf_ctx* c, const float intr[4], const tf_map_level* curr, const tf_map_level* prev,
                                      int levels, float affine_rt[12], int* ok, int* iterations)
 {
+    TF_FLUSH(c);
     if (!c || !curr || !prev || levels < 1 || levels > TF_LEVELS) return TF_INVALID_ARG;
     int used = 4;                                         // getUsedLevelsNum (projective_icp.cpp:103-108)
     while (used > 0 && c->p.icp_iter_num[used - 1] == 0) --used;
@@ -1092,6 +1156,7 @@ static hipError_t copy_dists_in(tf_ctx* c, const float* dists, size_t step)
 extern "C" tf_status tf_scene_alloc(tf_ctx* c, const float intr[4], const float pose_rt[12], const float* dists,
                                    size_t dists_step, int only_update_visible_list, int reset_visible_list)
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt || !dists) return TF_INVALID_ARG;
     TF_CHECK(order_after_caller(c));
     TF_CHECK(copy_dists_in(c, dists, dists_step));
@@ -1111,6 +1176,7 @@ extern "C" tf_status tf_scene_alloc(tf_ctx* c, const float intr[4], const float 
 extern "C" tf_status tf_scene_integrate(tf_ctx* c, const float intr[4], const float pose_rt[12], const float* dists,
                                        size_t dists_step)
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt || !dists) return TF_INVALID_ARG;
     TF_CHECK(order_after_caller(c));
     TF_CHECK(copy_dists_in(c, dists, dists_step));
@@ -1125,6 +1191,7 @@ extern "C" tf_status tf_scene_integrate(tf_ctx* c, const float intr[4], const fl
 extern "C" tf_status tf_scene_integrate_rgb(tf_ctx* c, const float intr[4], const float pose_rt[12], const float* dists,
                                            size_t dists_step, const uint8_t* dev_rgb, size_t rgb_step)
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt || !dists) return TF_INVALID_ARG;
     if (dev_rgb && !c->p.voxel_rgb) return TF_INVALID_ARG;
     RgbScope rs(c, dev_rgb, rgb_step);
@@ -1141,12 +1208,13 @@ static tf_status scene_swap(tf_ctx* c, int which)
     return TF_OK;
 }
 
-extern "C" tf_status tf_scene_swap(tf_ctx* c) { return scene_swap(c, 3); }
-extern "C" tf_status tf_scene_swap_in(tf_ctx* c) { return scene_swap(c, 1); }
-extern "C" tf_status tf_scene_swap_out(tf_ctx* c) { return scene_swap(c, 2); }
+extern "C" tf_status tf_scene_swap(tf_ctx* c) { TF_FLUSH(c); return scene_swap(c, 3); }
+extern "C" tf_status tf_scene_swap_in(tf_ctx* c) { TF_FLUSH(c); return scene_swap(c, 1); }
+extern "C" tf_status tf_scene_swap_out(tf_ctx* c) { TF_FLUSH(c); return scene_swap(c, 2); }
 
 extern "C" tf_status tf_swap_counts(tf_ctx* c, int counts[3])
 {
+    TF_FLUSH(c);
     if (!c || !counts) return TF_INVALID_ARG;
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
@@ -1158,6 +1226,7 @@ extern "C" tf_status tf_swap_counts(tf_ctx* c, int counts[3])
 // entry), then 512 voxels of 4 bytes per entry
 extern "C" tf_status tf_swap_save(tf_ctx* c, const char* path)
 {
+    TF_FLUSH(c);
     if (!c || !path || !c->p.use_swapping) return TF_INVALID_ARG;
     const size_t nf = (size_t)c->n_total, nv = sizeof(TfVoxel) * (size_t)c->n_total * TF_BLK3;
     void* host = malloc(nf + nv);
@@ -1177,6 +1246,7 @@ extern "C" tf_status tf_swap_save(tf_ctx* c, const char* path)
 
 extern "C" tf_status tf_swap_load(tf_ctx* c, const char* path)
 {
+    TF_FLUSH(c);
     if (!c || !path || !c->p.use_swapping) return TF_INVALID_ARG;
     const size_t nf = (size_t)c->n_total, nv = sizeof(TfVoxel) * (size_t)c->n_total * TF_BLK3;
     FILE* f = fopen(path, "rb");
@@ -1198,6 +1268,7 @@ extern "C" tf_status tf_swap_load(tf_ctx* c, const char* path)
 
 extern "C" tf_status tf_vis_expected_depths(tf_ctx* c, const float intr[4], const float pose_rt[12])
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt) return TF_INVALID_ARG;
     IntrScope is(c, intr);
     return tf_stage_expected_depths(c, pose_rt);
@@ -1206,6 +1277,7 @@ extern "C" tf_status tf_vis_expected_depths(tf_ctx* c, const float intr[4], cons
 extern "C" tf_status tf_vis_render_image(tf_ctx* c, const float intr[4], const float pose_rt[12], int type, int new_raycast,
                                         uint8_t* dev_rgba, size_t step)
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt || type < TF_RENDER_SHADED_GREYSCALE || type > TF_RENDER_COLOUR_FROM_CONFIDENCE) return TF_INVALID_ARG;
     IntrScope is(c, intr);
     tf_status s = set_pose_in(c, pose_rt, 0);
@@ -1224,6 +1296,7 @@ extern "C" tf_status tf_vis_render_image(tf_ctx* c, const float intr[4], const f
 extern "C" tf_status tf_vis_icp_maps(tf_ctx* c, const float intr[4], const float pose_rt[12], void* points,
                                     size_t points_step, void* normals, size_t normals_step)
 {
+    TF_FLUSH(c);
     if (!c || !pose_rt) return TF_INVALID_ARG;
     IntrScope is(c, intr);
     tf_status s = set_pose_in(c, pose_rt, 0);
@@ -1273,12 +1346,14 @@ static void* buffer_ptr(tf_ctx* c, int which, int level, size_t* bytes)
 
 extern "C" tf_status tf_buffer_bytes(tf_ctx* c, int which, int level, size_t* bytes)
 {
+    TF_FLUSH(c);
     if (!c || !bytes) return TF_INVALID_ARG;
     return buffer_ptr(c, which, level, bytes) ? TF_OK : TF_INVALID_ARG;
 }
 
 extern "C" tf_status tf_download(tf_ctx* c, int which, int level, void* host, size_t bytes)
 {
+    TF_FLUSH(c);
     if (!c || !host) return TF_INVALID_ARG;
     size_t n;
     void* p = buffer_ptr(c, which, level, &n);
@@ -1290,6 +1365,7 @@ extern "C" tf_status tf_download(tf_ctx* c, int which, int level, void* host, si
 
 extern "C" tf_status tf_download_range(tf_ctx* c, int which, size_t offset, void* host, size_t bytes)
 {
+    TF_FLUSH(c);
     if (!c || !host) return TF_INVALID_ARG;
     size_t n;
     void* p = buffer_ptr(c, which, 0, &n);
@@ -1301,6 +1377,7 @@ extern "C" tf_status tf_download_range(tf_ctx* c, int which, size_t offset, void
 
 extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host, size_t bytes)
 {
+    TF_FLUSH(c);
     if (!c || !host) return TF_INVALID_ARG;
     size_t n;
     void* p = buffer_ptr(c, which, level, &n);
@@ -1317,6 +1394,7 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
 
 extern "C" tf_status tf_set_pose(tf_ctx* c, const float rt[12])
 {
+    TF_FLUSH(c);
     if (!c || !rt) return TF_INVALID_ARG;
     TF_CHECK(hipMemcpyAsync(c->st->pose, rt, sizeof(float) * 12, hipMemcpyHostToDevice, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
@@ -1325,6 +1403,7 @@ extern "C" tf_status tf_set_pose(tf_ctx* c, const float rt[12])
 
 extern "C" tf_status tf_set_counters(tf_ctx* c, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries)
 {
+    TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
@@ -1339,6 +1418,7 @@ extern "C" tf_status tf_set_counters(tf_ctx* c, int lastFreeBlockId, int lastFre
 
 extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)
 {
+    TF_FLUSH(c);
     if (!c || !t) return TF_INVALID_ARG;
     tf_status s = sync_state(c);
     if (s != TF_OK) return s;
@@ -1357,6 +1437,7 @@ extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)
 
 extern "C" tf_status tf_reset_totals(tf_ctx* c)
 {
+    TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
     const size_t b = offsetof(TfDevState, tot_frames), e = offsetof(TfDevState, tot_swap_merged) + sizeof(long long);
     TF_CHECK(hipMemsetAsync((char*)c->st + b, 0, e - b, c->stream));

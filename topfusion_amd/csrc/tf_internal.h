@@ -361,6 +361,13 @@ struct tf_ctx {
     unsigned verdict_gen;                // generation of the record being armed
     int verdict_arm;                     // the frame being enqueued writes the verdict
     int percall_early;                   // TFUSION_PERCALL_EARLY (default 1)
+    // ... and a per-call frame leaves its last two launches (k_raycast_pair, k_icp_maps_end)
+    // unenqueued: the next call enqueues them with its own frame's bilateral and pyramid passes in
+    // their grid tails (the batch's lookahead), every other entry point first enqueues them as
+    // they are (flush_tail, tf_capi.hip)
+    int tail_pending;
+    int tail_fuse_ed;
+    int percall_defer;                   // TFUSION_PERCALL_DEFER (default 1)
 };
 #define TF_VERDICT_WORDS 16
 
@@ -420,7 +427,8 @@ int tfk_ed_fused(const tf_ctx* c);
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_render_snapshot(tf_ctx* c);   // render_snapshot as its own launch
 // CreateICPMaps + the frame end (tfk_reset_scene_on_failure) in one grid (the frame path)
-hipError_t tfk_icp_maps_end(tf_ctx* c, int slot);
+// pyr: + that frame's dists / pyramid / normals pass (its level-0 depth already in pyr.d0)
+hipError_t tfk_icp_maps_end(tf_ctx* c, int slot, TfAhead pyr = TfAhead{}, size_t pitch = 0);
 #define TF_END_BLOCKS 256        // workgroups of the frame-end / in-frame reset pass
 // keep_bins: the fill leaves the projection's bins in place (repeated fills of tf_time_stage)
 hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0, int keep_bins = 0);

@@ -919,12 +919,18 @@ k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
 // ResetScene of topfu.cpp:263-264 when ICP failed).  The two share nothing: the maps pass
 // reads the raycast and writes the previous-frame maps, and does nothing on a failed frame;
 // the frame end writes the pose / counters only, and the scene only on a failed frame.
+// n_pyr > 0 (per-call frames, process_frame_early): the next frame's dists / pyramid / normals
+// pass in the grid's last workgroups -- it writes only the current maps, the level 1-2 depths and
+// dists, which nothing of this frame reads any more, and its level-0 depth came from the
+// bilateral pass in this frame's k_raycast_pair.
 __global__ void __launch_bounds__(256)
-k_icp_maps_end(IcpMapArgs a, ResetArgs r, int gx, int nmaps)
+k_icp_maps_end(IcpMapArgs a, ResetArgs r, int gx, int nmaps, PyrArgs pyr, int pyr_gx)
 {
+    __shared__ PnLds pn;
     const int b = blockIdx.x;
     if (b < nmaps) icp_maps_block(a, r.st, b % gx, b / gx);
-    else reset_scene_block(r, b - nmaps, TF_END_BLOCKS);
+    else if (b < nmaps + TF_END_BLOCKS) reset_scene_block(r, b - nmaps, TF_END_BLOCKS);
+    else pyr_normals_block<256>(pyr, (b - nmaps - TF_END_BLOCKS) % pyr_gx, (b - nmaps - TF_END_BLOCKS) / pyr_gx, pn);
 }
 
 hipError_t tfk_icp_maps(tf_ctx* c)
@@ -937,7 +943,7 @@ hipError_t tfk_icp_maps(tf_ctx* c)
     return hipGetLastError();
 }
 
-hipError_t tfk_icp_maps_end(tf_ctx* c, int slot)
+hipError_t tfk_icp_maps_end(tf_ctx* c, int slot, TfAhead pyr, size_t pitch)
 {
     IcpMapArgs a;
     a.ray = (const float4*)c->raycast;
@@ -946,7 +952,16 @@ hipError_t tfk_icp_maps_end(tf_ctx* c, int slot)
     ResetArgs r;
     tf_reset_args(c, &r, 1, slot, 1);
     const int gx = (c->W + 31) / 32, nmaps = gx * ((c->H + 31) / 32);
-    tf_launch(c, k_icp_maps_end, dim3(nmaps + TF_END_BLOCKS), dim3(256), 0, a, r, gx, nmaps);
+    PyrArgs pp = PyrArgs{};
+    int n_pyr = 0, pyr_gx = 1;
+    if (pyr.src) {
+        BilArgs bx;
+        const hipError_t e = tf_pre_args(c, pyr.src, pitch, 1, pyr.d0, &bx, &pp);
+        if (e != hipSuccess) return e;
+        pyr_gx = tf_div_up(c->W, PN_T0);
+        n_pyr = pyr_gx * tf_div_up(c->H, PN_T0);
+    }
+    tf_launch(c, k_icp_maps_end, dim3(nmaps + TF_END_BLOCKS + n_pyr), dim3(256), 0, a, r, gx, nmaps, pp, pyr_gx);
     return hipGetLastError();
 }
 
