@@ -405,13 +405,15 @@ def walk_frames(n, W, H, seed, device):
 
 
 def per_call_rate(tf, base, frame_bytes, n):
-    """TopFu::operator() semantics (demo.cpp:102-105): one tf_process_frame call per frame, each
-    synchronous (a host round trip per frame, no lookahead), wall clock over n frames."""
+    """TopFu::operator() semantics (demo.cpp:102-105): one tf_process_frame call per frame (each
+    returns on its frame's ICP verdict; its last two launches go out with the next call), wall
+    clock over n frames including the last frame's whole work."""
     import torch
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(n):
         tf(base + k * frame_bytes)
+    tf.stats()                 # (the last frame's deferred launches, enqueued and waited for)
     torch.cuda.synchronize()
     return n / (time.perf_counter() - t0)
 
@@ -535,7 +537,7 @@ def main():
         nvis_bd = tbt["visible_sum"] / n_int
         tb.close()
         torch.cuda.synchronize()
-    # TopFu::operator() per call (one host round trip per frame, no lookahead) over the first
+    # TopFu::operator() per call (one call per frame, returning on the frame's verdict) over the first
     # frames of the timed region, from a fresh context, and the batched rate of a fresh context on
     # the same frames beside it (the orbit's cost per frame varies along it: compare like with like)
     per_call = per_call_batched = None
@@ -642,7 +644,9 @@ def main():
             "per_call_frames_per_sec": None if per_call is None else round(per_call, 2),
             "per_call_batched_same_frames": None if per_call_batched is None else round(per_call_batched, 2),
             "per_call": (f"TopFu::operator() per call: tf_process_frame on the timed region's first {nc} frames from a "
-                         "fresh context, one host round trip per frame, no lookahead (demo.cpp:102-105 semantics); "
+                         "fresh context, one call per frame (demo.cpp:102-105 semantics: each returns on its frame's ICP verdict, its "
+                         "last two launches go out with the next call, carrying that frame's preprocessing; the time ends after "
+                         "the last frame's whole work); "
                          "per_call_batched_same_frames: tf_process_frames on the same frames from a fresh context")
                         if per_call is not None else None,
             "icp_integrate_ms_per_frame": None if icp_integ is None else round(icp_integ, 4),
