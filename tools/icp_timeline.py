@@ -36,3 +36,15 @@ for i in range(its):
     if nxt is not None:
         line += f" next-start {nxt.min():5.2f}/{np.median(nxt):5.2f}/{nxt.max():5.2f}"
     print(line)
+# the shader clock workgroup 0 ran at (s_memtime against the 100 MHz s_memrealtime)
+try:
+    cb = (ctypes.c_ulonglong * 128)()
+    _lib.load().tf_debug_icp_clock(cb)
+    ck = np.frombuffer(cb, dtype=np.uint64).reshape(64, 2).astype(np.int64)
+    n = its
+    if n > 1:
+        dm = ck[n - 1, 0] - ck[0, 0]
+        dr = ck[n - 1, 1] - ck[0, 1]
+        print(f"shader clock over iterations 0..{n - 1}: {dm / dr * 100.0:.0f} MHz ({dm} s_memtime ticks in {dr / 100.0:.2f} us)")
+except Exception as ex:
+    print("clock:", ex)

@@ -43,6 +43,15 @@ extern "C" int tf_debug_icp_timeline(unsigned long long* out)
 {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_tl), sizeof(g_icp_tl), 0, hipMemcpyDeviceToHost);
 }
+// workgroup 0's shader clock (s_memtime) beside the 100 MHz clock at each iteration start: the
+// shader clock the kernel ran at
+__device__ unsigned long long g_icp_clk[64 * 2];
+#define IPT_CLK(it) do { if (blockIdx.x == 0 && threadIdx.x == 0 && (it) < 64) { \
+    g_icp_clk[2 * (it)] = __builtin_amdgcn_s_memtime(); g_icp_clk[2 * (it) + 1] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+extern "C" int tf_debug_icp_clock(unsigned long long* out)
+{
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_clk), sizeof(g_icp_clk), 0, hipMemcpyDeviceToHost);
+}
 #else
 #define ICP_TS0()
 #define ICP_TS(k)
@@ -50,6 +59,7 @@ extern "C" int tf_debug_icp_timeline(unsigned long long* out)
 #define IPT_ADD(k, v) do { } while (0)
 #define IPT_REC(it, slot) do { } while (0)
 #define IPT_REC_T(it, slot, t) do { } while (0)
+#define IPT_CLK(it) do { } while (0)
 #endif
 
 struct IcpLevel {
@@ -626,6 +636,7 @@ k_icp_frame(IcpFrameArgs a)
         for (int it = 0; it < iters; ++it) {
             ++gen;
             IPT_REC(done, wg);
+            IPT_CLK(done);
             if (det_pending && wave == IP_DETW) {
                 float Am[6][6], bv[6];
                 ip_unpack(det_sm, Am, bv);
