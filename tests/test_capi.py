@@ -118,3 +118,31 @@ def test_random_walk_synth():
     host = synth.random_walk_sequence(2, 96, 72, seed=13, noise_mm=0.0)
     dev = synth.render_depth_torch(R[:2], t[:2], 96, 72, noise_mm=0.0, device="cpu").numpy().view(np.uint16)
     assert np.array_equal(host, dev)
+
+
+def test_entry_points_flush_deferred_frame():
+    """A per-call frame leaves its last two launches to the next call (tf_capi.hip flush_tail): every
+    other C-ABI entry point that takes a context must enqueue them first (TF_FLUSH), so that it
+    sees the whole frame.  Static check of tf_capi.hip: the only entry points without it are the
+    per-call frame itself (it flushes with its own frame's lookahead) and the host-only ones."""
+    import re
+    src = open(os.path.join(ROOT, "topfusion_amd", "csrc", "tf_capi.hip")).read()
+    host_only = {"tf_destroy", "tf_get_params", "tf_get_stream", "tf_get_schedule", "tf_profile_enable",
+                 "tf_profile_stages", "tf_profile_sample", "tf_profile_reset", "tf_profile_read"}
+    per_call = {"tf_process_frame", "tf_process_frame_host"}
+    checked = 0
+    for m in re.finditer(r'extern "C" [^(]*\b(tf_\w+)\(([^)]*)\)\s*\{', src):
+        name, args = m.group(1), m.group(2)
+        if "tf_ctx* c" not in args or name in host_only:
+            continue
+        body = src[m.end():src.index("\n}", m.end()) if "\n}" in src[m.end():] else len(src)]
+        head = body[:400]
+        if name in per_call:
+            assert "process_frame_early" in head and "TF_FLUSH(c)" in head, name
+        else:
+            assert "TF_FLUSH(c)" in head, f"{name} does not flush a deferred per-call frame"
+        checked += 1
+    assert checked >= 40, checked
+    # tf_get_stream hands the stream out: a caller synchronising it itself must see whole frames
+    gs = src[src.index('extern "C" void* tf_get_stream'):]
+    assert "flush_tail(c)" in gs[:300]
