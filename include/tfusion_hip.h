@@ -99,8 +99,10 @@ typedef enum tf_buffer {
     TF_BUF_SWAP_STATE = 13,   /* uchar[n_buckets+n_excess] HashSwapState::state (GlobalCache.hpp:11-20) */
     TF_BUF_SWAP_STORED_FLAGS = 14,  /* uchar[n_buckets+n_excess] GlobalCache hasStoredData */
     TF_BUF_SWAP_STORED = 15,  /* Voxel_s[(n_buckets+n_excess)*512] GlobalCache storedVoxelBlocks */
-    TF_BUF_VBA_RGB = 16       /* voxel_rgb: uint32[n_blocks*512] Voxel_s_rgb clr + w_color (VoxelTypes.hpp:39-67),
+    TF_BUF_VBA_RGB = 16,      /* voxel_rgb: uint32[n_blocks*512] Voxel_s_rgb clr + w_color (VoxelTypes.hpp:39-67),
                                  r | g << 8 | b << 16 | w_color << 24 -- the colour half of each voxel */
+    TF_BUF_ALLOC_LIST = 17,   /* int[n_blocks] LocalVBA::allocationList, the free-block stack (LocalVBA.hpp:19, 35) */
+    TF_BUF_EXCESS_LIST = 18   /* int[n_excess] VoxelBlockHash::excessAllocationList (VoxelBlockHash.hpp:81, 88) */
 } tf_buffer;
 
 /* ---- device ---------------------------------------------------------------- */
@@ -247,6 +249,33 @@ tf_status tf_scene_swap_in(tf_ctx* ctx);
 tf_status tf_scene_swap_out(tf_ctx* ctx);
 /* blocks swapped in / out and reallocated by the last frame (or tf_scene_* call) */
 tf_status tf_swap_counts(tf_ctx* ctx, int counts[3]);
+/* The state after each frame of tf_scene_fuse_frames (no reference counterpart: the reference keeps
+ * these counters host-side, LocalVBA.hpp:26, VoxelBlockHash.hpp:69, RenderState_VH.hpp:33, and its
+ * allocation failures are silent, SceneReconstructionEngine_host.cu:374-381, 398-401). */
+typedef struct tf_fuse_record {
+    int lastFreeBlockId;
+    int lastFreeExcessListId;
+    int noVisibleEntries;
+    int alloc_failed_type1;             /* this frame's requests refused for want of a free block */
+    int alloc_failed_type2;             /* ... excess-list requests refused (no block or no excess slot) */
+    int swapped_in;                     /* use_swapping: IntegrateGlobalIntoLocal's state 1 -> 2 entries */
+    int swapped_out;                    /* SaveToGlobalMemory's blocks moved to the GlobalCache and freed */
+    int swap_realloc;                   /* reAllocateSwappedOutVoxelBlocks' blocks */
+    int swapped_in_merged;              /* stored blocks merged back into the VBA */
+    int pad;
+} tf_fuse_record;
+/* Engine-level fusion of n device-resident frames at given poses with no host round trip inside,
+ * TopFu's call order without the tracker: for frame k, cuda::computeDists(depth_k) (imgproc.cu:
+ * 263-290, topfu.cpp:166), SceneReconstructionEngine_CUDA::AllocateSceneFromDepth(scene, intr,
+ * poses[k], dists, renderState) and ::IntegrateIntoScene(...) (SceneReconstructionEngine_host.cu:
+ * 75-251, topfu.cpp:202-203), then with use_swapping the swapping engine (tf_scene_swap).  The
+ * results equal tf_imgproc_compute_dists + tf_scene_alloc + tf_scene_integrate (+ tf_scene_swap)
+ * called per frame.  dev_frames: uint16 depth, frame k at dev_frames + k * frame_stride_bytes, rows
+ * pitch_bytes apart (0: cols * 2); poses_rt: n world -> camera poses (host, row-major [R|t], as
+ * tf_scene_alloc takes them); intr: NULL = the context's; records: NULL or n host records.
+ * Returns when the batch is done. */
+tf_status tf_scene_fuse_frames(tf_ctx* ctx, const float intr[4], const uint16_t* dev_frames, size_t frame_stride_bytes,
+                               size_t pitch_bytes, const float* poses_rt, int n, tf_fuse_record* records);
 /* GlobalCache::SaveToFile / ReadFromFile (GlobalCache.hpp:79-110): hasStoredData as one byte per
  * entry, then every entry's 512 voxels (4 B each), n_buckets + n_excess entries */
 tf_status tf_swap_save(tf_ctx* ctx, const char* path);
@@ -342,6 +371,10 @@ typedef struct tf_totals {
     long long integrate_lanes_read;     /* 16-B voxel lanes (4 voxels) integration read: those with an update */
     long long integrate_lanes_written;  /* ... and wrote back: those whose value changed */
     long long swapped_in_merged;    /* the swap-ins whose entry held stored data: GlobalCache -> VBA transfers */
+    long long alloc_failed_type1;   /* allocation requests that failed silently for want of a free voxel block
+                                       (allocateVoxelBlocksList, SceneReconstructionEngine_host.cu:374-381) */
+    long long alloc_failed_type2;   /* ... excess-list requests that failed for want of a block or an excess
+                                       slot (:386-411) */
 } tf_totals;
 tf_status tf_get_totals(tf_ctx* ctx, tf_totals* totals);
 tf_status tf_reset_totals(tf_ctx* ctx);

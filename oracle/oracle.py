@@ -105,7 +105,8 @@ def lib(omp=False):
         L.tfo_swap_in.argtypes = [P]
         L.tfo_swap_out.argtypes = [P]
         L.tfo_swap_counts.argtypes = [P, P]
-        for name in ("tfo_hash", "tfo_vba", "tfo_visible_ids", "tfo_visible_type", "tfo_range_image",
+        L.tfo_alloc_failures.argtypes = [P, P]
+        for name in ("tfo_alloc_list", "tfo_excess_list", "tfo_hash", "tfo_vba", "tfo_visible_ids", "tfo_visible_type", "tfo_range_image",
                      "tfo_raycast_result", "tfo_dists", "tfo_frame_grey", "tfo_swap_state", "tfo_swap_stored_flags",
                      "tfo_swap_stored", "tfo_vba_rgb"):
             getattr(L, name).argtypes = [P]; getattr(L, name).restype = P
@@ -306,6 +307,38 @@ class Oracle:
         h = np.ascontiguousarray(h, HASH_DTYPE)
         assert h.shape == (self.n_total,)
         self._view(self.L.tfo_hash(self.ctx), HASH_DTYPE, self.n_total)[:] = h
+
+    def alloc_list(self):
+        """LocalVBA::allocationList, the free-block stack."""
+        return self._view(self.L.tfo_alloc_list(self.ctx), np.int32, self.params.n_blocks).copy()
+
+    def excess_list(self):
+        return self._view(self.L.tfo_excess_list(self.ctx), np.int32, self.params.n_excess).copy()
+
+    def alloc_failures(self):
+        """(type-1, type-2) allocation requests the last AllocateSceneFromDepth refused."""
+        out = np.zeros(2, np.int32)
+        self.L.tfo_alloc_failures(self.ctx, ptr(out))
+        return int(out[0]), int(out[1])
+
+    def load_scene_state(self, hash, vba, alloc_list, excess_list, visible_ids, visible_type, counters,
+                         swap_state=None, swap_stored_flags=None, swap_stored=None):
+        """Overwrite the scene and render-state arrays the engine-level passes read (a state taken
+        from another implementation, e.g. the GPU's at frame k of a stream): hash, voxels, both
+        free lists, the visible list and types, the counters (lastFreeBlockId,
+        lastFreeExcessListId, noVisibleEntries) and, in a swapping scene, the GlobalCache."""
+        n_tot, nb = self.n_total, self.params.n_blocks
+        self._view(self.L.tfo_hash(self.ctx), HASH_DTYPE, n_tot)[:] = np.asarray(hash, HASH_DTYPE)
+        self._view(self.L.tfo_vba(self.ctx), VOXEL_DTYPE, nb * 512)[:] = np.asarray(vba, VOXEL_DTYPE)
+        self._view(self.L.tfo_alloc_list(self.ctx), np.int32, nb)[:] = alloc_list
+        self._view(self.L.tfo_excess_list(self.ctx), np.int32, self.params.n_excess)[:] = excess_list
+        self._view(self.L.tfo_visible_ids(self.ctx), np.int32, self.params.vis_capacity)[:] = visible_ids
+        self._view(self.L.tfo_visible_type(self.ctx), np.uint8, n_tot)[:] = visible_type
+        self.set_counters(*counters)
+        if self.params.use_swapping:
+            self._view(self.L.tfo_swap_state(self.ctx), np.uint8, n_tot)[:] = swap_state
+            self._view(self.L.tfo_swap_stored_flags(self.ctx), np.uint8, n_tot)[:] = swap_stored_flags
+            self._view(self.L.tfo_swap_stored(self.ctx), VOXEL_DTYPE, n_tot * 512)[:] = np.asarray(swap_stored, VOXEL_DTYPE)
 
     def upload_visible_ids(self, ids):
         ids = np.ascontiguousarray(ids, np.int32)

@@ -531,6 +531,7 @@ struct tfo_ctx {
     tfo_voxel* vba;
     int* allocList;
     int lastFreeBlockId, lastFreeExcessListId;
+    int alloc_failed[2];      /* the last allocateVoxelBlocksList's failed type-1 / type-2 requests */
     /* SceneReconstructionEngine_CUDA temporaries */
     uint8_t* allocType;
     int16_t* blockCoords;     /* 4 shorts per entry */
@@ -683,6 +684,7 @@ int tfo_copy_state(tfo_ctx* d, const tfo_ctx* s)
     }
     if (s->p.voxel_rgb) memcpy(d->vba_rgb, s->vba_rgb, sizeof(uint32_t) * nb * BLK3);
     d->lastFreeBlockId = s->lastFreeBlockId; d->lastFreeExcessListId = s->lastFreeExcessListId;
+    d->alloc_failed[0] = s->alloc_failed[0]; d->alloc_failed[1] = s->alloc_failed[1];
     d->noVisibleEntries = s->noVisibleEntries; d->noTotalBlocks = s->noTotalBlocks;
     d->frame_counter = s->frame_counter;
     memcpy(d->pose, s->pose, sizeof(d->pose));
@@ -858,6 +860,7 @@ void tfo_alloc_ex(tfo_ctx* c, const float pose_rt[12], const float* dists, int o
     int noVisibleEntries = 0;
     if (reset_visible) c->noVisibleEntries = 0;
     memset(c->allocType, 0, (size_t)c->n_total);
+    c->alloc_failed[0] = c->alloc_failed[1] = 0;
     /* setToType3, :343-348 */
     for (int i = 0; i < c->noVisibleEntries; ++i) c->visType[c->visibleIds[i]] = 3;
     /* buildHashAllocAndVisibleType_device, :331-341, serial raster order */
@@ -879,6 +882,7 @@ void tfo_alloc_ex(tfo_ctx* c, const float pose_rt[12], const float* dists, int o
             } else {
                 c->visType[t] = 0;
                 noAllocatedVoxelEntries++;
+                c->alloc_failed[0]++;
             }
             break;
         case 2:
@@ -896,6 +900,7 @@ void tfo_alloc_ex(tfo_ctx* c, const float pose_rt[12], const float* dists, int o
             } else {
                 noAllocatedVoxelEntries++;
                 noAllocatedExcessEntries++;
+                c->alloc_failed[1]++;
             }
             break;
         default: break;
@@ -1794,6 +1799,9 @@ void tfo_set_counters(tfo_ctx* c, int lastFreeBlockId, int lastFreeExcessListId,
     c->noVisibleEntries = noVisibleEntries;
 }
 tfo_hash_entry* tfo_hash(tfo_ctx* c) { return c->hash; }
+int* tfo_alloc_list(tfo_ctx* c) { return c->allocList; }
+int* tfo_excess_list(tfo_ctx* c) { return c->excessList; }
+void tfo_alloc_failures(const tfo_ctx* c, int out[2]) { out[0] = c->alloc_failed[0]; out[1] = c->alloc_failed[1]; }
 tfo_voxel* tfo_vba(tfo_ctx* c) { return c->vba; }
 uint32_t* tfo_vba_rgb(tfo_ctx* c) { return c->vba_rgb; }
 int* tfo_visible_ids(tfo_ctx* c) { return c->visibleIds; }

@@ -162,6 +162,9 @@ uint8_t* tfo_swap_stored_flags(tfo_ctx* c);         /* GlobalCache hasStoredData
 tfo_voxel* tfo_swap_stored(tfo_ctx* c);             /* GlobalCache storedVoxelBlocks, 512 per entry */
 /* state access */
 tfo_hash_entry* tfo_hash(tfo_ctx* c);
+int* tfo_alloc_list(tfo_ctx* c);        /* LocalVBA::allocationList (n_blocks) */
+int* tfo_excess_list(tfo_ctx* c);       /* VoxelBlockHash::excessAllocationList (n_excess) */
+void tfo_alloc_failures(const tfo_ctx* c, int out[2]);   /* last allocation: failed type-1, type-2 requests */
 tfo_voxel* tfo_vba(tfo_ctx* c);
 uint32_t* tfo_vba_rgb(tfo_ctx* c);   /* voxel_rgb: per voxel r | g << 8 | b << 16 | w_color << 24 */
 int* tfo_visible_ids(tfo_ctx* c);

@@ -7,6 +7,8 @@ import ctypes
 import os
 import re
 
+import numpy as np
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TFUSION_HIP_LIB") or os.path.join(_HERE, "libtfusion_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tfusion_hip.h")
@@ -18,7 +20,8 @@ STAGE_NAMES = ("preprocess", "icp", "alloc", "integrate", "raycast_render", "gre
 
 (TF_BUF_HASH, TF_BUF_VBA, TF_BUF_VISIBLE_IDS, TF_BUF_VISIBLE_TYPE, TF_BUF_RANGE, TF_BUF_RAYCAST, TF_BUF_DISTS,
  TF_BUF_DEPTH, TF_BUF_CURR_POINTS, TF_BUF_CURR_NORMALS, TF_BUF_PREV_POINTS, TF_BUF_PREV_NORMALS, TF_BUF_GREY,
- TF_BUF_SWAP_STATE, TF_BUF_SWAP_STORED_FLAGS, TF_BUF_SWAP_STORED, TF_BUF_VBA_RGB) = range(17)
+ TF_BUF_SWAP_STATE, TF_BUF_SWAP_STORED_FLAGS, TF_BUF_SWAP_STORED, TF_BUF_VBA_RGB, TF_BUF_ALLOC_LIST,
+ TF_BUF_EXCESS_LIST) = range(19)
 
 
 class TfParams(ctypes.Structure):
@@ -49,10 +52,16 @@ class TfStats(ctypes.Structure):
 class TfTotals(ctypes.Structure):
     _fields_ = [(n, ctypes.c_longlong) for n in ("frames", "frames_tracked", "resets", "visible_sum", "tiles_sum",
                                                  "swapped_in", "swapped_out", "integrate_lanes_read",
-                                                 "integrate_lanes_written", "swapped_in_merged")]
+                                                 "integrate_lanes_written", "swapped_in_merged",
+                                                 "alloc_failed_type1", "alloc_failed_type2")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+FUSE_RECORD_FIELDS = ("lastFreeBlockId", "lastFreeExcessListId", "noVisibleEntries", "alloc_failed_type1",
+                      "alloc_failed_type2", "swapped_in", "swapped_out", "swap_realloc", "swapped_in_merged", "pad")
+FUSE_RECORD_DTYPE = np.dtype([(n, "<i4") for n in FUSE_RECORD_FIELDS])   # tf_fuse_record
 
 
 class TfMapLevel(ctypes.Structure):
@@ -135,6 +144,7 @@ def load():
         "tf_scene_integrate_rgb": ([P, P, P, P, S, P, S], I),
         "tf_vis_expected_depths": ([P, P, P], I),
         "tf_scene_swap": ([P], I),
+        "tf_scene_fuse_frames": ([P, P, P, S, S, P, I, P], I),
         "tf_scene_swap_in": ([P], I),
         "tf_scene_swap_out": ([P], I),
         "tf_swap_counts": ([P, P], I),

@@ -151,10 +151,10 @@ static void ctx_free(tf_ctx* c)
     }
     if (c->caller_ev) (void)hipEventDestroy(c->caller_ev);
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
-                     c->requestList, c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
+                     c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->edBins, c->edBinCnt, c->edDone, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
-                     c->vba_rgb_guard, c->rgb_in, c->integ_cnt };
+                     c->vba_rgb_guard, c->rgb_in, c->integ_cnt, c->fuse_pose, c->fuse_rec };
     for (void* b : bufs) if (b) (void)hipFree(b);
     // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
     float4* maps[4] = { c->curr_pts[0], c->curr_nrm[0], c->prev_pts[0], c->prev_nrm[0] };
@@ -255,7 +255,6 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->allocType, ntot_pad);
     ALLOC(c->winnerKey, sizeof(int) * ntot_pad);
     ALLOC(c->allocCounts, sizeof(int) * 2 * (size_t)c->alloc_chunks);
-    ALLOC(c->requestList, sizeof(int) * (size_t)c->n_total);
     ALLOC(c->visCounts, sizeof(int) * (size_t)c->vis_chunks);
     ALLOC(c->visibleIds, sizeof(int) * (size_t)pin->vis_capacity);
     ALLOC(c->visType, ntot_pad);
@@ -268,7 +267,17 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->blockOff, sizeof(int) * (size_t)pin->vis_capacity);
     ALLOC(c->edChunk, sizeof(int) * ((size_t)pin->vis_capacity / 256 + 1));
     ALLOC(c->edSpill, sizeof(int2) * (size_t)ed_nrows(c->H));
-    ALLOC(c->edBins, sizeof(uint4) * 2 * (size_t)ed_nrows(c->H) * ED_LDS_MAX_N);
+    {   // k_ed_fill: LDS rows up to ED_LDS_MAX_N visible entries, device-scope atomics past that
+        // (TFUSION_ED_LDS_MAX_N overrides the threshold; the parity tests run both paths)
+        const char* env = getenv("TFUSION_ED_LDS_MAX_N");
+        c->ed_lds_max_n = env ? atoi(env) : ED_LDS_MAX_N;
+        if (c->ed_lds_max_n > ED_LDS_MAX_N) c->ed_lds_max_n = ED_LDS_MAX_N;
+        if (c->ed_lds_max_n > pin->vis_capacity) c->ed_lds_max_n = pin->vis_capacity;   // (a bin holds <= n boxes)
+        // the binned boxes hold 12-bit coordinates (tf_ed.h ed_bin_pack), the fill's LDS rows ED_MAX_ROWS
+        if (c->W > ED_MAX_W || c->H > ED_MAX_W || c->ed_lds_max_n < 0) c->ed_lds_max_n = 0;
+    }
+    // the row bins exist only where binning can run: 2 bins per fill row of ed_lds_max_n boxes each
+    if (c->ed_lds_max_n > 0) ALLOC(c->edBins, sizeof(uint4) * 2 * (size_t)ed_nrows(c->H) * (size_t)c->ed_lds_max_n);
     ALLOC(c->edBinCnt, sizeof(int) * 2 * (size_t)ed_nrows(c->H));
     ALLOC(c->edDone, 64);
     ALLOC(c->depth_in, sizeof(uint16_t) * npx);
@@ -372,14 +381,6 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         const char* env = getenv("TFUSION_INTEG_WG_FRAME");
         c->integ_wg_frame = env ? atoi(env) : TF_INTEG_WG_FRAME;
         if (c->integ_wg_frame < 64 || c->integ_wg_frame > TF_INTEG_WG) c->integ_wg_frame = TF_INTEG_WG;
-    }
-    {   // k_ed_fill: LDS rows up to ED_LDS_MAX_N visible entries, device-scope atomics past that
-        // (TFUSION_ED_LDS_MAX_N overrides the threshold; the parity tests run both paths)
-        const char* env = getenv("TFUSION_ED_LDS_MAX_N");
-        c->ed_lds_max_n = env ? atoi(env) : ED_LDS_MAX_N;
-        if (c->ed_lds_max_n > ED_LDS_MAX_N) c->ed_lds_max_n = ED_LDS_MAX_N;
-        // the binned boxes hold 12-bit coordinates (tf_ed.h ed_bin_pack)
-        if (c->W > ED_MAX_W || c->H > ED_MAX_W) c->ed_lds_max_n = 0;
     }
     e = tfk_reset_scene(c);                              // topfu.cpp:75
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1212,6 +1213,35 @@ extern "C" tf_status tf_scene_swap(tf_ctx* c) { TF_FLUSH(c); return scene_swap(c
 extern "C" tf_status tf_scene_swap_in(tf_ctx* c) { TF_FLUSH(c); return scene_swap(c, 1); }
 extern "C" tf_status tf_scene_swap_out(tf_ctx* c) { TF_FLUSH(c); return scene_swap(c, 2); }
 
+hipError_t tfk_fuse_frames(tf_ctx* c, const uint16_t* frames, size_t stride, size_t pitch, int n);   // tf_fuse.hip
+
+extern "C" tf_status tf_scene_fuse_frames(tf_ctx* c, const float intr[4], const uint16_t* dev_frames, size_t stride,
+                                         size_t pitch, const float* poses_rt, int n, tf_fuse_record* records)
+{
+    TF_FLUSH(c);
+    if (!c || !dev_frames || !poses_rt || n < 0) return TF_INVALID_ARG;
+    if (pitch == 0) pitch = (size_t)c->W * 2;
+    if (pitch < (size_t)c->W * 2 || (n > 1 && stride < pitch * (size_t)c->H)) return TF_INVALID_ARG;
+    if (n == 0) return TF_OK;
+    if (n > c->fuse_cap) {              // the pose / record lists grow to the largest batch seen
+        TF_CHECK(hipStreamSynchronize(c->stream));
+        if (c->fuse_pose) TF_CHECK(hipFree(c->fuse_pose));
+        if (c->fuse_rec) TF_CHECK(hipFree(c->fuse_rec));
+        c->fuse_pose = nullptr; c->fuse_rec = nullptr; c->fuse_cap = 0;
+        TF_CHECK(dalloc(&c->fuse_pose, sizeof(float) * 12 * (size_t)n));
+        TF_CHECK(dalloc(&c->fuse_rec, sizeof(tf_fuse_record) * (size_t)n));
+        c->fuse_cap = n;
+    }
+    TF_CHECK(order_after_caller(c));
+    TF_CHECK(hipMemcpyAsync(c->fuse_pose, poses_rt, sizeof(float) * 12 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    IntrScope is(c, intr);
+    TF_CHECK(tfk_fuse_frames(c, dev_frames, stride, pitch, n));
+    if (records)
+        TF_CHECK(hipMemcpyAsync(records, c->fuse_rec, sizeof(tf_fuse_record) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return TF_OK;
+}
+
 extern "C" tf_status tf_swap_counts(tf_ctx* c, int counts[3])
 {
     TF_FLUSH(c);
@@ -1339,6 +1369,8 @@ static void* buffer_ptr(tf_ctx* c, int which, int level, size_t* bytes)
     case TF_BUF_SWAP_STORED_FLAGS: *bytes = c->swapFlags ? (size_t)c->n_total : 0; return c->swapFlags;
     case TF_BUF_SWAP_STORED: *bytes = c->swapStore ? sizeof(TfVoxel) * (size_t)c->n_total * TF_BLK3 : 0; return c->swapStore;
     case TF_BUF_VBA_RGB: *bytes = c->vba_rgb ? sizeof(unsigned) * (size_t)c->p.n_blocks * TF_BLK3 : 0; return c->vba_rgb;
+    case TF_BUF_ALLOC_LIST: *bytes = sizeof(int) * (size_t)c->p.n_blocks; return c->allocList;
+    case TF_BUF_EXCESS_LIST: *bytes = sizeof(int) * (size_t)c->p.n_excess; return c->excessList;
     }
     *bytes = 0;
     return nullptr;
@@ -1386,7 +1418,8 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
     if (which == TF_BUF_HASH) TF_CHECK(tfk_grid_rebuild(c));       // keep the block grid exact
     if (which == TF_BUF_RANGE) TF_CHECK(ed_spill_all(c));          // next CreateExpectedDepths: whole buffer
     static const int one = 1;
-    if (which == TF_BUF_HASH || which == TF_BUF_VBA || which == TF_BUF_VBA_RGB)   // next reset (in-frame ones too): full clear
+    if (which == TF_BUF_HASH || which == TF_BUF_VBA || which == TF_BUF_VBA_RGB || which == TF_BUF_ALLOC_LIST ||
+        which == TF_BUF_EXCESS_LIST)                               // next reset (in-frame ones too): full clear
         TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, scene_external), &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
     return TF_OK;
@@ -1427,6 +1460,7 @@ extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)
     t->visible_sum = d->tot_visible; t->tiles_sum = d->tot_tiles;
     t->swapped_in = d->tot_swap_in; t->swapped_out = d->tot_swap_out;
     t->swapped_in_merged = d->tot_swap_merged;
+    t->alloc_failed_type1 = d->tot_alloc_fail1; t->alloc_failed_type2 = d->tot_alloc_fail2;
     t->integrate_lanes_read = t->integrate_lanes_written = 0;
     std::vector<long long> h(2 * TF_INTEG_WG);
     TF_CHECK(hipMemcpyAsync(h.data(), c->integ_cnt, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, c->stream));
@@ -1439,7 +1473,7 @@ extern "C" tf_status tf_reset_totals(tf_ctx* c)
 {
     TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
-    const size_t b = offsetof(TfDevState, tot_frames), e = offsetof(TfDevState, tot_swap_merged) + sizeof(long long);
+    const size_t b = offsetof(TfDevState, tot_frames), e = offsetof(TfDevState, tot_alloc_fail2) + sizeof(long long);
     TF_CHECK(hipMemsetAsync((char*)c->st + b, 0, e - b, c->stream));
     TF_CHECK(hipMemsetAsync(c->integ_cnt, 0, sizeof(long long) * 2 * TF_INTEG_WG, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));

@@ -11,7 +11,7 @@ struct EdArgs {
     uint4* rec;          // per visible entry: ulx | uly << 16, lrx | lry << 16, zmin, zmax bits (x ~0u: none)
     int* tiles; int* off; int* chunk;
     int2* spill;         // per fill row: extent of the pixels the last fill wrote outside the /8 region
-    uint4* bins;         // [2 * nrows][ED_LDS_MAX_N] binned boxes (ed_bin_pack): row r's, then row r's
+    uint4* bins;         // [2 * nrows][lds_max_n] binned boxes (ed_bin_pack): row r's, then row r's
                          // share of the boxes reaching below the LDS rows (entry index % nrows == r)
     int* bin_cnt;        // [2 * nrows] entries in each bin (the fill's workgroup r zeroes its two)
     int keep_bins;       // the fill leaves the counts (tf_time_stage's repeated fills)
@@ -26,7 +26,7 @@ struct EdArgs {
 };
 
 #define ED_CHUNK 256     // visible entries per projection chunk (one workgroup pass)
-#define ED_MAX_ROWS 520  // k_ed_fill LDS rows for H <= 4096 (ed_nrows); binning needs W, H <= 4096
+#define ED_MAX_ROWS 520  // k_ed_fill LDS rows for H <= 4096 (ed_nrows); binning needs W, H <= 4096 (tf_create)
 
 // a binned box: its /8 pixel box (12 bits per coordinate), the visible-list index (16 bits, the
 // MAX_RENDERING_BLOCKS check) and the z range -- everything the fill reads in one 16-byte load
@@ -92,7 +92,7 @@ __device__ __forceinline__ void ed_project_block(const EdArgs& a, const TfDevSta
     // device atomic per bin and chunk); the order inside a bin is arbitrary -- the fill reduces
     // with min / max only, so its result does not depend on it.
     __shared__ int lcnt[2 * ED_MAX_ROWS], gbase[2 * ED_MAX_ROWS];
-    const bool binning = n <= a.lds_max_n;
+    const bool binning = a.lds_max_n > 0 && n <= a.lds_max_n;   // (no bins when lds_max_n is 0)
     const int nb2 = 2 * a.nrows;
     if (binning)
         for (int r = threadIdx.x; r < nb2; r += 256) lcnt[r] = 0;
@@ -162,8 +162,8 @@ __device__ __forceinline__ void ed_project_block(const EdArgs& a, const TfDevSta
             if (valid) {
                 const uint4 e = ed_bin_pack(rec.x & 0xffffu, (unsigned)uly, rec.y & 0xffffu, (unsigned)lry, (unsigned)i,
                                             rec.z, rec.w);
-                for (int r = uly; r <= r1; ++r) a.bins[(size_t)r * ED_LDS_MAX_N + gbase[r] + atomicAdd(&lcnt[r], 1)] = e;
-                if (below) a.bins[(size_t)bb * ED_LDS_MAX_N + gbase[bb] + atomicAdd(&lcnt[bb], 1)] = e;
+                for (int r = uly; r <= r1; ++r) a.bins[(size_t)r * a.lds_max_n + gbase[r] + atomicAdd(&lcnt[r], 1)] = e;
+                if (below) a.bins[(size_t)bb * a.lds_max_n + gbase[bb] + atomicAdd(&lcnt[bb], 1)] = e;
             }
             __syncthreads();
             for (int r = threadIdx.x; r < nb2; r += 256) lcnt[r] = 0;

@@ -54,9 +54,10 @@ struct TfDevState {
     int lastFreeExcessListId;
     int noVisibleEntries;
     int noTotalBlocks;
-    int alloc_exhausted;     // capacity exhausted this frame -> serial allocation
-    unsigned pad_tiles_;
-    int pad_[2];             // alloc totals (tf_scene.hip)
+    int alloc_fail[2];       // this AllocateSceneFromDepth's failed requests: type 1 (no free block), type 2
+                             // (no free block or excess slot) -- allocateVoxelBlocksList's silent failures
+                             // (SceneReconstructionEngine_host.cu:374-381, 398-401); zeroed by k_alloc_requests
+    int pad_[2];             // alloc totals: requests of both types, of type 2 (k_alloc_apply -> k_vis_count)
     unsigned icp_gen;        // last generation tag used by the persistent ICP kernel
     // device-driven frame control (TopFu::operator() branches decided on the device, so a
     // batch of frames is enqueued without host round trips)
@@ -65,7 +66,7 @@ struct TfDevState {
     int n_resets;            // resets taken after ICP failures
     unsigned reset_ticket;   // k_reset_scene: workgroups done (the last one resets the counters)
     int pad4_;
-    unsigned alloc_ticket;   // k_alloc_apply under exhaustion: workgroups done (the last one allocates)
+    unsigned pad5_;
     int scene_external;      // scene buffers / counters set from the host since the last full reset:
                              // the next reset (in-frame ones too) clears everything, then drops it
     int pad2_;
@@ -78,9 +79,12 @@ struct TfDevState {
     // swapping (tf_swap.hip): the last frame's counts, and the free-list top handed from the
     // swap-in launch to the swap-out launch
     int swap_in, swap_out, swap_realloc, swap_free0;
+    int swap_merged;         // the last IntegrateGlobalIntoLocal's merges of stored data (k_swap_count_in zeroes it)
+    int pad6_[3];
     // totals since creation / tf_reset_totals, accumulated by the frame end (tf_totals)
     long long tot_frames, tot_tracked, tot_resets, tot_visible, tot_tiles, tot_swap_in, tot_swap_out,
-        tot_swap_merged;         // swap-ins whose entry held stored data (a real GlobalCache -> VBA transfer)
+        tot_swap_merged,         // swap-ins whose entry held stored data (a real GlobalCache -> VBA transfer)
+        tot_alloc_fail1, tot_alloc_fail2;   // failed allocation requests (alloc_fail), accumulated by k_vis_count
 };
 
 // ---------------------------------------------------------------------------------------
@@ -283,7 +287,6 @@ struct tf_ctx {
     unsigned char* allocType;
     int* winnerKey;          // per-entry last-writer key (pixel*64+step), replaces blockCoords races
     int* allocCounts;        // per-chunk counts (2 ints per chunk)
-    int* requestList;        // ordered request indices
     int* visCounts;
     // RenderState_VH
     int* visibleIds;
@@ -368,6 +371,10 @@ struct tf_ctx {
     int tail_pending;
     int tail_fuse_ed;
     int percall_defer;                   // TFUSION_PERCALL_DEFER (default 1)
+    // engine-level batches (tf_scene_fuse_frames, tf_fuse.hip): the batch's poses and per-frame records
+    float* fuse_pose;                    // [fuse_cap][12] world -> camera, row-major [R|t]
+    int* fuse_rec;                       // [fuse_cap] tf_fuse_record
+    int fuse_cap;
 };
 #define TF_VERDICT_WORDS 16
 

@@ -1110,7 +1110,7 @@ __device__ __forceinline__ void ed_fill_block(const EdArgs& a, TfDevState* __res
     // (bin nrow + row); the projection pass binned them (ed_project_block)
     for (int part = 0; part < 2; ++part) {
         const int m = part ? cnt_below : cnt_row;
-        const uint4* bin = a.bins + (size_t)(part ? nrow + row : row) * ED_LDS_MAX_N;
+        const uint4* bin = a.bins + (size_t)(part ? nrow + row : row) * a.lds_max_n;
         for (int k0 = threadIdx.x; k0 < m; k0 += ED_INFLIGHT * ED_THREADS) {
             uint4 e[ED_INFLIGHT];
 #pragma unroll
@@ -1264,7 +1264,7 @@ __device__ __forceinline__ void ed_tile_range(const EdArgs& a, int X0, int Y0, i
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
         const int m = part ? c1 : c0;
-        const uint4* bin = a.bins + (size_t)(Y0 + part) * ED_LDS_MAX_N;
+        const uint4* bin = a.bins + (size_t)(Y0 + part) * a.lds_max_n;
         for (int k0 = threadIdx.x; k0 < m; k0 += 4 * 256) {
             uint4 e[4];
 #pragma unroll

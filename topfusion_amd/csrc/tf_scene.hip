@@ -7,8 +7,8 @@
 //   * allocation requests: per-entry atomicMax of key = pixel*64 + step (raster order,
 //     last writer wins); the winning block position is recomputed from the key;
 //   * block / excess slots: ordered by hash index through a chunked scan whose per-chunk
-//     counts the request pass accumulates (exact serial semantics, including capacity
-//     exhaustion, via a one-thread fallback in the last workgroup);
+//     counts the request pass accumulates; capacity exhaustion (the silent failures) is
+//     decided per request from the same prefix counts (k_alloc_apply), exactly the serial loop;
 //   * visible list: ordered compaction by hash index.
 #include "tf_internal.h"
 #include "tf_preproc.h"
@@ -280,7 +280,7 @@ __device__ __forceinline__ void alloc_probe(const AllocArgs& a, const TfHashEntr
 }
 
 __global__ void __launch_bounds__(256)
-k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+k_alloc_requests(AllocArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
                  unsigned char* __restrict__ allocType, unsigned char* __restrict__ visType, int* __restrict__ winnerKey,
                  int* __restrict__ counts, int gx, int n_alloc, BilArgs next, int next_gx)
 {
@@ -294,6 +294,7 @@ k_alloc_requests(AllocArgs a, const TfDevState* __restrict__ st, const TfHashEnt
         return;
     }
     if (st->abort) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { st->alloc_fail[0] = 0; st->alloc_fail[1] = 0; }   // (k_alloc_apply counts)
     __shared__ AllocLds lt;
     lt.idx[threadIdx.x] = -1;
     lt.key[threadIdx.x] = -1;
@@ -426,59 +427,23 @@ __device__ __forceinline__ int4 block_sum4(int4 v)
 // ---------------------------------------------------------------------------------------
 // allocateVoxelBlocksList_device (SceneReconstructionEngine_host.cu:350-415), ordered
 // ---------------------------------------------------------------------------------------
-// capacity exhaustion: the exact serial semantics of allocateVoxelBlocksList in index order
-// (SceneReconstructionEngine_host.cu:350-415), one thread
-__device__ void alloc_serial(const AllocArgs& a, TfDevState* __restrict__ st, unsigned char* __restrict__ allocType,
-                             int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
-                             unsigned char* __restrict__ visType, const int* __restrict__ allocList,
-                             const int* __restrict__ excessList, const int* __restrict__ requestList, int total12)
-{
-    int v = st->lastFreeBlockId, e = st->lastFreeExcessListId;
-    for (int r = 0; r < total12; ++r) {
-        int idx = requestList[r];
-        int t = allocType[idx];
-        if (t == 1) {
-            int vbaIdx = v--;
-            if (vbaIdx >= 0) {
-                short pos[3];
-                alloc_block_from_key(a, st->invM_alloc, winnerKey[idx], pos);
-                TfHashEntry he; he.x = pos[0]; he.y = pos[1]; he.z = pos[2]; he.pad = 0; he.offset = 0;
-                he.ptr = allocList[vbaIdx];
-                hash[idx] = he;
-                grid_set(a.grid, he, idx);
-            } else {
-                visType[idx] = 0;
-                v++;
-            }
-        } else if (t == 2) {
-            int vbaIdx = v--, exlIdx = e--;
-            if (vbaIdx >= 0 && exlIdx >= 0) {
-                short pos[3];
-                alloc_block_from_key(a, st->invM_alloc, winnerKey[idx], pos);
-                TfHashEntry he; he.x = pos[0]; he.y = pos[1]; he.z = pos[2]; he.pad = 0; he.offset = 0;
-                he.ptr = allocList[vbaIdx];
-                int exlOffset = excessList[exlIdx];
-                hash[idx].offset = exlOffset + 1;
-                hash[a.n_buckets + exlOffset] = he;
-                grid_set(a.grid, he, a.n_buckets + exlOffset);
-                visType[a.n_buckets + exlOffset] = 1;
-            } else {
-                v++; e++;
-            }
-        }
-        allocType[idx] = 0;
-        winnerKey[idx] = -1;
-    }
-    st->lastFreeBlockId = v;
-    st->lastFreeExcessListId = e;
-}
-
-
+// The serial loop over the requests in index order keeps two counters: v (lastFreeBlockId) and
+// e (lastFreeExcessListId).  A type-1 request takes v-- and fails (restoring v, visType = 0)
+// when v < 0; a type-2 request takes v-- and e-- and fails (restoring both) when either is < 0
+// (:358-413).  Both counters only ever go down, so the outcome of request k is a function of
+// prefix counts, with v0 / e0 the counters at the start:
+//   q(k)  = type-2 requests before k;   n1(k) = type-1 requests before k
+//   S(k)  = n1(k) + min(q(k), e0 + 1)   -- the successes before k while blocks last
+//   type 1 succeeds iff S(k) <= v0;  type 2 iff S(k) <= v0 and q(k) <= e0
+// (the type-2 successes are the first e0 + 1 type-2 requests until the blocks run out; once
+// S(k) > v0 nothing succeeds any more).  A success takes allocList[v0 - S(k)] and, for type 2,
+// excessList[e0 - q(k)].  Without exhaustion S(k) is k's rank among all requests.  So every
+// request is decided in parallel from the chunk prefix sums, with the serial loop's results.
 __global__ void __launch_bounds__(256)
 k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int* __restrict__ counts,
               unsigned char* __restrict__ allocType, int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
               unsigned char* __restrict__ visType, const int* __restrict__ allocList,
-              const int* __restrict__ excessList, int* __restrict__ requestList, int n_total)
+              const int* __restrict__ excessList, int n_total)
 {
     if (st->abort) return;
     // this chunk's request types, loaded before (and in flight with) the counts prefix
@@ -497,48 +462,46 @@ k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int*
         p12 = t.x; p2 = t.y; a12 = t.z; a2 = t.w;
     }
     const int v0 = st->lastFreeBlockId, e0 = st->lastFreeExcessListId;
-    const bool exhausted = (a12 > v0 + 1) || (a2 > e0 + 1);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->alloc_exhausted = exhausted ? 1 : 0;
-        st->pad_[0] = a12; st->pad_[1] = a2;
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) { st->pad_[0] = a12; st->pad_[1] = a2; }
     int l12 = 0, l2 = 0;
     if (base < n_total)
         for (int i = 0; i < 16; ++i) { unsigned t = byte16(lo, hi, i); l12 += t != 0; l2 += t == 2; }
     int wg12, tmp;
     const int o12 = block_excl_scan(l12, &wg12);          // this thread's first request in the workgroup
     const int r2_0 = p2 + block_excl_scan(l2, &tmp);
-    if (exhausted) {
-        int r12 = p12 + o12;
-        for (int i = 0; i < 16 && l12; ++i)
-            if (byte16(lo, hi, i)) requestList[r12++] = base + i;
-    } else if (wg12) {
-        // The workgroup's requests one per thread, in index order (request k takes free-list slot
-        // v0 - (p12 + k), its excess slot e0 - r2): the winner key, the free block and the excess
-        // slot are loaded together, then the key's depth sample; a thread holding several
-        // requests would chain those round trips.
-        __shared__ int rq_idx[256], rq_r2[256];
-        const float* invM = st->invM_alloc;
-        for (int k0 = 0; k0 < wg12; k0 += 256) {
-            int k = o12, q2 = r2_0;
-            for (int i = 0; i < 16 && l12; ++i) {
-                const unsigned t = byte16(lo, hi, i);
-                if (!t) continue;
-                if (k >= k0 && k < k0 + 256) { rq_idx[k - k0] = base + i; rq_r2[k - k0] = t == 2 ? q2 : -1; }
-                ++k;
-                if (t == 2) ++q2;
-            }
-            __syncthreads();
-            if (k0 + (int)threadIdx.x < wg12) {
-                const int idx = rq_idx[threadIdx.x], q = rq_r2[threadIdx.x];
+    if (!wg12) return;
+    // The workgroup's requests one per thread, in index order: the winner key, the free block and
+    // the excess slot are loaded together, then the key's depth sample; a thread holding several
+    // requests would chain those round trips.  rq_q: q(k) for a type-2 request, ~q(k) for type 1.
+    __shared__ int rq_idx[256], rq_q[256];
+    const float* invM = st->invM_alloc;
+    for (int k0 = 0; k0 < wg12; k0 += 256) {
+        int k = o12, q2 = r2_0;
+        for (int i = 0; i < 16 && l12; ++i) {
+            const unsigned t = byte16(lo, hi, i);
+            if (!t) continue;
+            if (k >= k0 && k < k0 + 256) { rq_idx[k - k0] = base + i; rq_q[k - k0] = t == 2 ? q2 : ~q2; }
+            ++k;
+            if (t == 2) ++q2;
+        }
+        __syncthreads();
+        bool fail1 = false, fail2 = false;
+        if (k0 + (int)threadIdx.x < wg12) {
+            const int idx = rq_idx[threadIdx.x], qq = rq_q[threadIdx.x];
+            const bool is2 = qq >= 0;
+            const int q = is2 ? qq : ~qq;
+            const int g = p12 + k0 + (int)threadIdx.x;          // rank among all requests
+            const int S = (g - q) + (q < e0 + 1 ? q : e0 + 1);    // successes before this request
+            const bool ok = S <= v0 && (!is2 || q <= e0);
+            if (ok) {
                 const int key = winnerKey[idx];
-                const int ptr = allocList[v0 - (p12 + k0 + (int)threadIdx.x)];
-                const int exlOffset = q >= 0 ? excessList[e0 - q] : 0;
+                const int ptr = allocList[v0 - S];
+                const int exlOffset = is2 ? excessList[e0 - q] : 0;
                 short pos[3];
                 alloc_block_from_key(a, invM, key, pos);
                 TfHashEntry e; e.x = pos[0]; e.y = pos[1]; e.z = pos[2]; e.pad = 0; e.offset = 0;
                 e.ptr = ptr;
-                if (q < 0) {
+                if (!is2) {
                     hash[idx] = e;
                     grid_set(a.grid, e, idx);
                 } else {
@@ -547,30 +510,24 @@ k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int*
                     grid_set(a.grid, e, a.n_buckets + exlOffset);
                     visType[a.n_buckets + exlOffset] = 1;
                 }
-                allocType[idx] = 0;
-                winnerKey[idx] = -1;
+            } else if (!is2) {
+                visType[idx] = 0;                               // :377
+                fail1 = true;
+            } else {
+                fail2 = true;
             }
-            __syncthreads();
+            allocType[idx] = 0;
+            winnerKey[idx] = -1;
         }
+        // failed requests of the frame, one atomic per wave that has any (the counters drop by
+        // the successes only: k_vis_count)
+        const unsigned long long b1 = __ballot(fail1), b2 = __ballot(fail2);
+        if ((threadIdx.x & 63) == 0 && (b1 | b2)) {
+            if (b1) atomicAdd(&st->alloc_fail[0], __popcll(b1));
+            if (b2) atomicAdd(&st->alloc_fail[1], __popcll(b2));
+        }
+        __syncthreads();
     }
-    // Without exhaustion the counters drop by the totals (k_vis_count, next launch: every
-    // workgroup here has read them).  With it, the workgroup that finishes last takes the
-    // requests in index order, serially; requestList is handed over with the agent-scope
-    // release -> ticket -> acquire of MI355X_MICROARCH.md "Valid forms".
-    if (!exhausted) return;
-    __shared__ int last_s;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last_s = __hip_atomic_fetch_add(&st->alloc_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last_s || threadIdx.x != 0) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    st->alloc_ticket = 0;
-    alloc_serial(a, st, allocType, winnerKey, hash, visType, allocList, excessList, requestList, a12);
 }
 
 
@@ -583,7 +540,7 @@ k_alloc_discard(TfDevState* __restrict__ st, const int* __restrict__ counts, uns
                 int* __restrict__ winnerKey, int n_total)
 {
     if (st->abort) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) { st->alloc_exhausted = 0; st->pad_[0] = 0; st->pad_[1] = 0; }
+    if (blockIdx.x == 0 && threadIdx.x == 0) { st->pad_[0] = 0; st->pad_[1] = 0; }
     if (counts[2 * blockIdx.x] == 0) return;             // no request in this chunk
     for (int i = blockIdx.x * CHUNK + threadIdx.x; i < (int)(blockIdx.x + 1) * CHUNK && i < n_total; i += 256) {
         if (allocType[i]) { allocType[i] = 0; winnerKey[i] = -1; }
@@ -605,9 +562,13 @@ k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restric
         // frame's requests, and (without exhaustion) the free-list counters drop by the totals
         allocCounts[2 * blockIdx.x] = 0;
         allocCounts[2 * blockIdx.x + 1] = 0;
-        if (blockIdx.x == 0 && !st->alloc_exhausted) {
-            st->lastFreeBlockId -= st->pad_[0];
-            st->lastFreeExcessListId -= st->pad_[1];
+        if (blockIdx.x == 0) {
+            // the counters drop by the successful requests (failed ones restored them, :378, :400-401)
+            const int f1 = st->alloc_fail[0], f2 = st->alloc_fail[1];
+            st->lastFreeBlockId -= st->pad_[0] - f1 - f2;
+            st->lastFreeExcessListId -= st->pad_[1] - f2;
+            st->tot_alloc_fail1 += f1;
+            st->tot_alloc_fail2 += f2;
         }
     }
     const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
@@ -724,7 +685,7 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch, int onl
     else
         hipLaunchKernelGGL(k_alloc_apply, dim3(c->alloc_chunks), dim3(256), 0, c->stream, a, c->st, c->alloc_chunks,
                            c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
-                           c->requestList, c->n_total);
+                           c->n_total);
     hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
                        c->visCounts, c->allocCounts, swapping ? c->swapState : nullptr);
     hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,

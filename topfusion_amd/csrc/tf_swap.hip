@@ -155,7 +155,7 @@ k_swap_realloc(TfDevState* __restrict__ st, TfHashEntry* __restrict__ hash, cons
 
 // swap-in candidates of a chunk: state 1 with a block
 __global__ void __launch_bounds__(256)
-k_swap_count_in(const TfDevState* __restrict__ st, const unsigned char* __restrict__ swapState,
+k_swap_count_in(TfDevState* __restrict__ st, const unsigned char* __restrict__ swapState,
                 const TfHashEntry* __restrict__ hash, int* __restrict__ counts, int n_total)
 {
     if (st->abort) return;
@@ -170,6 +170,7 @@ k_swap_count_in(const TfDevState* __restrict__ st, const unsigned char* __restri
     int tot;
     sw_excl_scan(c, &tot);
     if (threadIdx.x == 0) counts[2 * blockIdx.x] = tot;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->swap_merged = 0;   // (k_swap_in counts this pass's merges)
 }
 
 // CombineVoxelInformation (depth part): src = stored, dst = active; canonical arithmetic
@@ -240,7 +241,10 @@ k_swap_in(TfDevState* __restrict__ st, unsigned char* __restrict__ swapState, co
         }
         if (threadIdx.x == 0) swapState[id] = 2;
     }
-    if (threadIdx.x == 0 && merged) atomicAdd((unsigned long long*)&st->tot_swap_merged, (unsigned long long)merged);
+    if (threadIdx.x == 0 && merged) {
+        atomicAdd((unsigned long long*)&st->tot_swap_merged, (unsigned long long)merged);
+        atomicAdd(&st->swap_merged, merged);
+    }
     __syncthreads();
     // swap-out candidates of the chunk: state 2 (after the swap-ins above), a block, not visible
     int c = 0;

@@ -14,6 +14,8 @@ apps/demo.cpp:93-97), so every workload is rendered analytically:
 
 Depth is uint16 millimetres (the reference's cuda::Depth, types.hpp:62).
 """
+import os
+
 import numpy as np
 
 # TopFuParams::default_params intrinsics, topfu.cpp:24
@@ -293,3 +295,273 @@ def build_hash(pos, n_buckets, n_excess, dtype):
     entry = np.empty(n, np.int64)
     entry[blk] = entry_sorted
     return h, entry.astype(np.int32), n_excess - 1 - n_ex
+
+
+# ----------------------------------------------------------------------------------------
+# C5E: the hash stress proper -- an unbounded procedurally tiled hall (capacity
+# saturation, silent allocation failure, eviction churn).  The C5 walk above is confined to one
+# room, whose whole surface fits in a few thousand 10 mm blocks; this scene keeps new surface
+# entering the view however far the camera goes.
+#
+#   floor y = HALL_FLOOR, ceiling y = HALL_CEIL (world y points down, as the camera's);
+#   a lattice of HALL_PERIOD-metre cells in x / z, each holding (by an integer hash of the cell)
+#   a box standing on the floor, a box hanging from the ceiling, or nothing.  Floor boxes end at
+#   y >= 0.2, ceiling boxes at y <= -0.35 and the camera stays in y in [-0.15, 0.1], so the camera
+#   is never inside a box.
+#
+# Everything here is integer hashing and IEEE +, -, *, / in float64 (no transcendental function
+# of the pixel), so synth/tf_synth.hip renders the same uint16 millimetres bit for bit; noise is
+# the sum of four hashed uniforms (Irwin-Hall, std noise_mm).
+# ----------------------------------------------------------------------------------------
+HALL_FLOOR, HALL_CEIL, HALL_PERIOD, HALL_REACH = 0.55, -0.75, 0.8, 3
+HALL_CAM_Y = (-0.15, 0.10)
+_SQRT3 = 1.7320508075688772
+
+
+def _mix32(h):
+    """lowbias32 integer finaliser on uint32 (numpy arrays or scalars), wrapping arithmetic."""
+    h = np.asarray(h, np.uint32)
+    with np.errstate(over="ignore"):
+        h = h ^ (h >> np.uint32(16))
+        h = h * np.uint32(0x7FEB352D)
+        h = h ^ (h >> np.uint32(15))
+        h = h * np.uint32(0x846CA68B)
+        h = h ^ (h >> np.uint32(16))
+    return h
+
+
+def _u32(v):
+    return (np.asarray(v, np.int64) & 0xFFFFFFFF).astype(np.uint32)
+
+
+def _unit(h):
+    """uint32 -> float64 in [0, 1), exact."""
+    return np.asarray(h, np.uint32).astype(np.float64) * (1.0 / 4294967296.0)
+
+
+def hall_cell(i, j):
+    """The box of lattice cell (i, j): (kind, lo[3], hi[3]); kind 0 none, 1 floor box, 2 ceiling box."""
+    i = np.asarray(i, np.int64)
+    j = np.asarray(j, np.int64)
+    with np.errstate(over="ignore"):
+        h = _mix32(_u32(i) * np.uint32(0x9E3779B1) ^ _mix32(_u32(j) + np.uint32(0x632BE5AB)))
+        u = [_unit(h)]
+        for k in range(5):
+            h = _mix32(h + np.uint32(0x9E3779B9))
+            u.append(_unit(h))
+    kind = np.where(u[0] < 0.45, 1, np.where(u[0] < 0.8, 2, 0))
+    cx = (i.astype(np.float64) + 0.5) * HALL_PERIOD + (u[1] - 0.5) * 0.2
+    cz = (j.astype(np.float64) + 0.5) * HALL_PERIOD + (u[2] - 0.5) * 0.2
+    hx = 0.08 + 0.14 * u[3]
+    hz = 0.08 + 0.14 * u[4]
+    ylo = np.where(kind == 1, 0.2 + 0.2 * u[5], HALL_CEIL)
+    yhi = np.where(kind == 1, HALL_FLOOR, -0.35 - 0.2 * u[5])
+    lo = np.stack([cx - hx, ylo, cz - hz], -1)
+    hi = np.stack([cx + hx, yhi, cz + hz], -1)
+    return kind, lo, hi
+
+
+def _slab(o, d, lo, hi):
+    """Ray / axis-aligned box entry distance (inf if missed or behind); o (3,), d (..., 3)."""
+    tn = np.full(d.shape[:-1], -np.inf)
+    tf = np.full(d.shape[:-1], np.inf)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for a in range(3):
+            da = d[..., a]
+            t1 = (lo[a] - o[a]) / da
+            t2 = (hi[a] - o[a]) / da
+            inside = (o[a] >= lo[a]) & (o[a] <= hi[a])
+            par = da == 0
+            t1 = np.where(par, np.where(inside, -np.inf, np.inf), t1)
+            t2 = np.where(par, np.where(inside, np.inf, -np.inf), t2)
+            tn = np.maximum(tn, np.minimum(t1, t2))
+            tf = np.minimum(tf, np.maximum(t1, t2))
+    return np.where((tn <= tf) & (tn > 1e-6), tn, np.inf)
+
+
+def hall_noise(seed, frame, cols, rows):
+    """Irwin-Hall(4) noise of frame `frame`, unit variance, (rows, cols) float64."""
+    pix = np.arange(rows * cols, dtype=np.int64).reshape(rows, cols)
+    with np.errstate(over="ignore"):
+        base = _mix32(_mix32(_u32(seed) + np.uint32(0x2545F491)) ^ _u32(frame))
+        s = np.zeros((rows, cols))
+        for k in range(4):
+            s = s + _unit(_mix32(base ^ _mix32(_u32(pix * 4 + k) + np.uint32(0x68E31DA4))))
+    return (s - 2.0) * _SQRT3
+
+
+def render_hall(R, t, cols=640, rows=480, noise_mm=1.0, seed=13, frame=0, intr=None):
+    """uint16 depth (mm) of the hall from camera->world pose (R, t); 0 where nothing is hit.
+    The reference renderer of synth/tf_synth.hip (tfs_render_hall): same bits."""
+    fx, fy, cx, cy = intr if intr is not None else intrinsics(cols, rows)
+    R = np.asarray(R, np.float64)
+    o = np.asarray(t, np.float64)
+    u = np.arange(cols, dtype=np.float64)
+    v = np.arange(rows, dtype=np.float64)
+    uu, vv = np.meshgrid(u, v)
+    xc, yc = (uu - cx) / fx, (vv - cy) / fy
+    # d = R @ (xc, yc, 1), written out so the order of the operations is fixed
+    d = np.stack([(R[0, 0] * xc + R[0, 1] * yc) + R[0, 2], (R[1, 0] * xc + R[1, 1] * yc) + R[1, 2],
+                  (R[2, 0] * xc + R[2, 1] * yc) + R[2, 2]], -1)
+    best = np.full((rows, cols), np.inf)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for y0 in (HALL_FLOOR, HALL_CEIL):
+            tt = (y0 - o[1]) / d[..., 1]
+            best = np.minimum(best, np.where(tt > 1e-6, tt, np.inf))
+    ci, cj = int(np.floor(o[0] / HALL_PERIOD)), int(np.floor(o[2] / HALL_PERIOD))
+    for di in range(-HALL_REACH, HALL_REACH + 1):
+        for dj in range(-HALL_REACH, HALL_REACH + 1):
+            kind, lo, hi = hall_cell(ci + di, cj + dj)
+            if int(kind) == 0:
+                continue
+            best = np.minimum(best, _slab(o, d, lo, hi))
+    mm = best * 1000.0
+    if noise_mm > 0:
+        mm = mm + noise_mm * hall_noise(seed, frame, cols, rows)
+    mm = np.where(np.isfinite(mm), np.rint(mm), 0.0)
+    return np.clip(mm, 0, 65535).astype(np.uint16)
+
+
+def hall_walk_poses(n, seed=13, step_m=0.01, step_deg=0.5):
+    """Camera->world poses (R[n,3,3], t[n,3]) of the C5E walk through the hall: frame 0 at the
+    identity; per frame a translation of at most step_m (~0.75 step_m on average) along a heading
+    that turns by a bounded Ornstein-Uhlenbeck rate, the camera yawing with the heading and
+    pitching / rolling a few degrees, every relative rotation <= step_deg.  Unconfined in x / z,
+    y in HALL_CAM_Y (reflected).  float64."""
+    rng = np.random.default_rng(seed)
+    R = np.empty((n, 3, 3))
+    t = np.empty((n, 3))
+    pos = np.zeros(3)
+    yaw = pitch = roll = 0.0
+    w_yaw = w_pitch = w_roll = 0.0
+    vy = 0.0
+    d2r = np.pi / 180.0
+    lim_yaw, lim_pitch, lim_roll = 0.40 * step_deg * d2r, 0.20 * step_deg * d2r, 0.10 * step_deg * d2r
+    for k in range(n):
+        cy_, sy_ = np.cos(yaw), np.sin(yaw)
+        cp, sp = np.cos(pitch), np.sin(pitch)
+        cr, sr = np.cos(roll), np.sin(roll)
+        Ry = np.array([[cy_, 0, sy_], [0, 1, 0], [-sy_, 0, cy_]])
+        Rx = np.array([[1, 0, 0], [0, cp, -sp], [0, sp, cp]])
+        Rz = np.array([[cr, -sr, 0], [sr, cr, 0], [0, 0, 1]])
+        R[k], t[k] = Ry @ Rx @ Rz, pos
+        # turn rates: mean-reverting, bounded; pitch / roll pulled back to level
+        w_yaw = float(np.clip(0.995 * w_yaw + rng.normal(0, 0.08) * lim_yaw, -lim_yaw, lim_yaw))
+        w_pitch = float(np.clip(0.98 * w_pitch - 0.002 * pitch + rng.normal(0, 0.1) * lim_pitch, -lim_pitch, lim_pitch))
+        w_roll = float(np.clip(0.98 * w_roll - 0.002 * roll + rng.normal(0, 0.1) * lim_roll, -lim_roll, lim_roll))
+        yaw, pitch, roll = yaw + w_yaw, pitch + w_pitch, roll + w_roll
+        speed = step_m * (0.6 + 0.3 * rng.random())                  # <= 0.9 step_m horizontally
+        vy = float(np.clip(0.95 * vy + rng.normal(0, 0.05) * 0.2 * step_m, -0.2 * step_m, 0.2 * step_m))
+        pos = pos + np.array([speed * np.sin(yaw), vy, speed * np.cos(yaw)])
+        lo, hi = HALL_CAM_Y
+        if pos[1] < lo:
+            pos[1], vy = 2 * lo - pos[1], -vy
+        if pos[1] > hi:
+            pos[1], vy = 2 * hi - pos[1], -vy
+    return R, t
+
+
+def hall_sequence(n, cols=640, rows=480, seed=13, noise_mm=1.0, first=0):
+    """C5E frames first..first+n-1 on the host (numpy), uint16 (n, rows, cols)."""
+    R, t = hall_walk_poses(first + n, seed)
+    intr = intrinsics(cols, rows)
+    return np.stack([render_hall(R[k], t[k], cols, rows, noise_mm, seed, k, intr) for k in range(first, first + n)])
+
+
+def world_to_camera_rt(R, t):
+    """[R|t] camera->world -> row-major 3x4 world->camera (float32), what the engine entry points
+    (tf_scene_alloc, tf_scene_fuse_frames) take; float32 inverse of the float32 pose as
+    cv::Affine3f::inv computes it (tf_pose.h tf_rigid_inv)."""
+    R = np.asarray(R, np.float32)
+    t = np.asarray(t, np.float32)
+    out = np.zeros(R.shape[:-2] + (3, 4), np.float32)
+    Rt = np.swapaxes(R, -1, -2)
+    out[..., :3, :3] = Rt
+    # -(R^T t) summed in the order of tf_rigid_inv: (a0j*t0 + a1j*t1) + a2j*t2
+    for j in range(3):
+        out[..., j, 3] = -((R[..., 0, j] * t[..., 0] + R[..., 1, j] * t[..., 1]) + R[..., 2, j] * t[..., 2])
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+# GPU rendering of the synthetic streams (synth/libtfsynth.so, built by __graft_entry__.build()):
+# the frames go straight into HBM through the same HIP runtime libtfusion_hip.so links.
+# ----------------------------------------------------------------------------------------
+_SYNTH_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "synth", "libtfsynth.so")
+_synth = None
+
+
+def synth_lib():
+    """ctypes handle of synth/libtfsynth.so (raises if it was not built)."""
+    global _synth
+    if _synth is None:
+        import ctypes
+        if not os.path.exists(_SYNTH_SO):
+            raise RuntimeError(f"{_SYNTH_SO} not built: run `make -C synth` (or __graft_entry__.build())")
+        from topfusion_amd import _lib
+        _lib.load()                      # the product library first: one HIP runtime for both
+        L = ctypes.CDLL(_SYNTH_SO)
+        P, S, I, D = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double
+        L.tfs_render_hall.argtypes = [P, S, P, I, I, I, I, D, D, D, D, ctypes.c_uint, D]
+        L.tfs_malloc.argtypes = [ctypes.POINTER(P), S]
+        L.tfs_free.argtypes = [P]
+        L.tfs_download.argtypes = [P, P, S]
+        L.tfs_upload.argtypes = [P, P, S]
+        for f in ("tfs_render_hall", "tfs_malloc", "tfs_free", "tfs_download", "tfs_upload", "tfs_sync"):
+            getattr(L, f).restype = I
+        _synth = L
+    return _synth
+
+
+class DeviceStream:
+    """n uint16 depth frames (rows x cols) in one device allocation (libtfsynth's hipMalloc)."""
+
+    def __init__(self, n, cols, rows):
+        import ctypes
+        self.n, self.cols, self.rows = n, cols, rows
+        self.frame_bytes = cols * rows * 2
+        p = ctypes.c_void_p()
+        assert synth_lib().tfs_malloc(ctypes.byref(p), max(16, n * self.frame_bytes)) == 0, "tfs_malloc"
+        self.ptr = p.value
+
+    def frame_ptr(self, k):
+        return self.ptr + k * self.frame_bytes
+
+    def download(self, k0=0, n=1):
+        import ctypes
+        out = np.empty((n, self.rows, self.cols), np.uint16)
+        assert synth_lib().tfs_download(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(self.frame_ptr(k0)),
+                                        n * self.frame_bytes) == 0
+        return out
+
+    def upload(self, frames, k0=0):
+        import ctypes
+        a = np.ascontiguousarray(frames, np.uint16).reshape(-1, self.rows, self.cols)
+        assert synth_lib().tfs_upload(ctypes.c_void_p(self.frame_ptr(k0)), a.ctypes.data_as(ctypes.c_void_p), a.nbytes) == 0
+
+    def free(self):
+        import ctypes
+        if self.ptr:
+            synth_lib().tfs_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def render_hall_device(stream, R, t, first=0, seed=13, noise_mm=1.0, k0=0):
+    """Frames first..first+len(R)-1 of the hall (poses R, t camera->world) rendered on the GPU into
+    stream slots k0.. (synth/tf_synth.hip: render_hall's bits)."""
+    import ctypes
+    n = len(R)
+    P = np.zeros((n, 12), np.float64)
+    P[:, :9] = np.asarray(R, np.float64).reshape(n, 9)
+    P[:, 9:] = np.asarray(t, np.float64)
+    fx, fy, cx, cy = intrinsics(stream.cols, stream.rows)
+    rc = synth_lib().tfs_render_hall(ctypes.c_void_p(stream.frame_ptr(k0)), stream.frame_bytes,
+                                     P.ctypes.data_as(ctypes.c_void_p), n, first, stream.cols, stream.rows,
+                                     fx, fy, cx, cy, seed, noise_mm)
+    assert rc == 0, f"tfs_render_hall: {rc}"

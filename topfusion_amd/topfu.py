@@ -253,6 +253,28 @@ class TopFu:
         L.check(L.load().tf_set_counters(self._h, lastFreeBlockId, lastFreeExcessListId, noVisibleEntries),
                 "tf_set_counters")
 
+    def fuse_frames(self, dev_frames, poses_w2c, stride=None, pitch=0, intr=None):
+        """tf_scene_fuse_frames: computeDists + AllocateSceneFromDepth + IntegrateIntoScene (+ the
+        swapping engine) per frame of a device-resident uint16 batch (`dev_frames`: device address
+        of frame 0) at the world->camera poses `poses_w2c` (n x 3 x 4 or n x 12); returns the
+        per-frame records (numpy structured array, L.FUSE_RECORD_DTYPE)."""
+        P = np.ascontiguousarray(np.asarray(poses_w2c, np.float32).reshape(-1, 12))
+        n = len(P)
+        rec = np.zeros(n, L.FUSE_RECORD_DTYPE)
+        if stride is None:
+            stride = self.W * self.H * 2
+        ip = None if intr is None else _ptr(np.ascontiguousarray(intr, np.float32))
+        L.check(L.load().tf_scene_fuse_frames(self._h, ip, ctypes.c_void_p(int(dev_frames)), int(stride), int(pitch),
+                                              _ptr(P), n, _ptr(rec)), "tf_scene_fuse_frames")
+        return rec
+
+    def alloc_list(self):
+        """LocalVBA::allocationList (the free-block stack)."""
+        return self.download(L.TF_BUF_ALLOC_LIST).view(np.int32)
+
+    def excess_list(self):
+        return self.download(L.TF_BUF_EXCESS_LIST).view(np.int32)
+
     # swapping (GlobalCache in HBM)
     def swap(self):
         """The swapping engine once (IntegrateGlobalIntoLocal + SaveToGlobalMemory)."""
