@@ -43,7 +43,7 @@ CONFIGS = {
     "C2": dict(cols=640, rows=480, voxel=0.005, capacity={}, walk=False, steps=20),
     "C3": dict(cols=1280, rows=960, voxel=0.002, capacity=C3_CAPACITY, walk=False, steps=20),
     # C5 hash stress: 10 mm voxels, 50 k-frame random walk (seed 13 + rank, <= 1 cm / 0.5 deg per
-    # frame), reference capacities; frames rendered on the GPU (synth.render_depth_torch)
+    # frame), reference capacities; frames rendered on the GPU (synth.walk_device)
     "C5": dict(cols=640, rows=480, voxel=0.01, capacity={}, walk=True, steps=1563),
 }
 
@@ -152,25 +152,17 @@ def cpu_model():
     return name, os.cpu_count()
 
 
-def hbm_stream_copy(device, gib=1.0, reps=10):
-    """Measured device-to-device copy bandwidth (read + write bytes / time, HIP events) beside
-    the 8 TB/s spec peak the roofline fractions use."""
-    import torch
-    n = int(gib * (1 << 30)) // 4
-    x = torch.empty(n, dtype=torch.float32, device=device)
-    y = torch.empty_like(x)
-    y.copy_(x)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        y.copy_(x)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    del x, y
-    torch.cuda.empty_cache()
-    return 2.0 * n * 4 / (ms * 1e-3) / 1e9
+def hbm_stream_copy(gib=1.0, reps=10):
+    """Measured device-to-device copy bandwidth (read + write bytes / time, HIP events;
+    synth/libtfsynth.so) beside the 8 TB/s spec peak the roofline fractions use."""
+    from topfusion_amd import synth
+    return synth.synth_lib().tfs_copy_gbs(int(gib * (1 << 30)), reps)
+
+
+def device_sync():
+    """hipDeviceSynchronize through the runtime the product library uses."""
+    from topfusion_amd import synth
+    assert synth.synth_lib().tfs_sync() == 0, "hipDeviceSynchronize"
 
 
 def cpu_run(frames, params_kw, first, n, omp, start=None):
@@ -249,11 +241,9 @@ def c3_scene():
     the visible list, uploaded as a valid hash table (synth.build_hash) + visible list; dists of a
     wall at 1.5 m.  Returns (context, params, W, H, voxel size, block count, visible ids,
     lastFreeExcessListId)."""
-    import torch
     from topfusion_amd import TopFu, default_params, synth
     from topfusion_amd import _lib as L
     from topfusion_amd.topfu import HASH_DTYPE
-    torch.cuda.set_device(0)
     cfg = CONFIGS["C3"]
     W, H, vox = cfg["cols"], cfg["rows"], cfg["voxel"]
     fx, fy, cx, cy = synth.intrinsics(W, H)
@@ -372,63 +362,42 @@ def c3_raycast(args):
     tf.close()
 
 
-def orbit_frames(n, W, H, seed, device):
+def orbit_frames(n, W, H, seed):
     """C2/C3 input: n frames of the synthetic orbit (room + sphere, 0.25 deg per frame
     around a pivot 1.2 m ahead, swinging +-25 deg so the camera stays inside the room for any n;
-    1 mm noise), rendered on the GPU in batches straight into HBM (synth.render_depth_torch -- the
-    host renderer's geometry, torch's noise generator)."""
-    import torch
+    1 mm noise), rendered on the GPU straight into HBM (synth.orbit_device: synth/tf_synth.hip,
+    bit-identical to synth.render_room) through the HIP runtime the product library uses.
+    Returns a synth.DeviceStream."""
     from topfusion_amd import synth
-    R = np.empty((n, 3, 3))
-    t = np.empty((n, 3))
-    for k in range(n):
-        R[k], t[k] = synth.orbit_pose(k)
-        assert synth.orbit_in_room(R[k], t[k]), f"orbit frame {k}: camera outside the room"
-    dev = torch.empty((n, H, W), dtype=torch.int16, device=device)
-    gen = torch.Generator(device=device)
-    gen.manual_seed(seed)
-    for b0 in range(0, n, 128):
-        b1 = min(n, b0 + 128)
-        dev[b0:b1] = synth.render_depth_torch(R[b0:b1], t[b0:b1], W, H, noise_mm=1.0, generator=gen, device=device)
-    return dev
+    return synth.orbit_device(n, W, H, seed)
 
 
-def walk_frames(n, W, H, seed, device):
-    """C5 input: the seed-13 random walk (<= 1 cm / 0.5 deg per frame), rendered on the GPU."""
-    import torch
+def walk_frames(n, W, H, seed):
+    """C5 input: the seed-13 random walk in the room (<= 1 cm / 0.5 deg per frame), on the GPU."""
     from topfusion_amd import synth
-    R, t = synth.random_walk_poses(n, seed=seed)
-    dev = torch.empty((n, H, W), dtype=torch.int16, device=device)
-    gen = torch.Generator(device=device)
-    gen.manual_seed(seed)
-    for b0 in range(0, n, 128):
-        b1 = min(n, b0 + 128)
-        dev[b0:b1] = synth.render_depth_torch(R[b0:b1], t[b0:b1], W, H, noise_mm=1.0, generator=gen, device=device)
-    return dev
+    return synth.walk_device(n, W, H, seed)
 
 
 def per_call_rate(tf, base, frame_bytes, n):
     """TopFu::operator() semantics (demo.cpp:102-105): one tf_process_frame call per frame (each
     returns on its frame's ICP verdict; its last two launches go out with the next call), wall
     clock over n frames including the last frame's whole work."""
-    import torch
-    torch.cuda.synchronize()
+    device_sync()
     t0 = time.perf_counter()
     for k in range(n):
         tf(base + k * frame_bytes)
     tf.stats()                 # (the last frame's deferred launches, enqueued and waited for)
-    torch.cuda.synchronize()
+    device_sync()
     return n / (time.perf_counter() - t0)
 
 
 def batched_rate(tf, base, n, F):
     """The same frames through tf_process_frames in F-frame batches (wall clock)."""
-    import torch
-    torch.cuda.synchronize()
+    device_sync()
     t0 = time.perf_counter()
     for k0 in range(0, n, F):
         tf.process_frames(base + k0 * tf.W * tf.H * 2, min(F, n - k0))
-    torch.cuda.synchronize()
+    device_sync()
     return n / (time.perf_counter() - t0)
 
 
@@ -474,10 +443,8 @@ def c5e_bench(args):
     seed = 13 + rank
     n = (warm + steps) * F
     t0 = time.perf_counter()
-    R, t = synth.hall_walk_poses(n, seed)
+    stream, R, t = synth.hall_device(n, W, H, seed)
     w2c = synth.world_to_camera_rt(R, t)
-    stream = synth.DeviceStream(n, W, H)
-    synth.render_hall_device(stream, R, t, 0, seed, 1.0)
     t_render = time.perf_counter() - t0
     fx, fy, cx, cy = synth.intrinsics(W, H)
     pkw = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=vox)
@@ -567,14 +534,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
+    dist = None
     if world > 1:
+        # RCCL for the two per-rank numbers only: torch's HIP runtime (its wheel bundles its own
+        # libamdhip64) must initialise before the product's /opt/rocm one; frames, fusion and
+        # timing all run on the product's runtime
+        import torch
+        import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
     from topfusion_amd import TopFu, default_params, synth
+    from topfusion_amd import _lib as L
+    L.check(L.load().tf_set_device(local_rank), "tf_set_device")
 
     cfg = CONFIGS[args.config]
     if args.steps is None:
@@ -594,13 +565,13 @@ def main():
     n_frames = (args.warmup + args.steps) * F
     device = f"cuda:{local_rank}"
     seed = (13 if cfg["walk"] else 7) + rank
-    dev = (walk_frames if cfg["walk"] else orbit_frames)(n_frames, W, H, seed, device)
+    dev = (walk_frames if cfg["walk"] else orbit_frames)(n_frames, W, H, seed)
     frame_bytes = W * H * 2
-    base = dev.data_ptr()
+    base = dev.ptr
 
     tf = TopFu(default_params(**pkw), device=local_rank)
     single = [k for k in SINGLE_KERNEL_STAGES if k != "icp" or tf.icp_persistent()]
-    torch.cuda.synchronize()
+    device_sync()
     # warm-up (whole steps: full enqueue groups), every stage timed: picks the dominant
     # single-kernel stage
     dominant = "icp" if tf.icp_persistent() else "raycast_icp"
@@ -618,14 +589,14 @@ def main():
     # breakdown comes from a separate pass below)
     tf.profile(not args.no_profile, stages=[dominant], every=args.profile_every)
     tf.reset_totals()
-    torch.cuda.synchronize()
+    device_sync()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     oks = []
     for k in range(args.steps):
         oks.append(tf.process_frames(base + (args.warmup + k) * F * frame_bytes, F))
-    torch.cuda.synchronize()
+    device_sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -649,7 +620,7 @@ def main():
         lanes_bd = (tbt["integrate_lanes_read"] / n_int, tbt["integrate_lanes_written"] / n_int)
         nvis_bd = tbt["visible_sum"] / n_int
         tb.close()
-        torch.cuda.synchronize()
+        device_sync()
     # TopFu::operator() per call (one call per frame, returning on the frame's verdict) over the first
     # frames of the timed region, from a fresh context, and the batched rate of a fresh context on
     # the same frames beside it (the orbit's cost per frame varies along it: compare like with like)
@@ -718,14 +689,14 @@ def main():
                 roof_all["icp"]["limit"] = ("latency, not HBM: 19 dependent iterations, each rows -> two cross-CU "
                                             "hand-offs -> the serial 6x6 solve (DESIGN.md 5); the previous-frame "
                                             "gathers hit L2, so PMC traffic is a fraction of the algorithmic bytes")
-        stream_gbs = round(hbm_stream_copy(device), 1)
+        stream_gbs = round(hbm_stream_copy(), 1)
         cpu = None
         if not args.no_cpu_baseline:
             # all cores: the OpenMP build of the oracle; 1 thread: the serial build (reported
             # beside); BASELINE.md protocol: one warm-up frame, then the median of 5 repeats of a
             # bounded sample of the same stream
             first = args.warmup * F
-            frames = dev[:min(n_frames, first + 128)].cpu().numpy().view(np.uint16)
+            frames = dev.download(0, min(n_frames, first + 128))
             nt = omp_threads()
             cpu = cpu_baseline_protocol(frames, first, pkw, args.cpu_seconds, nt)
         out = {
@@ -794,6 +765,7 @@ def main():
         }
         print(json.dumps(out))
     tf.close()
+    dev.free()
     if world > 1:
         dist.destroy_process_group()
 

@@ -14,6 +14,16 @@
  * tfusion/include/tfusion/cuda/CUDADefines.hpp:26-33); here the caller decides.
  * ICP degeneracy is TF_ICP_FAIL and triggers the same reset as the reference
  * (tfusion/src/topfu.cpp:263-264).
+ *
+ * Device-side failures.  The frame's stages wait on each other inside grids with bounded spins.
+ * (1) The persistent ICP launch needs its 256 workgroups resident at once; if another process or
+ * kernel holds part of the device, the launch ends with a lost peer.  Nothing past the ICP has
+ * run then, and the frame is run again on the per-iteration ICP schedule (tf_totals::icp_fallbacks
+ * counts it): the caller sees the frame's normal result.  (2) A bounded spin past the ICP that
+ * times out leaves the frame half done: the context is in error from then on -- that frame's
+ * call, or the next call that synchronises with the device if the frame's call had already
+ * returned (per-call frames return on their ICP verdict), and every later call returns
+ * TF_HIP_ERROR until tf_reset.
  */
 #ifndef TFUSION_HIP_H
 #define TFUSION_HIP_H
@@ -127,7 +137,12 @@ tf_status tf_reset(tf_ctx* ctx);
  * (after its ICP), with its allocation, integration and raycasts still running on the context
  * stream -- the reference likewise returns with its last kernels in flight (topfu.cpp:307-329);
  * every later call that reads the state is ordered after them.  dev_depth has been consumed by
- * then.  stats (optional) waits for the whole frame; so do RGB frames and profiled contexts. */
+ * then.  stats (optional) waits for the whole frame; so do RGB frames and profiled contexts.
+ * Deferred tail: the frame's last two launches (CreateICPMaps' raycast + renderImage, and
+ * CreateICPMaps + the frame end) are not enqueued by this call but by the next tf_* call on the
+ * context (the next frame's call carries that frame's preprocessing in them).  A caller that
+ * synchronises the device or a stream itself must first call tf_get_stream(), which enqueues
+ * them; every other entry point does it before its own work. */
 tf_status tf_process_frame(tf_ctx* ctx, const uint16_t* dev_depth, size_t pitch_bytes,
                            float pose_out[12], tf_stats* stats);
 /* same, host depth (cuda::Depth::upload, device_array.hpp; demo.cpp:100) */
@@ -375,6 +390,8 @@ typedef struct tf_totals {
                                        (allocateVoxelBlocksList, SceneReconstructionEngine_host.cu:374-381) */
     long long alloc_failed_type2;   /* ... excess-list requests that failed for want of a block or an excess
                                        slot (:386-411) */
+    long long icp_fallbacks;        /* frames re-run on the per-iteration ICP schedule because the persistent
+                                       launch lost a peer (not all of its workgroups were co-resident) */
 } tf_totals;
 tf_status tf_get_totals(tf_ctx* ctx, tf_totals* totals);
 tf_status tf_reset_totals(tf_ctx* ctx);

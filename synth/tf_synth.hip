@@ -1,5 +1,6 @@
 // tf_synth.hip -- synthetic depth streams rendered on the GPU (bench / test input, not the
-// product): the C5E hall of topfusion_amd/synth.py (render_hall), bit for bit.
+// product): the C2 / C5 room (render_room) and the C5E hall (render_hall) of
+// topfusion_amd/synth.py, bit for bit.
 //
 // The numpy renderer is the definition; this is the same float64 arithmetic in the same order
 // (compiled with -ffp-contract=off: no contraction, IEEE-correct division), so a frame rendered
@@ -116,7 +117,105 @@ __global__ void __launch_bounds__(256) k_render_hall(HallArgs a)
     *(uint16_t*)((char*)a.out + (size_t)f * a.stride + ((size_t)y * a.W + x) * 2) = (uint16_t)r;
 }
 
+struct RoomArgs {
+    uint16_t* out; size_t stride;
+    const double* poses;
+    int first, W, H, sphere;
+    double fx, fy, cx, cy, noise_mm;
+    uint32_t seed;
+};
+
+__device__ static inline double hashed_noise(uint32_t seed, uint32_t frame, uint32_t pix)
+{
+    const uint32_t base = mix32(mix32(seed + 0x2545F491u) ^ frame);
+    double s = 0.0;
+    for (int k = 0; k < 4; ++k) s = s + unit32(mix32(base ^ mix32(pix * 4u + (uint32_t)k + 0x68E31DA4u)));
+    return (s - 2.0) * 1.7320508075688772;
+}
+
+// synth.render_room: the room of render_depth (six walls + the sphere) with the hashed noise
+__global__ void __launch_bounds__(256) k_render_room(RoomArgs a)
+{
+    __shared__ double P[12];
+    const int f = blockIdx.z;
+    if (threadIdx.x < 12) P[threadIdx.x] = a.poses[12 * (size_t)f + threadIdx.x];
+    __syncthreads();
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.W || y >= a.H) return;
+    const double o[3] = { P[9], P[10], P[11] };
+    const double xc = ((double)x - a.cx) / a.fx, yc = ((double)y - a.cy) / a.fy;
+    const double d[3] = { (P[0] * xc + P[1] * yc) + P[2], (P[3] * xc + P[4] * yc) + P[5], (P[6] * xc + P[7] * yc) + P[8] };
+    const int ax[6] = { 2, 1, 0, 0, 1, 2 };
+    const double off[6] = { 1.8, 0.6, -0.8, 1.1, -0.9, -0.6 };
+    double best = INFINITY;
+    for (int k = 0; k < 6; ++k) {
+        const double tt = (off[k] - o[ax[k]]) / d[ax[k]];
+        best = fmin(best, (tt > 1e-6) ? tt : INFINITY);
+    }
+    if (a.sphere) {
+        const double oc[3] = { o[0] - 0.15, o[1] - 0.25, o[2] - 1.3 };
+        const double b = (d[0] * oc[0] + d[1] * oc[1]) + d[2] * oc[2];
+        const double aa = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+        const double cc = ((oc[0] * oc[0] + oc[1] * oc[1]) + oc[2] * oc[2]) - 0.09;
+        const double disc = b * b - aa * cc;
+        const double t0 = (-b - sqrt(fmax(disc, 0.0))) / aa;
+        best = fmin(best, (disc >= 0 && t0 > 1e-6) ? t0 : INFINITY);
+    }
+    double mm = best * 1000.0;
+    if (a.noise_mm > 0) mm = mm + a.noise_mm * hashed_noise(a.seed, (uint32_t)(a.first + f), (uint32_t)(y * a.W + x));
+    double r = isfinite(mm) ? rint(mm) : 0.0;
+    r = r < 0.0 ? 0.0 : (r > 65535.0 ? 65535.0 : r);
+    *(uint16_t*)((char*)a.out + (size_t)f * a.stride + ((size_t)y * a.W + x) * 2) = (uint16_t)r;
+}
+
 extern "C" {
+
+// frames first..first+n-1 of the room at the host poses [n][12] (camera -> world), as
+// tfs_render_hall; sphere: render_depth's sphere in the room.  Synchronous.  0 = ok.
+int tfs_render_room(uint16_t* dev_out, size_t stride, const double* poses, int n, int first, int W, int H,
+                    double fx, double fy, double cx, double cy, unsigned seed, double noise_mm, int sphere)
+{
+    if (!dev_out || !poses || n < 0 || W <= 0 || H <= 0 || stride < (size_t)W * H * 2) return 1;
+    const int B = 256;
+    double* dp = nullptr;
+    if (hipMalloc((void**)&dp, sizeof(double) * 12 * (size_t)(n < B ? n : B) + 16) != hipSuccess) return 2;
+    int rc = 0;
+    for (int f0 = 0; f0 < n && !rc; f0 += B) {
+        const int nb = n - f0 < B ? n - f0 : B;
+        if (hipMemcpy(dp, poses + 12 * (size_t)f0, sizeof(double) * 12 * nb, hipMemcpyHostToDevice) != hipSuccess) { rc = 3; break; }
+        RoomArgs a;
+        a.out = (uint16_t*)((char*)dev_out + (size_t)f0 * stride); a.stride = stride;
+        a.poses = dp; a.first = first + f0; a.W = W; a.H = H; a.sphere = sphere;
+        a.fx = fx; a.fy = fy; a.cx = cx; a.cy = cy; a.noise_mm = noise_mm; a.seed = seed;
+        hipLaunchKernelGGL(k_render_room, dim3((W + 15) / 16, (H + 15) / 16, nb), dim3(256), 0, 0, a);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = 4;
+    }
+    (void)hipFree(dp);
+    return rc;
+}
+
+// device-to-device copy bandwidth (read + write bytes / s) over `bytes`, HIP events, reps copies
+double tfs_copy_gbs(size_t bytes, int reps)
+{
+    void *a = nullptr, *b = nullptr;
+    double gbs = -1.0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipMalloc(&a, bytes) == hipSuccess && hipMalloc(&b, bytes) == hipSuccess &&
+        hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+        hipMemcpy(b, a, bytes, hipMemcpyDeviceToDevice) == hipSuccess) {
+        (void)hipEventRecord(e0, 0);
+        for (int i = 0; i < reps; ++i) (void)hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, 0);
+        (void)hipEventRecord(e1, 0);
+        float ms = 0.f;
+        if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0)
+            gbs = 2.0 * (double)bytes * reps / (ms * 1e-3) / 1e9;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    return gbs;
+}
 
 // frames first..first+n-1 of the hall walk into dev_out (frame k - first at k * stride bytes);
 // poses: host float64 [n][12] camera -> world (R row-major, t).  Synchronous.  0 = ok.

@@ -76,12 +76,10 @@ def _c5_compare(g, o, tag, swapping):
 @pytest.mark.parametrize("swapping", [False, True])
 def test_c5_bench_frames_640x480(oracle_mod, swapping):
     import bench
-    import torch
     from topfusion_amd import TopFu, default_params
     W, H, F, steps = 640, 480, 32, 2
-    dev = bench.walk_frames(steps * F, W, H, 13, "cuda:0")
-    torch.cuda.synchronize()
-    host = dev.cpu().numpy().view(np.uint16)
+    dev = bench.walk_frames(steps * F, W, H, 13)
+    host = dev.download(0, steps * F)
     fx, fy, cx, cy = synth.intrinsics(W, H)
     args = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=0.01)
     if swapping:
@@ -91,7 +89,7 @@ def test_c5_bench_frames_640x480(oracle_mod, swapping):
     fb = W * H * 2
     swapped_out = 0
     for s in range(steps):
-        okg = g.process_frames(dev.data_ptr() + s * F * fb, F)
+        okg = g.process_frames(dev.ptr + s * F * fb, F)
         oko = []
         for k in range(s * F, (s + 1) * F):
             oko.append(o(host[k]))
@@ -105,4 +103,4 @@ def test_c5_bench_frames_640x480(oracle_mod, swapping):
         assert g.totals()["swapped_out"] == swapped_out
         assert g.totals()["swapped_in_merged"] == o.swap_merged_total()
     g.close()
-    del dev
+    dev.free()

@@ -4,16 +4,17 @@ import ctypes, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import torch
+import bench
 from topfusion_amd import TopFu, default_params, synth
 from topfusion_amd import _lib
 W, H = 640, 480
 fx, fy, cx, cy = synth.intrinsics(W, H)
 frames = synth.orbit_sequence(60, W, H, seed=7)
-dev = torch.from_numpy(frames.view(np.int16)).cuda()
+dev = synth.DeviceStream(len(frames), frames.shape[2], frames.shape[1])
+dev.upload(frames)
 tf = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy), device=0)
-tf.process_frames(dev.data_ptr(), 60)
-torch.cuda.synchronize()
+tf.process_frames(dev.ptr, 60)
+bench.device_sync()
 L = _lib.load()
 ts = (ctypes.c_ulonglong * 16)()
 L.tf_debug_icp_ts(ts)

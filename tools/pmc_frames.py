@@ -19,13 +19,12 @@ def main():
     out = sys.argv[1]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     warm = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-    import torch
     import bench
     from topfusion_amd import TopFu, default_params, synth
     W, H, F = 640, 480, 32
     n = (warm + steps) * F
-    dev = bench.orbit_frames(n, W, H, 7, "cuda:0")
-    torch.cuda.synchronize()
+    dev = bench.orbit_frames(n, W, H, 7)
+    bench.device_sync()
     fx, fy, cx, cy = synth.intrinsics(W, H)
     tf = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy))
     tf.profile(True)             # (also counts the integration's voxel lanes; events do not change any kernel's traffic)
@@ -33,9 +32,9 @@ def main():
     ok = []
     for s in range(warm + steps):
         if s == warm:
-            torch.cuda.synchronize()
+            bench.device_sync()
             tf.reset_totals()
-        ok.extend(int(v) for v in tf.process_frames(dev.data_ptr() + s * F * fb, F))
+        ok.extend(int(v) for v in tf.process_frames(dev.ptr + s * F * fb, F))
     tot = tf.totals()
     # frame types: frame 0 of a run (the first, and every frame after a reset) takes the
     # integrate-only path; a tracked frame's ICP succeeded; a reset frame's ICP failed

@@ -16,24 +16,23 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    import torch
     import bench
     from topfusion_amd import TopFu, default_params, synth
     from topfusion_amd import _lib as L
     W, H, F = 640, 480, 32
     first, nsamp = 160, int(sys.argv[1]) if len(sys.argv) > 1 else 24
-    dev = bench.orbit_frames(first + nsamp, W, H, 7, "cuda:0")
-    torch.cuda.synchronize()
+    dev = bench.orbit_frames(first + nsamp, W, H, 7)
+    bench.device_sync()
     fx, fy, cx, cy = synth.intrinsics(W, H)
     tf = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy))
     fb = W * H * 2
-    tf.process_frames(dev.data_ptr(), first)
+    tf.process_frames(dev.ptr, first)
     lib = L.load()
     lib.tf_debug_ray_stats.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     buf = np.zeros(2 * 1280 * 960, np.uint32)
     rows = []
     for k in range(first, first + nsamp):
-        ok = tf.process_frames(dev.data_ptr() + k * fb, 1)
+        ok = tf.process_frames(dev.ptr + k * fb, 1)
         if not ok[0]:
             continue
         assert lib.tf_debug_ray_stats(buf.ctypes.data, buf.nbytes) == 0

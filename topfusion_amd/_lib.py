@@ -53,7 +53,7 @@ class TfTotals(ctypes.Structure):
     _fields_ = [(n, ctypes.c_longlong) for n in ("frames", "frames_tracked", "resets", "visible_sum", "tiles_sum",
                                                  "swapped_in", "swapped_out", "integrate_lanes_read",
                                                  "integrate_lanes_written", "swapped_in_merged",
-                                                 "alloc_failed_type1", "alloc_failed_type2")]
+                                                 "alloc_failed_type1", "alloc_failed_type2", "icp_fallbacks")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

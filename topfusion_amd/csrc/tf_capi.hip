@@ -193,6 +193,9 @@ static tf_status sync_state(tf_ctx* c)
 {
     TF_CHECK(hipMemcpyAsync(c->st_host, c->st, sizeof(TfDevState), hipMemcpyDeviceToHost, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
+    // a frame that failed past its ICP (tf_reset.h: frame_ok -3) left the context in error until
+    // tf_reset -- also when the call that enqueued it had already returned (per-call frames)
+    if (c->st_host->sticky_error) return TF_HIP_ERROR;
     return TF_OK;
 }
 
@@ -200,6 +203,8 @@ static tf_status sync_state(tf_ctx* c)
 // (visible list / types / range image) is deliberately left as is, like the reference.
 __global__ void k_host_reset(TfDevState* st)
 {
+    st->halt = 0;                      // (a device-side failure is cleared by the reset)
+    st->sticky_error = 0;
     if (st->frame_counter) st->n_resets++;
     st->frame_counter = 0;
     for (int i = 0; i < 12; ++i) st->pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
@@ -332,6 +337,13 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->verdict_dev, c->verdict_host, 0);
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
     memset(c->verdict_host, 0, sizeof(unsigned long long) * TF_VERDICT_WORDS);
+    {   // TFUSION_ICP_FAULT=launch:iteration (tests): that persistent ICP launch of the context reports a
+        // lost peer at that iteration, so the run-time fallback to the per-iteration schedule runs
+        const char* env = getenv("TFUSION_ICP_FAULT");
+        long long fl = 0; int fi = -1;
+        if (env && sscanf(env, "%lld:%d", &fl, &fi) == 2 && fl > 0 && fi >= 0) { c->icp_fault_launch = fl; c->icp_fault_iter = fi; }
+        else { c->icp_fault_launch = 0; c->icp_fault_iter = -1; }
+    }
     {   // TFUSION_PERCALL_EARLY=0: per-call frames wait for the whole frame; TFUSION_PERCALL_DEFER=0:
         // they enqueue all their launches (A/B)
         const char* env = getenv("TFUSION_PERCALL_EARLY");
@@ -571,9 +583,13 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
 }
 
 
-// sync, read back slots [first, first+n) and the state; ok_out gets 1/0 per frame
-static tf_status finish_frames(tf_ctx* c, int first, int n, int* ok_out)
+// sync, read back slots [first, first+n) and the state; ok_out gets 1/0 per frame.  *lost: the
+// slot whose persistent ICP lost a peer (frame_ok -1: nothing of it ran past the ICP, and the
+// later slots were skipped, -2), for the caller to re-run from there; -1 if none.  A frame that
+// failed past its ICP (-3) is TF_HIP_ERROR.
+static tf_status finish_frames(tf_ctx* c, int first, int n, int* ok_out, int* lost = nullptr)
 {
+    if (lost) *lost = -1;
     // one device-to-host copy into the pinned mirror: the state and the slots' ok / mode
     TF_CHECK(hipMemcpyAsync(c->st_host, c->st, TF_ST_BYTES, hipMemcpyDeviceToHost, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
@@ -582,13 +598,37 @@ static tf_status finish_frames(tf_ctx* c, int first, int n, int* ok_out)
     c->frame_counter = c->st_host->frame_counter;
     c->n_resets = c->st_host->n_resets;
     prof_collect(c, first, n, okb, modeb);
+    if (c->st_host->sticky_error) return TF_HIP_ERROR;
     tf_status r = TF_OK;
     for (int i = 0; i < n; ++i) {
+        if (okb[i] == -1 && lost) { *lost = i; break; }
         if (okb[i] < 0) return TF_HIP_ERROR;
         if (ok_out) ok_out[i] = okb[i];
         if (okb[i] == 0) r = TF_ICP_FAIL;
     }
     return r;
+}
+
+// Run-time fallback of the persistent ICP: a frame whose persistent launch lost a peer (some of
+// its 256 workgroups could not be co-resident -- another process or kernel on the device; the
+// bounded spins ended it: frame_ok -1, the frame end halted the batch) is enqueued again, whole,
+// on the per-iteration schedule (k_icp_iter: one launch per iteration, no co-residency needed).
+// Nothing of the failed attempt changed the scene (every stage after the ICP no-oped on abort),
+// so the re-run is the frame as it would have run.  Synchronous; *ok = its frame_ok.
+static tf_status rerun_frame_fallback(tf_ctx* c, const uint16_t* depth, size_t pitch, int* ok)
+{
+    TF_CHECK(hipMemsetAsync((char*)c->st + offsetof(TfDevState, halt), 0, sizeof(int), c->stream));
+    const int saved = c->icp_persistent;
+    c->icp_persistent = 0;
+    c->icp_fallbacks++;
+    tf_status s = enqueue_frame(c, depth, pitch, 0);
+    c->icp_persistent = saved;
+    if (s != TF_OK) return s;
+    int okv = 0;
+    s = finish_frames(c, 0, 1, &okv);
+    if (s != TF_OK && s != TF_ICP_FAIL) return s;
+    if (ok) *ok = okv;
+    return s;
 }
 
 extern "C" tf_status tf_profile_enable(tf_ctx* c, int enable)
@@ -715,9 +755,19 @@ static tf_status process_frame_early(tf_ctx* c, const uint16_t* depth, size_t pi
         __builtin_ia32_pause();
     }
     const int mode = (int)(w[0] & 15u), ok = (int)((w[0] >> 4) & 15u) - 1;
-    if (ok < 0) {                                 // a lost peer in the persistent ICP
-        (void)hipStreamSynchronize(c->stream);
-        return TF_HIP_ERROR;
+    if (ok < 0) {
+        // the frame's launches end on the device (the halted / failed frame no-ops); its deferred
+        // tail holds the frame end, enqueued now without a lookahead
+        const tf_status fs = flush_tail(c);
+        if (fs != TF_OK) return fs;
+        TF_CHECK(hipStreamSynchronize(c->stream));
+        if ((w[0] >> 16) & 1u) return TF_HIP_ERROR;           // halted: an earlier frame failed past its ICP
+        // a lost peer in the persistent ICP: the frame again, on the per-iteration schedule
+        int okv = 0;
+        const tf_status s2 = rerun_frame_fallback(c, depth, pitch, &okv);
+        if (s2 != TF_OK && s2 != TF_ICP_FAIL) return s2;
+        if (pose_out) memcpy(pose_out, c->st_host->pose, sizeof(float) * 12);
+        return s2;
     }
     // host mirrors of the counters the frame end writes (tf_reset.h)
     if (mode == 0) c->frame_counter = 1;
@@ -740,7 +790,9 @@ extern "C" tf_status tf_process_frame(tf_ctx* c, const uint16_t* dev_depth, size
     TF_FLUSH(c);
     tf_status s = enqueue_frame(c, dev_depth, pitch, 0);
     if (s != TF_OK) return s;
-    s = finish_frames(c, 0, 1, nullptr);
+    int lost = -1;
+    s = finish_frames(c, 0, 1, nullptr, &lost);
+    if (lost == 0) s = rerun_frame_fallback(c, dev_depth, pitch, nullptr);   // the persistent ICP lost a peer
     if (s != TF_OK && s != TF_ICP_FAIL) return s;
     if (pose_out) memcpy(pose_out, c->st_host->pose, sizeof(float) * 12);
     fill_stats(c, stats);
@@ -811,25 +863,38 @@ static tf_status process_frames(tf_ctx* c, const uint16_t* dev_frames, size_t st
     if (!c || !dev_frames || n < 0) return TF_INVALID_ARG;
     if (rgb_frames && rgb_stride == 0) rgb_stride = (size_t)c->W * c->H * 4;
     auto frame = [&](int j) { return (const uint16_t*)((const char*)dev_frames + (size_t)j * stride); };
-    for (int first = 0; first < n; first += TF_PROF_RING) {
+    int s0 = 0;                 // the frame the lookahead chain starts at (0, or after a fallback re-run)
+    for (int first = 0; first < n;) {
         const int m = n - first < TF_PROF_RING ? n - first : TF_PROF_RING;
         for (int i = 0; i < m; ++i) {
             const int j = first + i;
             // two-frame lookahead (enqueue_frame): frame j+1's pyramid pass and frame j+2's
             // bilateral pass run in frame j's grid tails
-            TfFramePlan p = { j > 0, c->d0_buf[j & 1], {}, {}, {}, 0 };
+            TfFramePlan p = { j > s0, c->d0_buf[j & 1], {}, {}, {}, 0 };
             if (j + 1 < n) {
                 TfAhead next = { frame(j + 1), c->d0_buf[(j + 1) & 1] };
                 p.pair_pyr = next;
-                if (j == 0) p.alloc_bil = next;
+                if (j == s0) p.alloc_bil = next;
                 if (j + 2 < n) p.pair_bil = TfAhead{ frame(j + 2), c->d0_buf[j & 1] };
             }
             RgbScope rs(c, rgb_frames ? rgb_frames + (size_t)j * rgb_stride : nullptr, (size_t)c->W * 4);
             tf_status s = enqueue_frame(c, frame(j), (size_t)c->W * 2, i, &p);
             if (s != TF_OK) return s;
         }
-        tf_status s = finish_frames(c, 0, m, ok_out ? ok_out + first : nullptr);
+        int lost = -1;
+        tf_status s = finish_frames(c, 0, m, ok_out ? ok_out + first : nullptr, &lost);
         if (s != TF_OK && s != TF_ICP_FAIL) return s;
+        if (lost < 0) { first += m; continue; }
+        // frame first+lost lost an ICP peer, the rest of the group was skipped: re-run it on the
+        // per-iteration schedule (its own preprocessing: its maps were overwritten by the lookahead
+        // of the skipped frames), then continue the batch after it with a fresh lookahead chain
+        const int j = first + lost;
+        RgbScope rs(c, rgb_frames ? rgb_frames + (size_t)j * rgb_stride : nullptr, (size_t)c->W * 4);
+        int okv = 0;
+        s = rerun_frame_fallback(c, frame(j), (size_t)c->W * 2, &okv);
+        if (s != TF_OK && s != TF_ICP_FAIL) return s;
+        if (ok_out) ok_out[j] = okv;
+        first = s0 = j + 1;
     }
     return TF_OK;
 }
@@ -1461,6 +1526,7 @@ extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)
     t->swapped_in = d->tot_swap_in; t->swapped_out = d->tot_swap_out;
     t->swapped_in_merged = d->tot_swap_merged;
     t->alloc_failed_type1 = d->tot_alloc_fail1; t->alloc_failed_type2 = d->tot_alloc_fail2;
+    t->icp_fallbacks = c->icp_fallbacks;
     t->integrate_lanes_read = t->integrate_lanes_written = 0;
     std::vector<long long> h(2 * TF_INTEG_WG);
     TF_CHECK(hipMemcpyAsync(h.data(), c->integ_cnt, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, c->stream));
@@ -1477,5 +1543,6 @@ extern "C" tf_status tf_reset_totals(tf_ctx* c)
     TF_CHECK(hipMemsetAsync((char*)c->st + b, 0, e - b, c->stream));
     TF_CHECK(hipMemsetAsync(c->integ_cnt, 0, sizeof(long long) * 2 * TF_INTEG_WG, c->stream));
     TF_CHECK(hipStreamSynchronize(c->stream));
+    c->icp_fallbacks = 0;
     return TF_OK;
 }

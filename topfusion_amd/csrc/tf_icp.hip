@@ -335,19 +335,21 @@ struct IcpFrameArgs {
     // while the rest of the frame runs (tf_verdict_*, tf_capi.hip); nullptr: not requested
     unsigned long long* verdict;
     unsigned verdict_gen;
+    int fault_iter;                     // >= 0: report a lost peer at this iteration (fault injection, tests)
 };
 
 // the verdict record: TF_VERDICT_WORDS 64-bit words, each (generation << 32 | payload), written
 // with system-scope stores into fine-grained host memory; the host accepts the record once every
 // word carries the generation it armed.  Word 0: mode | (ok + 1) << 4 | iterations << 8;
-// words 1..12: the pose's float bits.
-static __device__ void icp_verdict(const IcpFrameArgs& a, int mode, int ok, int iters, const float* pose)
+// words 1..12: the pose's float bits.  Bit 16 of word 0: the context is halted by an earlier
+// frame (tf_reset.h) -- this frame did not run.
+static __device__ void icp_verdict(const IcpFrameArgs& a, int mode, int ok, int iters, const float* pose, int halted = 0)
 {
     const unsigned long long g = (unsigned long long)a.verdict_gen << 32;
     for (int i = 0; i < 12; ++i)
         __hip_atomic_store(&a.verdict[1 + i], g | __float_as_uint(pose[i]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&a.verdict[0], g | (unsigned)(mode | (ok + 1) << 4 | iters << 8), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.verdict[0], g | (unsigned)(mode | (ok + 1) << 4 | iters << 8 | (halted ? 1u << 16 : 0u)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // k_set_type3's work (render_snapshot + set_type3_pass) in every workgroup of the persistent
@@ -572,7 +574,20 @@ k_icp_frame(IcpFrameArgs a)
         // frame's mode; every workgroup derives it from frame_counter, which only the previous
         // frame's end wrote (so the preprocessing stream never touches the state)
         const bool frame0 = st->frame_counter == 0;
+        const bool halted = st->halt != 0;              // (only a frame end writes it: uniform)
         if (wg == 0 && tid == 0) tf_frame_begin(st);
+        if (halted) {                                   // an earlier frame failed: this one is skipped
+            if (a.verdict && wg == 0 && tid == 0) {
+                float pose[12];
+                for (int i = 0; i < 12; ++i) pose[i] = st->pose[i];
+                icp_verdict(a, frame0 ? 0 : 1, -1, 0, pose, 1);
+            }
+            if (a.fold_t3) {                            // (the renderImage snapshot's go flag: off)
+                __syncthreads();
+                icp_fold_t3(a, pose0_s, nullptr, 1, 2);
+            }
+            return;
+        }
         if (frame0) {
             if (a.verdict && wg == 0 && tid == 0) {             // return ++frame_counter_, true (topfu.cpp:209)
                 float pose[12];
@@ -761,7 +776,7 @@ k_icp_frame(IcpFrameArgs a)
                     }
                     tv[q][x] = __uint_as_float((unsigned)v);
                 }
-                const int any_timeout = __syncthreads_or(timeout);
+                const int any_timeout = __syncthreads_or(timeout || done == a.fault_iter);
                 IPT_REC(done, 2 * ICP_NWG + 0);
                 if (!any_timeout && (wave == 0 || wave == IP_DETW)) {
                     // steps 4, 2, 1: ((P0+P4) + (P2+P6)) + ((P1+P5) + (P3+P7)); lane q holds sum q
@@ -866,7 +881,7 @@ __global__ void k_icp_begin(TfDevState* st, int frame_begin)
     for (int i = 0; i < 12; ++i) st->affine[i] = (i % 5 == 0) ? 1.0f : 0.0f;   // affine = Identity
     st->icp_ok = 1;
     st->icp_iters = 0;
-    st->abort = 0;
+    st->abort = st->halt ? 1 : 0;              // a halted batch: the iterations no-op
 }
 
 // explicit pose (stage entry points / frame 0): pose_in -> matrices
@@ -969,6 +984,7 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
             a.verdict = c->verdict_dev;
             a.verdict_gen = c->verdict_gen;
         }
+        a.fault_iter = ++c->icp_launches == c->icp_fault_launch ? c->icp_fault_iter : -1;
         // IP_LDS_PAD bytes of dynamic LDS (unused) take the workgroup above 80 KiB: at most one
         // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up
         hipError_t e = tf_icp_order_before(c);

@@ -65,11 +65,13 @@ struct TfDevState {
     int frame_counter;       // TopFu::frame_counter_
     int n_resets;            // resets taken after ICP failures
     unsigned reset_ticket;   // k_reset_scene: workgroups done (the last one resets the counters)
-    int pad4_;
+    int halt;                // set by a frame end whose frame failed on the device (frame_ok < 0): every later
+                             // frame of the batch is skipped (frame_ok -2) until the host clears it
     unsigned pad5_;
     int scene_external;      // scene buffers / counters set from the host since the last full reset:
                              // the next reset (in-frame ones too) clears everything, then drops it
-    int pad2_;
+    int sticky_error;        // a frame failed past its ICP (a bounded spin in a later stage timed out): the
+                             // context reports TF_HIP_ERROR until tf_reset
     // the frame's renderImage runs in k_raycast_pair after CreateExpectedDepths has rewritten the
     // range image; it reads the raycast matrix, go flag and range region snapshotted before
     // (render_snapshot / icp_fold_t3)
@@ -371,6 +373,12 @@ struct tf_ctx {
     int tail_pending;
     int tail_fuse_ed;
     int percall_defer;                   // TFUSION_PERCALL_DEFER (default 1)
+    // persistent-ICP fault injection (tests): the icp_fault_launch-th persistent ICP launch of the
+    // context reports a lost peer at iteration icp_fault_iter (TFUSION_ICP_FAULT=launch:iteration)
+    long long icp_launches;
+    long long icp_fault_launch;
+    int icp_fault_iter;
+    long long icp_fallbacks;             // frames re-run on the per-iteration schedule after a lost peer
     // engine-level batches (tf_scene_fuse_frames, tf_fuse.hip): the batch's poses and per-frame records
     float* fuse_pose;                    // [fuse_cap][12] world -> camera, row-major [R|t]
     int* fuse_rec;                       // [fuse_cap] tf_fuse_record

@@ -85,7 +85,7 @@ static __device__ __attribute__((unused)) void tf_set_pose_matrices(TfDevState* 
 // per-frame flags; frame 0 uses poses_.back() as is for allocation / integration
 static __device__ __attribute__((unused)) void tf_frame_begin(TfDevState* st)
 {
-    st->abort = 0;
+    st->abort = st->halt ? 1 : 0;       // a halted batch (tf_reset.h): every stage of the frame no-ops
     st->mode = st->frame_counter == 0 ? 0 : 1;
     st->icp_ok = 1;
     st->icp_iters = 0;

@@ -1356,7 +1356,7 @@ k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
                 // the fill's atomic path writes the range image: wait until every row is done
                 unsigned spins = 0;
                 while (__hip_atomic_load(ed.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nfill) {
-                    if (++spins > (1u << 24)) { st->icp_ok = -1; break; }   // the frame end reports a HIP error
+                    if (++spins > (1u << 24)) { st->icp_ok = -2; break; }   // the frame end reports a HIP error (sticky)
                     __builtin_amdgcn_s_sleep(2);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

@@ -35,15 +35,22 @@ __device__ __forceinline__ void reset_scene_block(const ResetArgs& r, int bid, i
         // frame_counter / n_resets / pose change here, never the mode / icp_ok read below
         const int mode = st->mode, icp_ok = st->icp_ok;
         int ok;
-        if (mode == 0) { st->frame_counter = 1; ok = 1; }
-        else if (icp_ok < 0) ok = -1;                       // persistent ICP lost a peer
-        else if (icp_ok == 0) {                             // return reset(), false
+        if (st->halt) ok = -2;                              // skipped: an earlier frame of the batch failed
+        else if (mode == 0) { st->frame_counter = 1; ok = 1; }
+        else if (icp_ok == -1) {                            // the persistent ICP lost a peer: nothing past the
+            ok = -1;                                        // ICP ran, the host re-runs the frame (fallback)
+            st->halt = 1;
+        } else if (icp_ok < -1) {                           // a later stage's bounded spin timed out: the
+            ok = -3;                                        // frame is half done, the context is in error
+            st->halt = 1;
+            st->sticky_error = 1;
+        } else if (icp_ok == 0) {                           // return reset(), false
             st->n_resets++;
             st->frame_counter = 0;
             for (int i = 0; i < 12; ++i) st->pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
             ok = 0;
         } else { st->frame_counter++; ok = 1; }
-        st->tot_frames++;
+        if (ok >= 0) st->tot_frames++;
         if (ok == 0) st->tot_resets++;
         if (ok == 1) st->tot_visible += st->noVisibleEntries;      // the list this frame integrated
         if (ok == 1 && mode == 1) { st->tot_tracked++; st->tot_tiles += st->noTotalBlocks; }

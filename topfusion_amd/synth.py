@@ -210,40 +210,6 @@ def random_walk_sequence(n, cols=640, rows=480, seed=13, noise_mm=1.0, step_m=0.
     return out
 
 
-def render_depth_torch(R, t, cols=640, rows=480, noise_mm=1.0, generator=None, device="cuda"):
-    """The same analytic room + sphere as render_depth, for a batch of poses on a torch device
-    (float64; noise from torch's generator): the bench's way to make long sequences (C5's
-    50 k frames) without a host renderer in the loop.  Returns int16 (B, rows, cols) holding
-    the uint16 millimetre bits."""
-    import torch
-    fx, fy, cx, cy = intrinsics(cols, rows)
-    R = torch.as_tensor(R, dtype=torch.float64, device=device)
-    t = torch.as_tensor(t, dtype=torch.float64, device=device)
-    u = torch.arange(cols, dtype=torch.float64, device=device)
-    v = torch.arange(rows, dtype=torch.float64, device=device)
-    vv, uu = torch.meshgrid(v, u, indexing="ij")
-    dc = torch.stack([(uu - cx) / fx, (vv - cy) / fy, torch.ones_like(uu)], dim=-1)      # (H, W, 3)
-    dw = torch.einsum("hwk,bjk->bhwj", dc, R)                                           # (B, H, W, 3)
-    o = t[:, None, None, :]
-    best = torch.full(dw.shape[:3], float("inf"), dtype=torch.float64, device=device)
-    for ax, off in [(2, 1.8), (1, 0.6), (0, -0.8), (0, 1.1), (1, -0.9), (2, -0.6)]:
-        tt = (off - o[..., ax]) / dw[..., ax]
-        best = torch.minimum(best, torch.where(tt > 1e-6, tt, torch.full_like(tt, float("inf"))))
-    c = torch.tensor([0.15, 0.25, 1.3], dtype=torch.float64, device=device)
-    oc = o - c
-    b = (dw * oc).sum(-1)
-    a = (dw * dw).sum(-1)
-    cc = (oc * oc).sum(-1) - 0.09
-    disc = b * b - a * cc
-    t0 = (-b - torch.sqrt(torch.clamp(disc, min=0))) / a
-    best = torch.minimum(best, torch.where((disc >= 0) & (t0 > 1e-6), t0, torch.full_like(t0, float("inf"))))
-    mm = best * 1000.0
-    if noise_mm > 0:
-        mm = mm + noise_mm * torch.randn(mm.shape, dtype=torch.float64, device=device, generator=generator)
-    mm = torch.where(torch.isfinite(mm), torch.round(mm), torch.zeros_like(mm))
-    return torch.clamp(mm, 0, 65535).to(torch.int32).to(torch.int16)
-
-
 # ----------------------------------------------------------------------------------------
 # A voxel-block hash built directly from a list of block positions (the C3 HBM-scale scene)
 # ----------------------------------------------------------------------------------------
@@ -503,11 +469,14 @@ def synth_lib():
         L = ctypes.CDLL(_SYNTH_SO)
         P, S, I, D = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double
         L.tfs_render_hall.argtypes = [P, S, P, I, I, I, I, D, D, D, D, ctypes.c_uint, D]
+        L.tfs_render_room.argtypes = [P, S, P, I, I, I, I, D, D, D, D, ctypes.c_uint, D, I]
+        L.tfs_copy_gbs.argtypes = [S, I]
+        L.tfs_copy_gbs.restype = D
         L.tfs_malloc.argtypes = [ctypes.POINTER(P), S]
         L.tfs_free.argtypes = [P]
         L.tfs_download.argtypes = [P, P, S]
         L.tfs_upload.argtypes = [P, P, S]
-        for f in ("tfs_render_hall", "tfs_malloc", "tfs_free", "tfs_download", "tfs_upload", "tfs_sync"):
+        for f in ("tfs_render_hall", "tfs_render_room", "tfs_malloc", "tfs_free", "tfs_download", "tfs_upload", "tfs_sync"):
             getattr(L, f).restype = I
         _synth = L
     return _synth
@@ -565,3 +534,89 @@ def render_hall_device(stream, R, t, first=0, seed=13, noise_mm=1.0, k0=0):
                                      P.ctypes.data_as(ctypes.c_void_p), n, first, stream.cols, stream.rows,
                                      fx, fy, cx, cy, seed, noise_mm)
     assert rc == 0, f"tfs_render_hall: {rc}"
+
+
+def render_room(R, t, cols=640, rows=480, noise_mm=1.0, seed=7, frame=0, sphere=True, intr=None):
+    """The C2 / C5 room (render_depth's geometry: six walls, the sphere r = 0.3 m at (0.15, 0.25,
+    1.3)) with the hall's hashed Irwin-Hall noise instead of numpy's generator, every operation in
+    a fixed order: the reference renderer of synth/tf_synth.hip (tfs_render_room), same bits.
+    This is what the bench and the GPU tests render on the device."""
+    fx, fy, cx, cy = intr if intr is not None else intrinsics(cols, rows)
+    R = np.asarray(R, np.float64)
+    o = np.asarray(t, np.float64)
+    u = np.arange(cols, dtype=np.float64)
+    v = np.arange(rows, dtype=np.float64)
+    uu, vv = np.meshgrid(u, v)
+    xc, yc = (uu - cx) / fx, (vv - cy) / fy
+    d = [(R[0, 0] * xc + R[0, 1] * yc) + R[0, 2], (R[1, 0] * xc + R[1, 1] * yc) + R[1, 2],
+         (R[2, 0] * xc + R[2, 1] * yc) + R[2, 2]]
+    best = np.full((rows, cols), np.inf)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for ax, off in ROOM_PLANES:
+            tt = (off - o[ax]) / d[ax]
+            best = np.minimum(best, np.where(tt > 1e-6, tt, np.inf))
+        if sphere:
+            oc = (o[0] - 0.15, o[1] - 0.25, o[2] - 1.3)
+            b = (d[0] * oc[0] + d[1] * oc[1]) + d[2] * oc[2]
+            a = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]
+            cc = ((oc[0] * oc[0] + oc[1] * oc[1]) + oc[2] * oc[2]) - 0.09
+            disc = b * b - a * cc
+            t0 = (-b - np.sqrt(np.maximum(disc, 0.0))) / a
+            best = np.minimum(best, np.where((disc >= 0) & (t0 > 1e-6), t0, np.inf))
+    mm = best * 1000.0
+    if noise_mm > 0:
+        mm = mm + noise_mm * hall_noise(seed, frame, cols, rows)
+    mm = np.where(np.isfinite(mm), np.rint(mm), 0.0)
+    return np.clip(mm, 0, 65535).astype(np.uint16)
+
+
+ROOM_PLANES = ((2, 1.8), (1, 0.6), (0, -0.8), (0, 1.1), (1, -0.9), (2, -0.6))   # render_depth's walls
+
+
+def render_room_device(stream, R, t, first=0, seed=7, noise_mm=1.0, k0=0, sphere=True, intr=None):
+    """Frames first.. of the room at poses (R, t) camera->world, rendered on the GPU into stream
+    slots k0.. (synth/tf_synth.hip: render_room's bits)."""
+    import ctypes
+    n = len(R)
+    P = np.zeros((n, 12), np.float64)
+    P[:, :9] = np.asarray(R, np.float64).reshape(n, 9)
+    P[:, 9:] = np.asarray(t, np.float64)
+    fx, fy, cx, cy = intr if intr is not None else intrinsics(stream.cols, stream.rows)
+    rc = synth_lib().tfs_render_room(ctypes.c_void_p(stream.frame_ptr(k0)), stream.frame_bytes,
+                                     P.ctypes.data_as(ctypes.c_void_p), n, first, stream.cols, stream.rows,
+                                     fx, fy, cx, cy, seed, noise_mm, 1 if sphere else 0)
+    assert rc == 0, f"tfs_render_room: {rc}"
+
+
+def orbit_device(n, cols=640, rows=480, seed=7, noise_mm=1.0):
+    """C2 / C3: n frames of the orbit (orbit_pose; asserted inside the room) rendered on the GPU."""
+    R = np.empty((n, 3, 3))
+    t = np.empty((n, 3))
+    for k in range(n):
+        R[k], t[k] = orbit_pose(k)
+        assert orbit_in_room(R[k], t[k]), f"orbit frame {k}: camera outside the room"
+    s = DeviceStream(n, cols, rows)
+    for b0 in range(0, n, 1024):
+        b1 = min(n, b0 + 1024)
+        render_room_device(s, R[b0:b1], t[b0:b1], first=b0, seed=seed, noise_mm=noise_mm, k0=b0)
+    return s
+
+
+def walk_device(n, cols=640, rows=480, seed=13, noise_mm=1.0):
+    """C5: n frames of the room random walk (random_walk_poses) rendered on the GPU."""
+    R, t = random_walk_poses(n, seed=seed)
+    s = DeviceStream(n, cols, rows)
+    for b0 in range(0, n, 1024):
+        b1 = min(n, b0 + 1024)
+        render_room_device(s, R[b0:b1], t[b0:b1], first=b0, seed=seed, noise_mm=noise_mm, k0=b0)
+    return s
+
+
+def hall_device(n, cols=640, rows=480, seed=13, noise_mm=1.0):
+    """C5E: n frames of the hall walk rendered on the GPU; returns (stream, R, t)."""
+    R, t = hall_walk_poses(n, seed)
+    s = DeviceStream(n, cols, rows)
+    for b0 in range(0, n, 1024):
+        b1 = min(n, b0 + 1024)
+        render_hall_device(s, R[b0:b1], t[b0:b1], first=b0, seed=seed, noise_mm=noise_mm, k0=b0)
+    return s, R, t
