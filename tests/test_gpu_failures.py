@@ -1,0 +1,80 @@
+"""Device-side failures (include/tfusion_hip.h, "Device-side failures"), each forced
+deterministically by a fault-injection switch read at tf_create:
+
+* TFUSION_ICP_FAULT=launch:iteration -- that persistent ICP launch reports a lost peer (as when
+  another process holds part of the device and not all 256 workgroups are co-resident).  The
+  frame is re-run on the per-iteration schedule and continues: every frame bit-exact with the
+  oracle, whichever path (batch, per-call returning on the verdict, per-call synchronous).
+* TFUSION_FILL_FAULT=launch -- that k_raycast_pair launch's wait for the range image fails (past
+  the ICP: the frame is half done).  The context reports TF_HIP_ERROR from then on -- on the next
+  call for a per-call frame that had already returned -- until tf_reset."""
+import numpy as np
+import pytest
+
+from parity_util import DeviceFrames
+from test_gpu_parity import _compare_frame_state, compare_scene, make_pair
+from topfusion_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+W, H, N = 320, 240, 8
+
+
+@pytest.mark.parametrize("mode", ["batch", "per_call", "per_call_sync"])
+def test_icp_lost_peer_fallback(oracle_mod, monkeypatch, mode):
+    from topfusion_amd import _lib as L
+    monkeypatch.setenv("TFUSION_ICP_FAULT", "3:5")        # frame 2's persistent launch, at iteration 5
+    if mode == "per_call_sync":
+        monkeypatch.setenv("TFUSION_PERCALL_EARLY", "0")
+    g, o = make_pair(oracle_mod, W, H)
+    assert g.icp_persistent()
+    frames = synth.orbit_sequence(N, W, H, seed=7)
+    dev = DeviceFrames(frames)
+    fb = W * H * 2
+    if mode == "batch":
+        okg = g.process_frames(dev.ptr, N)
+    else:
+        okg = np.array([g(dev.ptr + k * fb) for k in range(N)])
+    oko = np.array([o(frames[k]) for k in range(N)])
+    assert np.array_equal(okg, oko), (okg, oko)
+    assert okg[2], "frame 2 must be a tracked frame for the fault to hit"
+    pg = g.getCameraPose()[:3, :4]
+    assert np.array_equal(pg.view(np.uint32), o.pose().view(np.uint32))
+    _compare_frame_state(g, o, f"lost peer ({mode})", grey=bool(oko[-1]))
+    compare_scene(g, o, f"lost peer ({mode})")
+    assert g.totals()["icp_fallbacks"] == 1
+    assert g.stats()["icp_iterations"] == o.counters()["icp_iterations"]
+    g.close()
+    dev.free()
+
+
+@pytest.mark.parametrize("mode", ["batch", "per_call"])
+def test_error_past_icp_is_sticky(monkeypatch, mode):
+    from topfusion_amd import TopFu, default_params, _lib as L
+    monkeypatch.setenv("TFUSION_ED_LDS_MAX_N", "0")       # the fill's atomic path: CreateICPMaps' tiles wait on it
+    monkeypatch.setenv("TFUSION_FILL_FAULT", "3")         # frame 2's k_raycast_pair: the wait fails
+    fx, fy, cx, cy = synth.intrinsics(W, H)
+    g = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy))
+    frames = synth.orbit_sequence(N, W, H, seed=7)
+    dev = DeviceFrames(frames)
+    fb = W * H * 2
+    if mode == "batch":
+        with pytest.raises(L.TfError) as ei:
+            g.process_frames(dev.ptr, N)
+        assert ei.value.status == L.TF_HIP_ERROR
+    else:
+        for k in range(3):
+            assert g(dev.ptr + k * fb)                     # frame 2 returns on its verdict, before its tail runs
+        with pytest.raises(L.TfError) as ei:
+            g(dev.ptr + 3 * fb)                            # reported by the next call
+        assert ei.value.status == L.TF_HIP_ERROR
+    for call in (g.stats, g.getCameraPose, lambda: g(dev.ptr)):
+        with pytest.raises(L.TfError) as ei:               # sticky: every call until tf_reset
+            call()
+        assert ei.value.status == L.TF_HIP_ERROR
+    g.reset()
+    ok = g.process_frames(dev.ptr, N)                      # the context works again
+    assert ok.all()
+    assert g.stats()["frame_counter"] == N
+    g.close()
+    dev.free()

@@ -343,6 +343,10 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         long long fl = 0; int fi = -1;
         if (env && sscanf(env, "%lld:%d", &fl, &fi) == 2 && fl > 0 && fi >= 0) { c->icp_fault_launch = fl; c->icp_fault_iter = fi; }
         else { c->icp_fault_launch = 0; c->icp_fault_iter = -1; }
+        // TFUSION_FILL_FAULT=launch: that k_raycast_pair launch's wait for the range image fails
+        // (past the ICP: the sticky-error path)
+        env = getenv("TFUSION_FILL_FAULT");
+        c->fill_fault_launch = env ? atoll(env) : 0;
     }
     {   // TFUSION_PERCALL_EARLY=0: per-call frames wait for the whole frame; TFUSION_PERCALL_DEFER=0:
         // they enqueue all their launches (A/B)

@@ -21,6 +21,7 @@ struct EdArgs {
     int nrows;           // k_ed_fill's LDS rows (ed_nrows: rr + ED_XROWS, at most H)
     int lds_max_n;       // k_ed_fill's LDS-row path up to this many visible entries
     int vcap, nchunk_max;   // box / chunk-total buffer lengths (k_ed_fill's early loads)
+    int fault;           // fault injection (tests): the ICP tiles' wait on the fill's atomic path fails
     float fx, fy, cx, cy, voxelSize;
     unsigned cap;
 };

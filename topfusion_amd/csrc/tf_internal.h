@@ -379,6 +379,9 @@ struct tf_ctx {
     long long icp_fault_launch;
     int icp_fault_iter;
     long long icp_fallbacks;             // frames re-run on the per-iteration schedule after a lost peer
+    // ... and the fill_fault_launch-th k_raycast_pair launch's range-image wait fails (TFUSION_FILL_FAULT)
+    long long pair_launches;
+    long long fill_fault_launch;
     // engine-level batches (tf_scene_fuse_frames, tf_fuse.hip): the batch's poses and per-frame records
     float* fuse_pose;                    // [fuse_cap][12] world -> camera, row-major [R|t]
     int* fuse_rec;                       // [fuse_cap] tf_fuse_record

@@ -1201,7 +1201,7 @@ void tf_ed_args(tf_ctx* c, EdArgs* out)
     a.hash = c->hash; a.visibleIds = c->visibleIds; a.range = (float2*)c->range;
     a.rec = c->blockRec; a.tiles = c->blockTiles; a.off = c->blockOff; a.chunk = c->edChunk;
     a.spill = c->edSpill;
-    a.bins = c->edBins; a.bin_cnt = c->edBinCnt; a.keep_bins = 0; a.done = nullptr;
+    a.bins = c->edBins; a.bin_cnt = c->edBinCnt; a.keep_bins = 0; a.done = nullptr; a.fault = 0;
     a.W = c->W; a.H = c->H;
     a.rc = (c->W - 1) / TF_SUBSAMPLE + 1; a.rr = (c->H - 1) / TF_SUBSAMPLE + 1;
     a.nrows = ed_nrows(c->H);
@@ -1356,7 +1356,7 @@ k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
                 // the fill's atomic path writes the range image: wait until every row is done
                 unsigned spins = 0;
                 while (__hip_atomic_load(ed.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nfill) {
-                    if (++spins > (1u << 24)) { st->icp_ok = -2; break; }   // the frame end reports a HIP error (sticky)
+                    if (++spins > (1u << 24) || ed.fault) { st->icp_ok = -2; break; }   // the frame end: a sticky HIP error
                     __builtin_amdgcn_s_sleep(2);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1427,6 +1427,7 @@ hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch, i
         nfill_pad = (nfill + 7) / 8 * 8;        // keeps the tiles' XCD swizzle aligned
         ed.done = c->edDone;
     }
+    ed.fault = ++c->pair_launches == c->fill_fault_launch;
     tf_launch(c, k_raycast_pair, dim3(nfill_pad + 2 * nb + n_pyr + n_bil), dim3(256), 0, ai, ar, c->st, tx, n, nb,
               pp, n_pyr, pyr_gx, bb, bil_gx, ed, nfill, nfill_pad);
     return hipGetLastError();
