@@ -76,6 +76,9 @@ def parse():
                          "blocks out of view evicted / brought back every frame (SURVEY §8f-2; C5 churn)")
     ap.add_argument("--swap-transfer-blocks", type=int, default=0x1000,
                     help="blocks moved per direction per frame (SDF_TRANSFER_BLOCK_NUM, VoxelBlockHash.hpp:27)")
+    ap.add_argument("--colour", action="store_true",
+                    help="C2 with the colour TSDF: Voxel_s_rgb voxels integrated from a synthetic colour stream "
+                         "(depth+colour, TopFu::operator()(depth, image), topfu.hpp:80); GPU-rendered RGB frames")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample length")
     ap.add_argument("--no-profile", action="store_true", help="disable the per-stage HIP-event timing")
@@ -218,7 +221,9 @@ def cpu_baseline_protocol(frames, first, params_kw, seconds, nt):
                                         f"median of 5 runs after 1 warm-up ({s1['runs_s']} s)",
                               "c1_ms_per_frame": round(s1["c1_ms"], 3)},
             "cpu_model": model, "nproc": nproc, "affinity_cpus": len(os.sched_getaffinity(0)),
-            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "cores_note": ("OMP_NUM_THREADS: the GPU pool gives a one-GPU job a share of the host's CPUs (16 of the "
+                           "machine's, which the 8 GPUs' jobs share); nproc / affinity show the whole machine")}
 
 
 def combine_ranks(elapsed, frames, device, world):
@@ -561,6 +566,8 @@ def main():
     pkw = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=args.voxel, **cfg["capacity"])
     if args.swapping:
         pkw.update(use_swapping=1, swap_transfer_blocks=args.swap_transfer_blocks)
+    if args.colour:
+        pkw.update(voxel_rgb=1)            # rgb_intr 0 / depth_to_rgb 0: the colour camera registered with the depth one
     n_breakdown = 0 if args.no_profile else min(args.breakdown_frames, args.steps * F)
     n_frames = (args.warmup + args.steps) * F
     device = f"cuda:{local_rank}"
@@ -568,6 +575,14 @@ def main():
     dev = (walk_frames if cfg["walk"] else orbit_frames)(n_frames, W, H, seed)
     frame_bytes = W * H * 2
     base = dev.ptr
+    rgb = synth.orbit_colour_device(n_frames, W, H) if args.colour else None
+    rgb_bytes = W * H * 4
+
+    def run(tfx, k0, n):
+        """frames k0..k0+n-1 of the stream as one tf_process_frames(_rgb) batch"""
+        if rgb is None:
+            return tfx.process_frames(base + k0 * frame_bytes, n)
+        return tfx.process_frames(base + k0 * frame_bytes, n, rgb_frames=rgb.ptr + k0 * rgb_bytes, rgb_stride=rgb_bytes)
 
     tf = TopFu(default_params(**pkw), device=local_rank)
     single = [k for k in SINGLE_KERNEL_STAGES if k != "icp" or tf.icp_persistent()]
@@ -578,7 +593,7 @@ def main():
     if args.warmup > 0:
         tf.profile(not args.no_profile)
         for w in range(args.warmup):
-            tf.process_frames(base + w * F * frame_bytes, F)
+            run(tf, w * F, F)
         if not args.no_profile:
             pw = tf.profile_read()
             avg = {k: pw[k][0] / pw[k][1] for k in single if pw[k][1]}
@@ -595,7 +610,7 @@ def main():
     t0 = time.perf_counter()
     oks = []
     for k in range(args.steps):
-        oks.append(tf.process_frames(base + (args.warmup + k) * F * frame_bytes, F))
+        oks.append(run(tf, (args.warmup + k) * F, F))
     device_sync()
     if world > 1:
         dist.barrier()
@@ -610,10 +625,10 @@ def main():
         # per-stage breakdown: a fresh context replays the warm-up and the first frames of the
         # timed region with every stage timed (outside the timed region)
         tb = TopFu(default_params(**pkw), device=local_rank)
-        tb.process_frames(base, args.warmup * F)
+        run(tb, 0, args.warmup * F)
         tb.profile(True)
         tb.reset_totals()
-        tb.process_frames(base + args.warmup * F * frame_bytes, n_breakdown)
+        run(tb, args.warmup * F, n_breakdown)
         prof = tb.profile_read()
         tbt = tb.totals()
         n_int = max(1, tbt["frames"] - tbt["resets"])
@@ -625,7 +640,7 @@ def main():
     # frames of the timed region, from a fresh context, and the batched rate of a fresh context on
     # the same frames beside it (the orbit's cost per frame varies along it: compare like with like)
     per_call = per_call_batched = None
-    nc = min(args.per_call_frames, args.steps * F)
+    nc = min(args.per_call_frames, args.steps * F) if rgb is None else 0   # (colour: RGB frames wait for the whole frame)
     if nc > 0:
         pc_base = base + args.warmup * F * frame_bytes
         tc = TopFu(default_params(**pkw), device=local_rank)
@@ -635,6 +650,21 @@ def main():
         per_call_batched = batched_rate(tc, pc_base, nc, F)
         tc.close()
 
+    # C1 (BASELINE configs[0]): the frame-0 path -- computeDists + preprocessing,
+    # AllocateSceneFromDepth and IntegrateIntoScene of the first frame, no ICP (topfu.cpp:200-207) --
+    # on a fresh context each time: wall time of the call (host sync included), median of 5 after a
+    # warm-up, beside the CPU baseline's c1_ms_per_frame on the same frame
+    c1_gpu = None
+    if rgb is None:
+        c1 = []
+        for rep in range(6):
+            t1 = TopFu(default_params(**pkw), device=local_rank)
+            device_sync()
+            ts = time.perf_counter()
+            run(t1, 0, 1)
+            c1.append(time.perf_counter() - ts)
+            t1.close()
+        c1_gpu = 1000.0 * sorted(c1[1:])[2]
     total_steps_frames = args.steps * F
     elapsed_max, total_frames = combine_ranks(elapsed, total_steps_frames, device, world)
 
@@ -701,7 +731,8 @@ def main():
             cpu = cpu_baseline_protocol(frames, first, pkw, args.cpu_seconds, nt)
         out = {
             "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame"
-                      + (" (swapping scene)" if args.swapping else ""),
+                      + (" (swapping scene)" if args.swapping else "")
+                      + (" (depth+colour stream, Voxel_s_rgb)" if args.colour else ""),
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -725,6 +756,15 @@ def main():
                        "swapping": (f"on: GlobalCache in HBM, <= {args.swap_transfer_blocks} blocks per direction "
                                     "per frame") if args.swapping else "off (topfu.cpp:67)"},
             "ms_per_frame": round(elapsed_max / total_steps_frames * 1000.0, 5),
+            "c1": None if c1_gpu is None else {
+                "gpu_ms_per_frame": round(c1_gpu, 4),
+                "cpu_ms_per_frame": cpu["c1_ms_per_frame"] if cpu else None,
+                "cpu_single_thread_ms_per_frame": cpu["single_thread"]["c1_ms_per_frame"] if cpu else None,
+                "is": "BASELINE configs[0]: the frame-0 path (preprocessing + AllocateSceneFromDepth + IntegrateIntoScene, "
+                      "no ICP; topfu.cpp:200-207) of the stream's first frame on a fresh context; GPU: wall time of the "
+                      "call with its host sync, median of 5 after a warm-up; CPU: the oracle on the same frame"},
+            "colour": ("on: Voxel_s_rgb, the colour camera registered with the depth one, GPU-rendered colour stream "
+                       "(synth/tf_synth.hip k_render_room_rgb); computeUpdatedVoxelColorInfo in every integration") if args.colour else None,
             "per_call_frames_per_sec": None if per_call is None else round(per_call, 2),
             "per_call_batched_same_frames": None if per_call_batched is None else round(per_call_batched, 2),
             "per_call": (f"TopFu::operator() per call: tf_process_frame on the timed region's first {nc} frames from a "
@@ -766,6 +806,8 @@ def main():
         print(json.dumps(out))
     tf.close()
     dev.free()
+    if rgb is not None:
+        rgb.free()
     if world > 1:
         dist.destroy_process_group()
 

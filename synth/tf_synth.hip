@@ -168,7 +168,74 @@ __global__ void __launch_bounds__(256) k_render_room(RoomArgs a)
     *(uint16_t*)((char*)a.out + (size_t)f * a.stride + ((size_t)y * a.W + x) * 2) = (uint16_t)r;
 }
 
+// synth.render_colour: the colour camera's view of the room (uchar4, alpha 255, black where no
+// surface is hit) -- the RGB stream of the colour TSDF lines.  Not bit-identical with numpy (sin /
+// cos of the device's libm): only the GPU renders it, and the parity tests feed both sides the
+// same downloaded images.
+__global__ void __launch_bounds__(256) k_render_room_rgb(RoomArgs a, uchar4* out)
+{
+    __shared__ double P[12];
+    const int f = blockIdx.z;
+    if (threadIdx.x < 12) P[threadIdx.x] = a.poses[12 * (size_t)f + threadIdx.x];
+    __syncthreads();
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.W || y >= a.H) return;
+    const double o[3] = { P[9], P[10], P[11] };
+    const double xc = ((double)x - a.cx) / a.fx, yc = ((double)y - a.cy) / a.fy;
+    const double d[3] = { (P[0] * xc + P[1] * yc) + P[2], (P[3] * xc + P[4] * yc) + P[5], (P[6] * xc + P[7] * yc) + P[8] };
+    const int ax[6] = { 2, 1, 0, 0, 1, 2 };
+    const double off[6] = { 1.8, 0.6, -0.8, 1.1, -0.9, -0.6 };
+    double best = INFINITY;
+    for (int k = 0; k < 6; ++k) {
+        const double tt = (off[k] - o[ax[k]]) / d[ax[k]];
+        best = fmin(best, (tt > 1e-6) ? tt : INFINITY);
+    }
+    if (a.sphere) {
+        const double oc[3] = { o[0] - 0.15, o[1] - 0.25, o[2] - 1.3 };
+        const double b = (d[0] * oc[0] + d[1] * oc[1]) + d[2] * oc[2];
+        const double aa = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+        const double cc = ((oc[0] * oc[0] + oc[1] * oc[1]) + oc[2] * oc[2]) - 0.09;
+        const double disc = b * b - aa * cc;
+        const double t0 = (-b - sqrt(fmax(disc, 0.0))) / aa;
+        best = fmin(best, (disc >= 0 && t0 > 1e-6) ? t0 : INFINITY);
+    }
+    uchar4 c = make_uchar4(0, 0, 0, 0);
+    if (isfinite(best)) {
+        const double p[3] = { o[0] + d[0] * best, o[1] + d[1] * best, o[2] + d[2] * best };
+        const double tp = 6.283185307179586;
+        c.x = (unsigned char)rint(127.5 + 120.0 * sin(tp * p[0] / 0.13));
+        c.y = (unsigned char)rint(127.5 + 120.0 * sin(tp * (p[1] + p[2]) / 0.17));
+        c.z = (unsigned char)rint(127.5 + 120.0 * cos(tp * (p[2] - p[0]) / 0.23));
+        c.w = 255;
+    }
+    *(uchar4*)((char*)out + (size_t)f * a.stride + ((size_t)y * a.W + x) * 4) = c;
+}
+
 extern "C" {
+
+// frames first..first+n-1 of the colour camera's view of the room (uchar4), the RGB stream of the
+// colour TSDF lines; stride in bytes (>= W * H * 4).  Synchronous.  0 = ok.
+int tfs_render_room_rgb(uchar4* dev_out, size_t stride, const double* poses, int n, int W, int H,
+                        double fx, double fy, double cx, double cy, int sphere)
+{
+    if (!dev_out || !poses || n < 0 || W <= 0 || H <= 0 || stride < (size_t)W * H * 4) return 1;
+    const int B = 256;
+    double* dp = nullptr;
+    if (hipMalloc((void**)&dp, sizeof(double) * 12 * (size_t)(n < B ? n : B) + 16) != hipSuccess) return 2;
+    int rc = 0;
+    for (int f0 = 0; f0 < n && !rc; f0 += B) {
+        const int nb = n - f0 < B ? n - f0 : B;
+        if (hipMemcpy(dp, poses + 12 * (size_t)f0, sizeof(double) * 12 * nb, hipMemcpyHostToDevice) != hipSuccess) { rc = 3; break; }
+        RoomArgs a;
+        a.out = nullptr; a.stride = stride; a.poses = dp; a.first = f0; a.W = W; a.H = H; a.sphere = sphere;
+        a.fx = fx; a.fy = fy; a.cx = cx; a.cy = cy; a.noise_mm = 0; a.seed = 0;
+        hipLaunchKernelGGL(k_render_room_rgb, dim3((W + 15) / 16, (H + 15) / 16, nb), dim3(256), 0, 0, a,
+                           (uchar4*)((char*)dev_out + (size_t)f0 * stride));
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = 4;
+    }
+    (void)hipFree(dp);
+    return rc;
+}
 
 // frames first..first+n-1 of the room at the host poses [n][12] (camera -> world), as
 // tfs_render_hall; sphere: render_depth's sphere in the room.  Synchronous.  0 = ok.

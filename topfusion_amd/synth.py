@@ -470,13 +470,14 @@ def synth_lib():
         P, S, I, D = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_double
         L.tfs_render_hall.argtypes = [P, S, P, I, I, I, I, D, D, D, D, ctypes.c_uint, D]
         L.tfs_render_room.argtypes = [P, S, P, I, I, I, I, D, D, D, D, ctypes.c_uint, D, I]
+        L.tfs_render_room_rgb.argtypes = [P, S, P, I, I, I, D, D, D, D, I]
         L.tfs_copy_gbs.argtypes = [S, I]
         L.tfs_copy_gbs.restype = D
         L.tfs_malloc.argtypes = [ctypes.POINTER(P), S]
         L.tfs_free.argtypes = [P]
         L.tfs_download.argtypes = [P, P, S]
         L.tfs_upload.argtypes = [P, P, S]
-        for f in ("tfs_render_hall", "tfs_render_room", "tfs_malloc", "tfs_free", "tfs_download", "tfs_upload", "tfs_sync"):
+        for f in ("tfs_render_hall", "tfs_render_room", "tfs_render_room_rgb", "tfs_malloc", "tfs_free", "tfs_download", "tfs_upload", "tfs_sync"):
             getattr(L, f).restype = I
         _synth = L
     return _synth
@@ -620,3 +621,23 @@ def hall_device(n, cols=640, rows=480, seed=13, noise_mm=1.0):
         b1 = min(n, b0 + 1024)
         render_hall_device(s, R[b0:b1], t[b0:b1], first=b0, seed=seed, noise_mm=noise_mm, k0=b0)
     return s, R, t
+
+
+def orbit_colour_device(n, cols=640, rows=480):
+    """The colour camera's view (registered with the depth camera) of the first n orbit frames,
+    rendered on the GPU (synth/tf_synth.hip k_render_room_rgb): uchar4 frames in one device
+    allocation; returns (DeviceStream-like buffer, its device address)."""
+    import ctypes
+    R = np.empty((n, 3, 3))
+    t = np.empty((n, 3))
+    for k in range(n):
+        R[k], t[k] = orbit_pose(k)
+    P = np.zeros((n, 12), np.float64)
+    P[:, :9] = R.reshape(n, 9)
+    P[:, 9:] = t
+    buf = DeviceStream(2 * n, cols, rows)              # 4 bytes per pixel = two uint16 frames' worth
+    fx, fy, cx, cy = intrinsics(cols, rows)
+    rc = synth_lib().tfs_render_room_rgb(ctypes.c_void_p(buf.ptr), cols * rows * 4, P.ctypes.data_as(ctypes.c_void_p), n,
+                                         cols, rows, fx, fy, cx, cy, 1)
+    assert rc == 0, f"tfs_render_room_rgb: {rc}"
+    return buf
