@@ -29,11 +29,12 @@ for i in range(its):
     pub = (tl[i, NW:2 * NW] - t0) / 100.0
     g = (tl[i, 2 * NW] - t0) / 100.0
     tail = (tl[i, 2 * NW + 1] - t0) / 100.0
-    ph = [(tl[i, 2 * NW + k] - t0) / 100.0 for k in (2, 3, 4, 5)]
+    ph = [(tl[i, 2 * NW + k] - t0) / 100.0 for k in (6, 2, 3, 7, 4, 5)]
     nxt = (tl[i + 1, :NW] - t0) / 100.0 if i + 1 < its else None
     line = (f"it {i:2d}: start[min/med/max] {st.min():5.2f}/{np.median(st):5.2f}/{st.max():5.2f} "
             f"pub {pub.min():5.2f}/{np.median(pub):5.2f}/{pub.max():5.2f} (max wg {int(pub.argmax())}) "
-            f"wg0 pub {pub[0]:5.2f} gathered {g:5.2f} [tree {ph[0]:5.2f} solve {ph[1]:5.2f} rod+comp {ph[2]:5.2f} det {ph[3]:5.2f}] tail {tail:5.2f}")
+            f"wg0 pub {pub[0]:5.2f} gathered {g:5.2f} [tree+readlane {ph[0]:5.2f} unpack {ph[1]:5.2f} solve {ph[2]:5.2f} "
+            f"rodrigues {ph[3]:5.2f} compose {ph[4]:5.2f} det {ph[5]:5.2f}] tail {tail:5.2f}")
     if nxt is not None:
         line += f" next-start {nxt.min():5.2f}/{np.median(nxt):5.2f}/{nxt.max():5.2f}"
     print(line)

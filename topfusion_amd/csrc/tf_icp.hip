@@ -38,7 +38,12 @@ extern "C" int tf_debug_icp_ts(unsigned long long* out)
 #define IPT_STRIDE (2 * ICP_NWG + 8)
 __device__ unsigned long long g_icp_tl[64 * IPT_STRIDE];
 #define IPT_REC(it, slot) IPT_REC_T(it, slot, 0)
-#define IPT_REC_T(it, slot, t) do { if (threadIdx.x == (t) && (it) < 64) g_icp_tl[(it) * IPT_STRIDE + (slot)] = IPT_NOW(); } while (0)
+// the stamp is fenced against the scheduler (no instruction moves across it) and issued after the
+// VALU work before it has been issued; the data it measures lives in registers, so the segment
+// between two stamps is that segment's issue time
+#define IPT_REC_T(it, slot, t) do { __builtin_amdgcn_sched_barrier(0); \
+    if (threadIdx.x == (t) && (it) < 64) g_icp_tl[(it) * IPT_STRIDE + (slot)] = IPT_NOW(); \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
 extern "C" int tf_debug_icp_timeline(unsigned long long* out)
 {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_tl), sizeof(g_icp_tl), 0, hipMemcpyDeviceToHost);
@@ -789,6 +794,7 @@ k_icp_frame(IcpFrameArgs a)
 #pragma unroll
                     for (int q = 0; q < 27; ++q)
                         sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), q));
+                    IPT_REC(done, 2 * ICP_NWG + 6);
                     ip_unpack(sm, Am, bv);
                     IPT_REC(done, 2 * ICP_NWG + 2);
                     if (wave == IP_DETW) {                             // det after the barrier
@@ -799,6 +805,7 @@ k_icp_frame(IcpFrameArgs a)
                         icp_solve6_ldl(Am, bv, rv);                     // projective_icp.cpp:206-209
                         IPT_REC(done, 2 * ICP_NWG + 3);
                         icp_rodrigues(rv, R);
+                        IPT_REC(done, 2 * ICP_NWG + 7);
 #pragma unroll
                         for (int j = 0; j < 3; ++j) {
                             tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1];
