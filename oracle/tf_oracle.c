@@ -191,7 +191,41 @@ void tfo_rigid_inv(const float a[12], float out[12])
 }
 
 /* cv::Affine3f(rvec, t) rotation part: Rodrigues in double */
+/* Affine3f(rvec, t)'s rotation (cv::Affine3::rotation(const Vec3&), OpenCV affine.hpp; OpenCV is
+   absent here: parity unpinned).  R = cos t I + ((1 - cos t) / t^2) r r^T + (sin t / t) [r]x with
+   r = rvec unnormalised -- the same matrix as cv's c I + (1 - c) u u^T + s [u]x with u = r / t --
+   and the three even functions of t as nested polynomials in t^2 with fma (the coefficients of
+   tfo_sincos; 2 (1 - cos t) / t^2 = 1 - t^2/12 (1 - t^2/30 (...))).  No square root, no division:
+   the GPU's serial ICP tail evaluates exactly this (tf_icp_tail.h icp_rodrigues).  t > pi (never
+   for an ICP increment) uses rodrigues_sqrt, the direct form with tfo_sincos' range reduction. */
+static void rodrigues_sqrt(const float r[3], float R[9]);
+static const double k_inv_cos15 = 1.0 / 756.0;
 void tfo_rodrigues(const float r[3], float R[9])
+{
+    const double rx = r[0], ry = r[1], rz = r[2];
+    const double t2 = (rx * rx + ry * ry) + rz * rz;
+    if (t2 < DBL_EPSILON * DBL_EPSILON) {
+        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+        return;
+    }
+    if (t2 > 9.869604401089358) { rodrigues_sqrt(r, R); return; }
+    double pc = 1.0, pa = 1.0, pb = 1.0;
+    const int nt = t2 < 0.015625 ? 6 : 13;
+    for (int n = nt; n >= 1; --n) {
+        pc = fma(-(t2 * k_inv_cos[n]), pc, 1.0);
+        pa = fma(-(t2 * k_inv_sin[n]), pa, 1.0);
+        pb = fma(-(t2 * (n + 1 < 14 ? k_inv_cos[n + 1] : k_inv_cos15)), pb, 1.0);
+    }
+    const double b = 0.5 * pb;
+    const double rrt[9] = { rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz };
+    const double rxm[9] = { 0, -rz, ry, rz, 0, -rx, -ry, rx, 0 };
+    for (int k = 0; k < 9; ++k) {
+        const double I = (k % 4 == 0) ? 1.0 : 0.0;
+        R[k] = (float)((pc * I + b * rrt[k]) + pa * rxm[k]);
+    }
+}
+
+static void rodrigues_sqrt(const float r[3], float R[9])
 {
     double rx = r[0], ry = r[1], rz = r[2];
     double theta = sqrt((rx * rx + ry * ry) + rz * rz);

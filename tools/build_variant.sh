@@ -8,7 +8,7 @@ mkdir -p $O
 cd $R/topfusion_amd/csrc
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero"
 objs=""
-for f in tf_preproc tf_icp tf_scene tf_render tf_capi tf_imgproc tf_swap; do
+for f in tf_preproc tf_icp tf_scene tf_render tf_capi tf_imgproc tf_swap tf_fuse; do
   /opt/rocm/bin/hipcc $FL "$@" -c $f.hip -o $O/$f.o &
   objs="$objs $O/$f.o"
 done
