@@ -211,26 +211,12 @@ __host__ __device__ __forceinline__ bool tf_grid_in(int bx, int by, int bz)
     return ((unsigned)(bx + TF_GRID_HALF) | (unsigned)(by + TF_GRID_HALF) | (unsigned)(bz + TF_GRID_HALF)) <
            (unsigned)TF_GRID_DIM;
 }
-// Cell layout: bricks of 2 x 2 x 4 cells (x, y, z) -- 16 cells of 8 B, one 128-byte cache line --
-// so a ray's successive blocks along z and a 2x2x2 corner set share lines (a row-major grid put
-// z-neighbours 512 KiB apart).  The index is a sum of one term per axis (tf_grid_px/py/pz of the
-// shifted coordinate), so a 2x2x2 set is 6 terms and 8 adds.  TF_GRID_BRICK=0: row-major (A/B).
-#ifndef TF_GRID_BRICK
-#define TF_GRID_BRICK 1
-#endif
-#if TF_GRID_BRICK
-__host__ __device__ __forceinline__ unsigned tf_grid_px(unsigned x) { return ((x >> 1) << 4) | (x & 1u); }
-__host__ __device__ __forceinline__ unsigned tf_grid_py(unsigned y) { return ((y >> 1) << 11) | ((y & 1u) << 1); }
-__host__ __device__ __forceinline__ unsigned tf_grid_pz(unsigned z) { return ((z >> 2) << 18) | ((z & 3u) << 2); }
-#else
-__host__ __device__ __forceinline__ unsigned tf_grid_px(unsigned x) { return x; }
-__host__ __device__ __forceinline__ unsigned tf_grid_py(unsigned y) { return y << TF_GRID_LOG; }
-__host__ __device__ __forceinline__ unsigned tf_grid_pz(unsigned z) { return z << (2 * TF_GRID_LOG); }
-#endif
+// (row-major: a layout in 2 x 2 x 4-cell bricks, one 128-byte line each, measured 4 us slower on
+// the raycast pair in round 4 -- DESIGN §8)
 __host__ __device__ __forceinline__ size_t tf_grid_cell(int bx, int by, int bz)
 {
-    return (size_t)(tf_grid_px((unsigned)(bx + TF_GRID_HALF)) + tf_grid_py((unsigned)(by + TF_GRID_HALF)) +
-                    tf_grid_pz((unsigned)(bz + TF_GRID_HALF)));
+    return ((size_t)(bz + TF_GRID_HALF) << (2 * TF_GRID_LOG)) | ((size_t)(by + TF_GRID_HALF) << TF_GRID_LOG) |
+           (size_t)(bx + TF_GRID_HALF);
 }
 
 // the cell of a block the hash now holds (allocation, reallocation after a swap-out)

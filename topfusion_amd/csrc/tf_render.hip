@@ -66,11 +66,10 @@ __device__ __forceinline__ bool blk_offsets8(const int (&X)[2], const int (&Y)[2
 {
     const unsigned x0 = (unsigned)(X[0] + TF_GRID_HALF), y0 = (unsigned)(Y[0] + TF_GRID_HALF), z0 = (unsigned)(Z[0] + TF_GRID_HALF);
     const unsigned x1 = (unsigned)(X[1] + TF_GRID_HALF), y1 = (unsigned)(Y[1] + TF_GRID_HALF), z1 = (unsigned)(Z[1] + TF_GRID_HALF);
-    const unsigned px0 = tf_grid_px(x0) * 8u, px1 = tf_grid_px(x1) * 8u;
-    const unsigned py0 = tf_grid_py(y0) * 8u, py1 = tf_grid_py(y1) * 8u;
-    const unsigned pz0 = tf_grid_pz(z0) * 8u, pz1 = tf_grid_pz(z1) * 8u;
-    o[0] = px0 + py0 + pz0; o[1] = px1 + py0 + pz0; o[2] = px0 + py1 + pz0; o[3] = px1 + py1 + pz0;
-    o[4] = o[0] - pz0 + pz1; o[5] = o[1] - pz0 + pz1; o[6] = o[2] - pz0 + pz1; o[7] = o[3] - pz0 + pz1;
+    const unsigned base = ((z0 << (2 * TF_GRID_LOG)) | (y0 << TF_GRID_LOG) | x0) * 8u;
+    const unsigned dx = (x1 - x0) * 8u, dy = (y1 - y0) << (TF_GRID_LOG + 3), dz = (z1 - z0) << (2 * TF_GRID_LOG + 3);
+    o[0] = base; o[1] = base + dx; o[2] = base + dy; o[3] = o[1] + dy;
+    o[4] = base + dz; o[5] = o[1] + dz; o[6] = o[2] + dz; o[7] = o[3] + dz;
     return (x0 | x1 | y0 | y1 | z0 | z1) < (unsigned)TF_GRID_DIM;
 }
 // (hash entry index, VBA voxel offset) per corner, or (-1, TF_VOFF_NONE) when findVoxel fails
