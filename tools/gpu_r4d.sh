@@ -7,7 +7,7 @@ cd $R
 TAG=${1:-r4d}; shift
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 TFUSION_HIP_LIB=tools/_build/libtfusion_hip_timing.so timeout -k 10 120 python tools/icp_timeline.py > $O/icp_timeline.txt 2>&1 \
   || { tail -20 $O/icp_timeline.txt; exit 1; }
@@ -15,11 +15,11 @@ tail -3 $O/icp_timeline.txt | cut -c1-250
 for round in 1 2; do
   for v in tree "$@"; do
     if [ $v = tree ]; then L=$PWD/topfusion_amd/libtfusion_hip.so; else L=$PWD/tools/_build/$v/libtfusion_hip.so; fi
-    TFUSION_HIP_LIB=$L timeout -k 10 200 python bench.py --no-cpu-baseline --per-call-frames 0 > $O/ab_$v_$round.log 2>&1 \
-      || { tail -20 $O/ab_$v_$round.log; exit 1; }
+    TFUSION_HIP_LIB=$L timeout -k 10 200 python bench.py --no-cpu-baseline --per-call-frames 0 > $O/ab_${v}_$round.log 2>&1 \
+      || { tail -20 $O/ab_${v}_$round.log; exit 1; }
     python -c "
 import json
-e=json.loads(open('$O/ab_$v_$round.log').read().strip().splitlines()[-1])
+e=json.loads(open('$O/ab_${v}_$round.log').read().strip().splitlines()[-1])
 print('$v', 'C2 fps', e['value'], {k: v for k, v in e['stage_ms_per_frame'].items() if v})"
   done
 done

@@ -1309,6 +1309,18 @@ __device__ __forceinline__ void ed_tile_range(const EdArgs& a, int X0, int Y0, i
     __syncthreads();
 }
 
+#ifdef TF_PAIR_TIMELINE
+// diagnostic builds only (tools/pair_timeline.py): per workgroup of the last k_raycast_pair
+// launch, [start, end of wave 0..3, end, kind | xcc << 8 | cu << 16] on the 100 MHz clock
+#define PTL_MAX 8192
+__device__ unsigned long long tf_pair_tl[PTL_MAX * 7];
+extern "C" int tf_debug_pair_timeline(void* host, size_t bytes)
+{
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tf_pair_tl), bytes < sizeof(tf_pair_tl) ? bytes : sizeof(tf_pair_tl), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
+
 // every branch's LDS overlaid: the kernel keeps the raycast's occupancy (8 workgroups per CU)
 union PairLds {
     int vtab[256 * VTAB_STRIDE];
@@ -1332,21 +1344,53 @@ union PairLds {
 // its rows to count done (the fill workgroups come first in dispatch order, and wait on nothing).
 // (8 waves per SIMD: the allocator left alone takes 70 VGPRs over the kernel's branches, each of
 // which fits 64 on its own; held to 64 it spills one 8-byte value once per thread)
+__device__ __forceinline__ int pair_body(PairLds& L, RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
+                                         int n_tiles, int nb, PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx,
+                                         EdArgs ed, int nfill, int nfill_pad);
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x, int n_tiles, int nb,
                PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx, EdArgs ed, int nfill, int nfill_pad)
 {
     __shared__ PairLds L;
+#ifdef TF_PAIR_TIMELINE
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const int kind = pair_body(L, ai, ar, st, tiles_x, n_tiles, nb, pyr, n_pyr, pyr_gx, bil, bil_gx, ed, nfill, nfill_pad);
+    const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x < PTL_MAX) {
+        unsigned long long* o = &tf_pair_tl[blockIdx.x * 7];
+        if ((threadIdx.x & 63) == 0) o[1 + (threadIdx.x >> 6)] = tw;
+        if (threadIdx.x == 0) {
+            unsigned xcc = 0, hw = 0;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            o[0] = t0; o[5] = t1;
+            o[6] = (unsigned long long)(kind & 0xff) | ((unsigned long long)(xcc & 0xf) << 8) |
+                   ((unsigned long long)((hw >> 8) & 0xf) << 16) | ((unsigned long long)((hw >> 13) & 0x7) << 20);
+        }
+    }
+#else
+    pair_body(L, ai, ar, st, tiles_x, n_tiles, nb, pyr, n_pyr, pyr_gx, bil, bil_gx, ed, nfill, nfill_pad);
+#endif
+}
+
+// the branch kind (diagnostics): 0 fill, 1 CreateICPMaps tile, 2 renderImage tile, 3 pyramid /
+// normals, 4 bilateral, 5 nothing to do
+__device__ __forceinline__ int pair_body(PairLds& L, RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
+                                         int n_tiles, int nb, PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx,
+                                         EdArgs ed, int nfill, int nfill_pad)
+{
     int b = (int)blockIdx.x;
     if (b < nfill_pad) {
         if (b < nfill) ed_fill_block<ED_PAIR_W>(ed, st, b, nfill, L.ed, false);
-        return;
+        return b < nfill ? 0 : 5;
     }
     b -= nfill_pad;
     if (b < nb) {
-        if (!raycast_go<1>(st)) return;
+        if (!raycast_go<1>(st)) return 5;
         const int tile = xcd_tile(b, n_tiles);
-        if (tile < 0) return;
+        if (tile < 0) return 5;
         const int tx = tile % tiles_x, ty = tile / tiles_x;
         const int n = st->noVisibleEntries;
         if (nfill > 0 && n <= ed.lds_max_n) {
@@ -1370,15 +1414,15 @@ k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
         }
         // (one instance of the march for both sources of the range: a second costs registers)
         raycast_tile<1, true>(ai, st, tile, tiles_x, nullptr, L.ir.rng);
-        return;
+        return 1;
     }
     b -= nb;
     if (b < nb) {
-        if (!raycast_go<2>(st)) return;
+        if (!raycast_go<2>(st)) return 5;
         const int tile = xcd_tile(b, n_tiles);
-        if (tile < 0) return;
+        if (tile < 0) return 5;
         raycast_tile<2>(ar, st, tile, tiles_x, L.vtab);
-        return;
+        return 2;
     }
     b -= nb;
     // Later frames of the batch in this grid's tail, not gated by this frame's abort: the next
@@ -1386,8 +1430,9 @@ k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
     // last readers of dists and of the current maps, are done; its level-0 depth was filtered
     // a launch or more ago), then the bilateral pass of the frame after it (into the other
     // level-0 buffer: this frame's, whose last reader was its own pyramid pass)
-    if (b < n_pyr) pyr_normals_block<256>(pyr, b % pyr_gx, b / pyr_gx, L.pn);
-    else bilateral_block<false>(bil, (b - n_pyr) % bil_gx, (b - n_pyr) / bil_gx, L.bil);
+    if (b < n_pyr) { pyr_normals_block<256>(pyr, b % pyr_gx, b / pyr_gx, L.pn); return 3; }
+    bilateral_block<false>(bil, (b - n_pyr) % bil_gx, (b - n_pyr) / bil_gx, L.bil);
+    return 4;
 }
 
 // CreateICPMaps' raycast + the frame's renderImage in one launch (after CreateExpectedDepths'
