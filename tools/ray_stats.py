@@ -1,9 +1,11 @@
 """Ray-march step statistics of the C2 bench frames (diagnostic; needs the TF_RAY_STATS build:
 bash tools/build_variant.sh raystats -DTF_RAY_STATS, run with TFUSION_HIP_LIB pointing at it).
 
-Per tracked frame: steps per ray in unallocated space (a grid lookup only) and steps that read
-voxels, for CreateICPMaps' castRay<true> and renderImage's castRay; per 64-lane wave (4 rows of a
-16x16 tile) the longest ray, which sets the wave's time."""
+Per tracked frame: steps per ray in unallocated space (a grid lookup only), steps that read
+voxels and, of those, band steps (the eight interpolation corners read too), for CreateICPMaps'
+castRay<true> and renderImage's castRay; per 64-lane wave (an 8x8 quadrant of a 16x16 tile) the
+longest ray, which sets the wave's time, and the composition of the longest waves' longest rays
+with a round-trip count (1 per free step, 2 per voxel step, 2 more per band step)."""
 import ctypes
 import json
 import os
@@ -39,17 +41,27 @@ def main():
         res = {"frame": k}
         for half, name in ((0, "icp"), (1, "render")):
             a = buf[half * 1280 * 960: half * 1280 * 960 + W * H].reshape(H, W)
-            free = (a & 0xffff).astype(np.int64)
-            found = (a >> 16).astype(np.int64)
+            free = (a & 0x3ff).astype(np.int64)
+            found = ((a >> 10) & 0x7ff).astype(np.int64)
+            band = (a >> 21).astype(np.int64)
             tot = free + found
-            # waves: 16x16 tiles, 4 rows each
-            t = tot.reshape(H // 16, 16, W // 16, 16).transpose(0, 2, 1, 3).reshape(-1, 4, 64)
-            wmax = t.max(axis=2).ravel()
-            res[name] = {"ray_free": float(free.mean()), "ray_found": float(found.mean()), "ray_total": float(tot.mean()),
+            rt = free + 2 * found + 2 * band
+
+            def waves(v):   # 8x8 quadrants: (H/8, 8, W/8, 8) -> (waves, 64)
+                return v.reshape(H // 8, 8, W // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64)
+            wt, wf, wb, wr = waves(tot), waves(free), waves(band), waves(rt)
+            wmax = wt.max(axis=1)
+            arg = wt.argmax(axis=1)
+            top = np.argsort(-wmax)[:max(1, len(wmax) // 100)]          # the longest 1 % of waves
+            lr = lambda v: v[top, arg[top]]
+            res[name] = {"ray_free": float(free.mean()), "ray_found": float(found.mean()), "ray_band": float(band.mean()),
+                         "ray_total": float(tot.mean()),
                          "wave_max_mean": float(wmax.mean()), "wave_max_p50": float(np.percentile(wmax, 50)),
                          "wave_max_p90": float(np.percentile(wmax, 90)), "wave_max_max": int(wmax.max()),
-                         "ray_total_max": int(tot.max()), "wave_free_max_mean":
-                         float((free.reshape(H // 16, 16, W // 16, 16).transpose(0, 2, 1, 3).reshape(-1, 4, 64)).max(axis=2).mean())}
+                         "wave_rt_max_mean": float(wr.max(axis=1).mean()), "wave_rt_max_max": int(wr.max()),
+                         "top1pct_ray_steps": float(lr(wt).mean()), "top1pct_ray_free": float(lr(wf).mean()),
+                         "top1pct_ray_band": float(lr(wb).mean()), "top1pct_ray_rt": float(lr(wr).mean()),
+                         "top1pct_live_lanes_at_half": float(np.mean([(wt[w] > wmax[w] // 2).sum() for w in top]))}
         rows.append(res)
         print(json.dumps(res), flush=True)
     for name in ("icp", "render"):

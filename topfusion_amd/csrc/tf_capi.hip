@@ -154,7 +154,7 @@ static void ctx_free(tf_ctx* c)
                      c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->edBins, c->edBinCnt, c->edDone, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
-                     c->vba_rgb_guard, c->rgb_in, c->integ_cnt, c->fuse_pose, c->fuse_rec };
+                     c->vba_rgb_guard, c->rgb_in, c->integ_cnt, c->fuse_pose, c->fuse_rec, c->tile_cost, c->tile_order };
     for (void* b : bufs) if (b) (void)hipFree(b);
     // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
     float4* maps[4] = { c->curr_pts[0], c->curr_nrm[0], c->prev_pts[0], c->prev_nrm[0] };
@@ -182,7 +182,7 @@ static tf_status flush_tail(tf_ctx* c, TfAhead nxt = TfAhead{}, size_t pitch = 0
 {
     if (!c->tail_pending) return TF_OK;
     c->tail_pending = 0;
-    TF_CHECK(tfk_raycast_pair(c, TfAhead{}, nxt, pitch, c->tail_fuse_ed));
+    TF_CHECK(tfk_raycast_pair(c, TfAhead{}, nxt, pitch, c->tail_fuse_ed, 1));
     TF_CHECK(tfk_icp_maps_end(c, 0, nxt, pitch));
     return TF_OK;
 }
@@ -285,6 +285,15 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (c->ed_lds_max_n > 0) ALLOC(c->edBins, sizeof(uint4) * 2 * (size_t)ed_nrows(c->H) * (size_t)c->ed_lds_max_n);
     ALLOC(c->edBinCnt, sizeof(int) * 2 * (size_t)ed_nrows(c->H));
     ALLOC(c->edDone, 64);
+    {   // the raycast tiles' dispatch order, longest first per XCD region (k_raycast_pair, sorted in
+        // k_icp_maps_end's grid from the last frame's workgroup times); TFUSION_TILE_ORDER=0: the plain
+        // XCD-swizzled order (A/B)
+        const int nt = ((c->W + 15) / 16) * ((c->H + 15) / 16), nb = (nt + 7) / 8 * 8;
+        const char* env = getenv("TFUSION_TILE_ORDER");
+        c->tile_ljf = nb / 8 <= TF_LJF_MAX && !(env && env[0] == '0');
+        ALLOC(c->tile_cost, sizeof(unsigned) * 2 * (size_t)nt);
+        ALLOC(c->tile_order, sizeof(int) * 2 * (size_t)nb);
+    }
     ALLOC(c->depth_in, sizeof(uint16_t) * npx);
     ALLOC(c->dists, sizeof(float) * npx);
     {   // each map's three pyramid levels are contiguous in one allocation
@@ -375,6 +384,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipMemsetAsync(c->raycast, 0, sizeof(float) * 4 * npx, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->edBinCnt, 0, sizeof(int) * 2 * (size_t)ed_nrows(c->H), c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->edDone, 0, 64, c->stream);
+    if (e == hipSuccess) e = tfk_tile_order_init(c);
     if (e == hipSuccess) e = hipMemsetAsync(c->grey, 0, sizeof(uchar4) * npx, c->stream);
     for (int l = 0; l < TF_LEVELS && e == hipSuccess; ++l) {
         size_t n = (size_t)c->lw[l] * c->lh[l];
@@ -580,7 +590,7 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
         return TF_OK;
     }
     // CreateICPMaps' raycast + renderImage (topfu.cpp:284-285 + 307) in one launch (snapshot range)
-    STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch, fuse_ed));
+    STAGE(TF_STAGE_RAYCAST_ICP, tfk_raycast_pair(c, plan->pair_pyr, plan->pair_bil, pitch, fuse_ed, 1));
     // renderICP + resizePointsNormals (topfu.cpp:308-309) + the frame end (topfu.cpp:263-264)
     STAGE(TF_STAGE_ICP_MAPS, tfk_icp_maps_end(c, slot));
     return TF_OK;

@@ -307,6 +307,11 @@ struct tf_ctx {
     uint4* edBins;           // k_ed_fill's per-row bins of boxes (tf_ed.h EdArgs::bins)
     int* edBinCnt;
     unsigned* edDone;        // the fused fill's atomic path: rows done (k_raycast_pair)
+    // k_raycast_pair's frame path: per CreateICPMaps / renderImage tile the time its workgroup took in
+    // the last launch, and the dispatch order that sorts each XCD's tiles longest first (TF_LJF_MAX)
+    unsigned* tile_cost;
+    int* tile_order;
+    int tile_ljf;
     int2* edSpill;           // per k_ed_fill row (ed_nrows): extent [0,x) x [0,y) of the pixels k_ed_fill wrote outside
                              // the /8 region (cleared by the next projection pass)
     int ed_lds_max_n;        // k_ed_fill reduces in LDS per /8 row up to this many visible entries
@@ -442,7 +447,10 @@ hipError_t tfk_render_type(tf_ctx* c, int type);   // RenderImage pixel stage (t
 // CreateICPMaps raycast + renderImage, one launch (frame path); next: + that frame's dists/pyramid/normals
 // + dists/pyramid/normals of pyr, bilateral of bil; fuse_ed: CreateExpectedDepths' fill in the same
 // grid (frame path, when tfk_ed_fused: then no separate tfk_expected_depths launch)
-hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = TfAhead{}, size_t pitch = 0, int fuse_ed = 0);
+hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = TfAhead{}, size_t pitch = 0, int fuse_ed = 0,
+                            int ljf = 0);
+#define TF_LJF_MAX 1024          // tiles per XCD region the longest-first ordering sorts (one LDS sort)
+hipError_t tfk_tile_order_init(tf_ctx* c);   // the XCD-swizzled order, zero costs
 int tfk_ed_fused(const tf_ctx* c);
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_render_snapshot(tf_ctx* c);   // render_snapshot as its own launch

@@ -305,8 +305,9 @@ __device__ __forceinline__ bool ray_refine(const RayArgs& a, Ray& R)
     return true;
 }
 #ifdef TF_RAY_STATS
-// diagnostic builds only (tools/ray_stats.py): per ray, steps in unallocated space (low 16 bits)
-// and steps that read voxels (high 16 bits), for the two raycasts of the last pair launch
+// diagnostic builds only (tools/ray_stats.py): per ray, steps in unallocated space (bits 0-9),
+// steps that read voxels (bits 10-20) and of those the band steps that also read the eight
+// interpolation corners (bits 21-31), for the two raycasts of the last pair launch
 __device__ unsigned tf_ray_stats_buf[2 * 1280 * 960];
 extern "C" int tf_debug_ray_stats(void* host, size_t bytes)
 {
@@ -372,7 +373,7 @@ __device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* i
     ray_init(a, invM, x, y, vf, R);
     const float stepScale = a.mu * a.oneOverVoxelSize;
 #ifdef TF_RAY_STATS
-    unsigned n_free = 0, n_found = 0;
+    unsigned n_free = 0, n_found = 0, n_band = 0;
 #endif
     while (R.active) {
         const int rx = tf_round(R.pt[0]), ry = tf_round(R.pt[1]), rz = tf_round(R.pt[2]);
@@ -397,7 +398,12 @@ __device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* i
         if (!vmIndex) {
             stepLength = (float)TF_BLK;
         } else {
-            if ((sdfValue <= 0.1f) && (sdfValue >= -0.5f)) sdfValue = interp_at(a.s, R.pt, &R.k, nullptr);
+            if ((sdfValue <= 0.1f) && (sdfValue >= -0.5f)) {
+#ifdef TF_RAY_STATS
+                ++n_band;
+#endif
+                sdfValue = interp_at(a.s, R.pt, &R.k, nullptr);
+            }
             if (sdfValue <= 0.0f) { R.sdfValue = sdfValue; R.active = false; continue; }   // the loop's break
             const float qq = sdfValue * stepScale;
             stepLength = (qq < 1.0f) ? 1.0f : qq;
@@ -408,7 +414,8 @@ __device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* i
         R.active = R.totalLength < R.totalLengthMax;
     }
 #ifdef TF_RAY_STATS
-    if (x + y * a.W < 1280 * 960) tf_ray_stats_buf[(MARK ? 0 : 1280 * 960) + x + y * a.W] = n_free | (n_found << 16);
+    if (x + y * a.W < 1280 * 960)
+        tf_ray_stats_buf[(MARK ? 0 : 1280 * 960) + x + y * a.W] = min(n_free, 1023u) | (min(n_found, 2047u) << 10) | (min(n_band, 2047u) << 21);
 #endif
     float w = 0.0f;
     if (ray_refine(a, R)) {                 // ray_finish on interp_at's confidence read
@@ -923,14 +930,65 @@ k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
 // pass in the grid's last workgroups -- it writes only the current maps, the level 1-2 depths and
 // dists, which nothing of this frame reads any more, and its level-0 depth came from the
 // bilateral pass in this frame's k_raycast_pair.
-__global__ void __launch_bounds__(256)
-k_icp_maps_end(IcpMapArgs a, ResetArgs r, int gx, int nmaps, PyrArgs pyr, int pyr_gx)
+// Longest-first dispatch order of the next frame's raycast tiles (k_raycast_pair's frame path).
+// The pair kernel's run time is its longest workgroups' -- tiles whose rays graze a surface
+// inside its truncation band take ~45 us against a median ~20 us -- and a launch holds more
+// workgroups than the chip does at once, so a long tile dispatched late ends late
+// (tools/pair_timeline.py).  Tile costs are this frame's workgroup times; the camera moves little
+// per frame.  Workgroup b of a half runs on XCD b % 8 as its (b / 8)-th tile: each XCD keeps its
+// band of consecutive image tiles (xcd_tile: the L2 locality of the voxels its rays read), sorted
+// by cost, longest first.  Only the schedule changes: every tile computes the same values.
+struct TileSortArgs {
+    const unsigned* cost;    // [2][n]
+    int* order;              // [2][nb]
+    int n, nb;               // tiles, padded dispatch slots per half
+};
+// one XCD region of one half: rank sort (each key's rank = the keys above it; keys are distinct,
+// the tile index rides in the low bits), a few hundred LDS broadcast reads per thread
+__device__ __forceinline__ void tile_sort_block(const TileSortArgs& a, int s, unsigned* keys)
 {
-    __shared__ PnLds pn;
-    const int b = blockIdx.x;
-    if (b < nmaps) icp_maps_block(a, r.st, b % gx, b / gx);
+    const int h = s >> 3, x = s & 7, per = a.nb >> 3, lo = x * per;
+    const int cnt = max(0, min(per, a.n - lo));
+    for (int i = threadIdx.x; i < cnt; i += 256)
+        keys[i] = (min(a.cost[h * a.n + lo + i], 0xfffffu) << 12) | (unsigned)i;
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += 256) {
+        const unsigned ki = keys[i];
+        int rank = 0;
+        for (int j = 0; j < cnt; ++j) rank += keys[j] > ki ? 1 : 0;
+        a.order[h * a.nb + rank * 8 + x] = lo + i;               // longest first
+    }
+    for (int k = cnt + threadIdx.x; k < per; k += 256) a.order[h * a.nb + k * 8 + x] = -1;
+}
+
+// the sort's 16 workgroups first (done long before the maps pass), then CreateICPMaps' tiles, the
+// frame end and the per-call lookahead
+__global__ void __launch_bounds__(256)
+k_icp_maps_end(IcpMapArgs a, ResetArgs r, int gx, int nmaps, PyrArgs pyr, int pyr_gx, int n_sort, TileSortArgs ts)
+{
+    __shared__ union { PnLds pn; unsigned keys[TF_LJF_MAX]; } L;
+    const int b = (int)blockIdx.x - n_sort;
+    if (b < 0) tile_sort_block(ts, (int)blockIdx.x, L.keys);
+    else if (b < nmaps) icp_maps_block(a, r.st, b % gx, b / gx);
     else if (b < nmaps + TF_END_BLOCKS) reset_scene_block(r, b - nmaps, TF_END_BLOCKS);
-    else pyr_normals_block<256>(pyr, (b - nmaps - TF_END_BLOCKS) % pyr_gx, (b - nmaps - TF_END_BLOCKS) / pyr_gx, pn);
+    else pyr_normals_block<256>(pyr, (b - nmaps - TF_END_BLOCKS) % pyr_gx, (b - nmaps - TF_END_BLOCKS) / pyr_gx, L.pn);
+}
+
+// the XCD-swizzled order (xcd_tile) and zero costs: a new context's first frames
+hipError_t tfk_tile_order_init(tf_ctx* c)
+{
+    const int n = ((c->W + 15) / 16) * ((c->H + 15) / 16), nb = (n + 7) / 8 * 8;
+    int* o = (int*)malloc(sizeof(int) * 2 * (size_t)nb);
+    if (!o) return hipErrorOutOfMemory;
+    const int per = nb / 8;
+    for (int b = 0; b < nb; ++b) {
+        const int t = (b % 8) * per + b / 8;
+        o[b] = o[nb + b] = t < n ? t : -1;
+    }
+    hipError_t e = hipMemcpy(c->tile_order, o, sizeof(int) * 2 * (size_t)nb, hipMemcpyHostToDevice);
+    free(o);
+    if (e == hipSuccess) e = hipMemsetAsync(c->tile_cost, 0, sizeof(unsigned) * 2 * (size_t)n, c->stream);
+    return e;
 }
 
 hipError_t tfk_icp_maps(tf_ctx* c)
@@ -961,7 +1019,15 @@ hipError_t tfk_icp_maps_end(tf_ctx* c, int slot, TfAhead pyr, size_t pitch)
         pyr_gx = tf_div_up(c->W, PN_T0);
         n_pyr = pyr_gx * tf_div_up(c->H, PN_T0);
     }
-    tf_launch(c, k_icp_maps_end, dim3(nmaps + TF_END_BLOCKS + n_pyr), dim3(256), 0, a, r, gx, nmaps, pp, pyr_gx);
+    TileSortArgs ts = TileSortArgs{};
+    int n_sort = 0;
+    if (c->tile_ljf) {                   // 2 halves x 8 XCD regions
+        ts.cost = c->tile_cost; ts.order = c->tile_order;
+        ts.n = ((c->W + 15) / 16) * ((c->H + 15) / 16); ts.nb = (ts.n + 7) / 8 * 8;
+        n_sort = 16;
+    }
+    tf_launch(c, k_icp_maps_end, dim3(n_sort + nmaps + TF_END_BLOCKS + n_pyr), dim3(256), 0, a, r, gx, nmaps, pp, pyr_gx,
+              n_sort, ts);
     return hipGetLastError();
 }
 
@@ -1346,15 +1412,17 @@ union PairLds {
 // which fits 64 on its own; held to 64 it spills one 8-byte value once per thread)
 __device__ __forceinline__ int pair_body(PairLds& L, RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
                                          int n_tiles, int nb, PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx,
-                                         EdArgs ed, int nfill, int nfill_pad);
+                                         EdArgs ed, int nfill, int nfill_pad, const int* __restrict__ order,
+                                         unsigned* __restrict__ cost);
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x, int n_tiles, int nb,
-               PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx, EdArgs ed, int nfill, int nfill_pad)
+               PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx, EdArgs ed, int nfill, int nfill_pad,
+               const int* __restrict__ order, unsigned* __restrict__ cost)
 {
     __shared__ PairLds L;
 #ifdef TF_PAIR_TIMELINE
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    const int kind = pair_body(L, ai, ar, st, tiles_x, n_tiles, nb, pyr, n_pyr, pyr_gx, bil, bil_gx, ed, nfill, nfill_pad);
+    const int kind = pair_body(L, ai, ar, st, tiles_x, n_tiles, nb, pyr, n_pyr, pyr_gx, bil, bil_gx, ed, nfill, nfill_pad, order, cost);
     const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
@@ -1371,16 +1439,25 @@ k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
         }
     }
 #else
-    pair_body(L, ai, ar, st, tiles_x, n_tiles, nb, pyr, n_pyr, pyr_gx, bil, bil_gx, ed, nfill, nfill_pad);
+    pair_body(L, ai, ar, st, tiles_x, n_tiles, nb, pyr, n_pyr, pyr_gx, bil, bil_gx, ed, nfill, nfill_pad, order, cost);
 #endif
 }
 
 // the branch kind (diagnostics): 0 fill, 1 CreateICPMaps tile, 2 renderImage tile, 3 pyramid /
 // normals, 4 bilateral, 5 nothing to do
+// the ray tiles' workgroup time, for the next frame's longest-first order (tf_ctx::tile_order)
+__device__ __forceinline__ void pair_tile_cost(unsigned* cost, int slot, unsigned long long t0)
+{
+    if (!cost) return;
+    __syncthreads();                 // (the workgroup's LDS is held until its last wave anyway)
+    if (threadIdx.x == 0) cost[slot] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - t0, 0xffffeull);
+}
 __device__ __forceinline__ int pair_body(PairLds& L, RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
                                          int n_tiles, int nb, PyrArgs pyr, int n_pyr, int pyr_gx, BilArgs bil, int bil_gx,
-                                         EdArgs ed, int nfill, int nfill_pad)
+                                         EdArgs ed, int nfill, int nfill_pad, const int* __restrict__ order,
+                                         unsigned* __restrict__ cost)
 {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     int b = (int)blockIdx.x;
     if (b < nfill_pad) {
         if (b < nfill) ed_fill_block<ED_PAIR_W>(ed, st, b, nfill, L.ed, false);
@@ -1389,7 +1466,7 @@ __device__ __forceinline__ int pair_body(PairLds& L, RayArgs ai, RayArgs ar, TfD
     b -= nfill_pad;
     if (b < nb) {
         if (!raycast_go<1>(st)) return 5;
-        const int tile = xcd_tile(b, n_tiles);
+        const int tile = order ? order[b] : xcd_tile(b, n_tiles);
         if (tile < 0) return 5;
         const int tx = tile % tiles_x, ty = tile / tiles_x;
         const int n = st->noVisibleEntries;
@@ -1414,14 +1491,16 @@ __device__ __forceinline__ int pair_body(PairLds& L, RayArgs ai, RayArgs ar, TfD
         }
         // (one instance of the march for both sources of the range: a second costs registers)
         raycast_tile<1, true>(ai, st, tile, tiles_x, nullptr, L.ir.rng);
+        pair_tile_cost(cost, tile, t0);
         return 1;
     }
     b -= nb;
     if (b < nb) {
         if (!raycast_go<2>(st)) return 5;
-        const int tile = xcd_tile(b, n_tiles);
+        const int tile = order ? order[nb + b] : xcd_tile(b, n_tiles);
         if (tile < 0) return 5;
         raycast_tile<2>(ar, st, tile, tiles_x, L.vtab);
+        pair_tile_cost(cost, n_tiles + tile, t0);
         return 2;
     }
     b -= nb;
@@ -1440,7 +1519,7 @@ __device__ __forceinline__ int pair_body(PairLds& L, RayArgs ai, RayArgs ar, TfD
 // fuse_ed: CreateExpectedDepths' fill runs in this grid (frame path; W <= ED_PAIR_W)
 int tfk_ed_fused(const tf_ctx* c) { return c->W <= ED_PAIR_W; }
 
-hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch, int fuse_ed)
+hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch, int fuse_ed, int ljf)
 {
     RayArgs ai, ar;
     ray_args(c, ai);
@@ -1473,7 +1552,9 @@ hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch, i
         ed.done = c->edDone;
     }
     ed.fault = ++c->pair_launches == c->fill_fault_launch;
+    const bool order = ljf && c->tile_ljf;
     tf_launch(c, k_raycast_pair, dim3(nfill_pad + 2 * nb + n_pyr + n_bil), dim3(256), 0, ai, ar, c->st, tx, n, nb,
-              pp, n_pyr, pyr_gx, bb, bil_gx, ed, nfill, nfill_pad);
+              pp, n_pyr, pyr_gx, bb, bil_gx, ed, nfill, nfill_pad, order ? (const int*)c->tile_order : nullptr,
+              order ? c->tile_cost : nullptr);
     return hipGetLastError();
 }
