@@ -18,11 +18,15 @@ dev = bench.orbit_frames(N0 + 40, W, H, 7)
 tf = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy), device=0)
 tf.process_frames(dev.ptr, N0)
 k = N0
-while True:
-    ok = tf.process_frames(dev.frame_ptr(k), 1)
-    k += 1
-    if ok[0] and tf.stats()["frame_counter"] > 1 or k >= N0 + 40:
-        break
+if os.environ.get("PTL_BATCH"):      # (the ptl_la build: the last launch of a 32-frame batch with lookahead)
+    tf.process_frames(dev.frame_ptr(k), 32)
+    k += 32
+else:
+    while True:
+        ok = tf.process_frames(dev.frame_ptr(k), 1)
+        k += 1
+        if ok[0] and tf.stats()["frame_counter"] > 1 or k >= N0 + 40:
+            break
 bench.device_sync()
 PTL = 8192
 buf = (ctypes.c_ulonglong * (PTL * 7))()

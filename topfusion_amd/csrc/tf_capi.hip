@@ -288,11 +288,15 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     {   // the raycast tiles' dispatch order, longest first per XCD region (k_raycast_pair, sorted in
         // k_icp_maps_end's grid from the last frame's workgroup times); TFUSION_TILE_ORDER=0: the plain
         // XCD-swizzled order (A/B)
-        const int nt = ((c->W + 15) / 16) * ((c->H + 15) / 16), nb = (nt + 7) / 8 * 8;
+        // TFUSION_TILE_MAP=rows: XCD x takes the tile rows = x (mod 8) instead of the x-th band
+        const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, nt = tx * ty;
         const char* env = getenv("TFUSION_TILE_ORDER");
-        c->tile_ljf = nb / 8 <= TF_LJF_MAX && !(env && env[0] == '0');
+        const char* map = getenv("TFUSION_TILE_MAP");
+        c->tile_rows = map && strcmp(map, "rows") == 0;
+        c->tile_slots = c->tile_rows ? 8 * ((ty + 7) / 8) * tx : (nt + 7) / 8 * 8;
+        c->tile_ljf = c->tile_slots / 8 <= TF_LJF_MAX && !(env && env[0] == '0');
         ALLOC(c->tile_cost, sizeof(unsigned) * 2 * (size_t)nt);
-        ALLOC(c->tile_order, sizeof(int) * 2 * (size_t)nb);
+        ALLOC(c->tile_order, sizeof(int) * 2 * (size_t)c->tile_slots);
     }
     ALLOC(c->depth_in, sizeof(uint16_t) * npx);
     ALLOC(c->dists, sizeof(float) * npx);

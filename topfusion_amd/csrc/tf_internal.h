@@ -312,6 +312,8 @@ struct tf_ctx {
     unsigned* tile_cost;
     int* tile_order;
     int tile_ljf;
+    int tile_rows;           // XCD x's tiles: 0 the x-th band of consecutive tiles; 1 the tile rows = x (mod 8)
+    int tile_slots;          // dispatch slots per half with the order (8 x the largest XCD share)
     int2* edSpill;           // per k_ed_fill row (ed_nrows): extent [0,x) x [0,y) of the pixels k_ed_fill wrote outside
                              // the /8 region (cleared by the next projection pass)
     int ed_lds_max_n;        // k_ed_fill reduces in LDS per /8 row up to this many visible entries
@@ -451,6 +453,19 @@ hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = Tf
                             int ljf = 0);
 #define TF_LJF_MAX 1024          // tiles per XCD region the longest-first ordering sorts (one LDS sort)
 hipError_t tfk_tile_order_init(tf_ctx* c);   // the XCD-swizzled order, zero costs
+// the i-th tile of XCD x's share (-1: none), and the share's size; per = slots / 8
+__host__ __device__ __forceinline__ int tf_tile_of(int x, int i, int n, int tx, int ty, int per, int rows)
+{
+    if (rows) { const int r = x + 8 * (i / tx); return r < ty ? r * tx + i % tx : -1; }
+    const int t = x * per + i;
+    return (i < per && t < n) ? t : -1;
+}
+__host__ __device__ __forceinline__ int tf_tile_count(int x, int n, int tx, int ty, int per, int rows)
+{
+    if (rows) return ty > x ? ((ty - x + 7) / 8) * tx : 0;
+    const int c = n - x * per;
+    return c < 0 ? 0 : (c < per ? c : per);
+}
 int tfk_ed_fused(const tf_ctx* c);
 hipError_t tfk_icp_maps(tf_ctx* c);
 hipError_t tfk_render_snapshot(tf_ctx* c);   // render_snapshot as its own launch

@@ -941,22 +941,23 @@ k_icp_maps(IcpMapArgs a, const TfDevState* __restrict__ st)
 struct TileSortArgs {
     const unsigned* cost;    // [2][n]
     int* order;              // [2][nb]
-    int n, nb;               // tiles, padded dispatch slots per half
+    int n, nb;               // tiles, dispatch slots per half (tf_ctx::tile_slots)
+    int tx, ty, rows;        // tiles per row / column, tf_ctx::tile_rows
 };
 // one XCD region of one half: rank sort (each key's rank = the keys above it; keys are distinct,
 // the tile index rides in the low bits), a few hundred LDS broadcast reads per thread
 __device__ __forceinline__ void tile_sort_block(const TileSortArgs& a, int s, unsigned* keys)
 {
-    const int h = s >> 3, x = s & 7, per = a.nb >> 3, lo = x * per;
-    const int cnt = max(0, min(per, a.n - lo));
+    const int h = s >> 3, x = s & 7, per = a.nb >> 3;
+    const int cnt = tf_tile_count(x, a.n, a.tx, a.ty, per, a.rows);
     for (int i = threadIdx.x; i < cnt; i += 256)
-        keys[i] = (min(a.cost[h * a.n + lo + i], 0xfffffu) << 12) | (unsigned)i;
+        keys[i] = (min(a.cost[h * a.n + tf_tile_of(x, i, a.n, a.tx, a.ty, per, a.rows)], 0xfffffu) << 12) | (unsigned)i;
     __syncthreads();
     for (int i = threadIdx.x; i < cnt; i += 256) {
         const unsigned ki = keys[i];
         int rank = 0;
         for (int j = 0; j < cnt; ++j) rank += keys[j] > ki ? 1 : 0;
-        a.order[h * a.nb + rank * 8 + x] = lo + i;               // longest first
+        a.order[h * a.nb + rank * 8 + x] = tf_tile_of(x, i, a.n, a.tx, a.ty, per, a.rows);   // longest first
     }
     for (int k = cnt + threadIdx.x; k < per; k += 256) a.order[h * a.nb + k * 8 + x] = -1;
 }
@@ -977,13 +978,13 @@ k_icp_maps_end(IcpMapArgs a, ResetArgs r, int gx, int nmaps, PyrArgs pyr, int py
 // the XCD-swizzled order (xcd_tile) and zero costs: a new context's first frames
 hipError_t tfk_tile_order_init(tf_ctx* c)
 {
-    const int n = ((c->W + 15) / 16) * ((c->H + 15) / 16), nb = (n + 7) / 8 * 8;
+    const int tx = (c->W + 15) / 16, ty = (c->H + 15) / 16, n = tx * ty, nb = c->tile_slots;
     int* o = (int*)malloc(sizeof(int) * 2 * (size_t)nb);
     if (!o) return hipErrorOutOfMemory;
     const int per = nb / 8;
     for (int b = 0; b < nb; ++b) {
-        const int t = (b % 8) * per + b / 8;
-        o[b] = o[nb + b] = t < n ? t : -1;
+        const int x = b % 8, i = b / 8;
+        o[b] = o[nb + b] = i < tf_tile_count(x, n, tx, ty, per, c->tile_rows) ? tf_tile_of(x, i, n, tx, ty, per, c->tile_rows) : -1;
     }
     hipError_t e = hipMemcpy(c->tile_order, o, sizeof(int) * 2 * (size_t)nb, hipMemcpyHostToDevice);
     free(o);
@@ -1023,7 +1024,8 @@ hipError_t tfk_icp_maps_end(tf_ctx* c, int slot, TfAhead pyr, size_t pitch)
     int n_sort = 0;
     if (c->tile_ljf) {                   // 2 halves x 8 XCD regions
         ts.cost = c->tile_cost; ts.order = c->tile_order;
-        ts.n = ((c->W + 15) / 16) * ((c->H + 15) / 16); ts.nb = (ts.n + 7) / 8 * 8;
+        ts.tx = (c->W + 15) / 16; ts.ty = (c->H + 15) / 16; ts.n = ts.tx * ts.ty;
+        ts.nb = c->tile_slots; ts.rows = c->tile_rows;
         n_sort = 16;
     }
     tf_launch(c, k_icp_maps_end, dim3(n_sort + nmaps + TF_END_BLOCKS + n_pyr), dim3(256), 0, a, r, gx, nmaps, pp, pyr_gx,
@@ -1426,6 +1428,10 @@ k_raycast_pair(RayArgs ai, RayArgs ar, TfDevState* __restrict__ st, int tiles_x,
     const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    // (TFUSION_PTL_LOOKAHEAD builds: only launches that carry later frames' preprocessing)
+#ifdef TF_PTL_LOOKAHEAD
+    if (n_pyr + (int)gridDim.x - nfill_pad - 2 * nb - n_pyr <= 0) return;
+#endif
     if (blockIdx.x < PTL_MAX) {
         unsigned long long* o = &tf_pair_tl[blockIdx.x * 7];
         if ((threadIdx.x & 63) == 0) o[1 + (threadIdx.x >> 6)] = tw;
@@ -1553,7 +1559,8 @@ hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch, i
     }
     ed.fault = ++c->pair_launches == c->fill_fault_launch;
     const bool order = ljf && c->tile_ljf;
-    tf_launch(c, k_raycast_pair, dim3(nfill_pad + 2 * nb + n_pyr + n_bil), dim3(256), 0, ai, ar, c->st, tx, n, nb,
+    const int nbl = order ? c->tile_slots : nb;
+    tf_launch(c, k_raycast_pair, dim3(nfill_pad + 2 * nbl + n_pyr + n_bil), dim3(256), 0, ai, ar, c->st, tx, n, nbl,
               pp, n_pyr, pyr_gx, bb, bil_gx, ed, nfill, nfill_pad, order ? (const int*)c->tile_order : nullptr,
               order ? c->tile_cost : nullptr);
     return hipGetLastError();
