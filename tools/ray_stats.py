@@ -31,7 +31,7 @@ def main():
     tf.process_frames(dev.ptr, first)
     lib = L.load()
     lib.tf_debug_ray_stats.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-    buf = np.zeros(2 * 1280 * 960, np.uint32)
+    buf = np.zeros(4 * 1280 * 960, np.uint32)
     rows = []
     for k in range(first, first + nsamp):
         ok = tf.process_frames(dev.ptr + k * fb, 1)
@@ -44,12 +44,13 @@ def main():
             free = (a & 0x3ff).astype(np.int64)
             found = ((a >> 10) & 0x7ff).astype(np.int64)
             band = (a >> 21).astype(np.int64)
+            one = buf[(2 + half) * 1280 * 960: (2 + half) * 1280 * 960 + W * H].reshape(H, W).astype(np.int64)
             tot = free + found
             rt = free + 2 * found + 2 * band
 
             def waves(v):   # 8x8 quadrants: (H/8, 8, W/8, 8) -> (waves, 64)
                 return v.reshape(H // 8, 8, W // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64)
-            wt, wf, wb, wr = waves(tot), waves(free), waves(band), waves(rt)
+            wt, wf, wb, wr, wo = waves(tot), waves(free), waves(band), waves(rt), waves(one)
             wmax = wt.max(axis=1)
             arg = wt.argmax(axis=1)
             top = np.argsort(-wmax)[:max(1, len(wmax) // 100)]          # the longest 1 % of waves
@@ -61,7 +62,18 @@ def main():
                          "wave_rt_max_mean": float(wr.max(axis=1).mean()), "wave_rt_max_max": int(wr.max()),
                          "top1pct_ray_steps": float(lr(wt).mean()), "top1pct_ray_free": float(lr(wf).mean()),
                          "top1pct_ray_band": float(lr(wb).mean()), "top1pct_ray_rt": float(lr(wr).mean()),
+                         "ray_found_sdf1": float(one.mean()), "top1pct_ray_found_sdf1": float(lr(wo).mean()),
                          "top1pct_live_lanes_at_half": float(np.mean([(wt[w] > wmax[w] // 2).sum() for w in top]))}
+        if k == first + nsamp - 1 or len(rows) == 0:
+            try:
+                vis = tf.visible_ids()
+                ptr = tf.hash()["ptr"][vis]
+                ptr = ptr[ptr >= 0]
+                sdf = tf.vba()["sdf"].reshape(-1, 512)[ptr]
+                res["visible_blocks"] = int(len(ptr))
+                res["uniform_sdf1_blocks"] = int((sdf == 0x7fff).all(axis=1).sum())
+            except Exception as ex:
+                res["uniform_note"] = repr(ex)[:160]
         rows.append(res)
         print(json.dumps(res), flush=True)
     for name in ("icp", "render"):

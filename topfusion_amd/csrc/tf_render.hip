@@ -308,7 +308,7 @@ __device__ __forceinline__ bool ray_refine(const RayArgs& a, Ray& R)
 // diagnostic builds only (tools/ray_stats.py): per ray, steps in unallocated space (bits 0-9),
 // steps that read voxels (bits 10-20) and of those the band steps that also read the eight
 // interpolation corners (bits 21-31), for the two raycasts of the last pair launch
-__device__ unsigned tf_ray_stats_buf[2 * 1280 * 960];
+__device__ unsigned tf_ray_stats_buf[4 * 1280 * 960];   // [2][W*H] counts, then [2][W*H] sdf = 1 voxel steps
 extern "C" int tf_debug_ray_stats(void* host, size_t bytes)
 {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tf_ray_stats_buf), bytes < sizeof(tf_ray_stats_buf) ? bytes : sizeof(tf_ray_stats_buf), 0,
@@ -373,7 +373,7 @@ __device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* i
     ray_init(a, invM, x, y, vf, R);
     const float stepScale = a.mu * a.oneOverVoxelSize;
 #ifdef TF_RAY_STATS
-    unsigned n_free = 0, n_found = 0, n_band = 0;
+    unsigned n_free = 0, n_found = 0, n_band = 0, n_one = 0;
 #endif
     while (R.active) {
         const int rx = tf_round(R.pt[0]), ry = tf_round(R.pt[1]), rz = tf_round(R.pt[2]);
@@ -393,6 +393,9 @@ __device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* i
         if (wave_any(found)) raw = vox_at(a.s, g.y, lin_x(rx) + lin_y(ry) + lin_zg(rz));
         // a missing block reads Voxel_s(): 32767 / 32767 = 1
         float sdfValue = found ? tf_short_to_float((short)(raw & 0xffffu)) : 1.0f;
+#ifdef TF_RAY_STATS
+        if (found && (raw & 0xffffu) == 0x7fffu) ++n_one;
+#endif
         if (MARK && vmIndex) a.visType[vmIndex - 1] = 1;
         float stepLength;
         if (!vmIndex) {
@@ -415,7 +418,10 @@ __device__ __forceinline__ float ray_march_lite(const RayArgs& a, const float* i
     }
 #ifdef TF_RAY_STATS
     if (x + y * a.W < 1280 * 960)
+    {
         tf_ray_stats_buf[(MARK ? 0 : 1280 * 960) + x + y * a.W] = min(n_free, 1023u) | (min(n_found, 2047u) << 10) | (min(n_band, 2047u) << 21);
+        tf_ray_stats_buf[2 * 1280 * 960 + (MARK ? 0 : 1280 * 960) + x + y * a.W] = n_one;
+    }
 #endif
     float w = 0.0f;
     if (ray_refine(a, R)) {                 // ray_finish on interp_at's confidence read
