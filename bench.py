@@ -427,6 +427,112 @@ def icp_occupancy():
     return out
 
 
+def c5e_bench(args):
+    """C5E (BASELINE configs[4], SURVEY §8d C5: "capacity saturation and silent allocation failure"):
+    the engine-level hash stress.  A 50 k-frame seed-13 walk (<= 1 cm / 0.5 deg per frame) through
+    the unbounded tiled hall of synth.render_hall, rendered on the GPU into HBM first; per frame
+    computeDists + AllocateSceneFromDepth + IntegrateIntoScene at the ground-truth pose (+ the
+    swapping engine with --swapping) through tf_scene_fuse_frames -- no ICP, so no frame-mixing
+    resets, and the reference capacities (65 536 blocks, 2^20 buckets, 2^17 excess), so the VBA fills
+    and every later frame's new blocks fail silently (SceneReconstructionEngine_host.cu:358-413).
+    A step is one tf_scene_fuse_frames batch of F frames; the per-frame records give the allocated
+    blocks, the failed requests and (swapping) the evictions / merges of every frame."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:                      # torch's HIP runtime first (it must initialise before the product's)
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    from topfusion_amd import TopFu, default_params, synth
+    from topfusion_amd import _lib as L
+    L.check(L.load().tf_set_device(local_rank), "tf_set_device")
+    F = args.frames_per_step or 1000
+    steps = args.steps if args.steps is not None else 50
+    warm = args.warmup if args.warmup is not None else 1
+    W, H = args.cols or 640, args.rows or 480
+    vox = args.voxel or 0.01
+    seed = 13 + rank
+    n = (warm + steps) * F
+    t0 = time.perf_counter()
+    stream, R, t = synth.hall_device(n, W, H, seed)
+    w2c = synth.world_to_camera_rt(R, t)
+    t_render = time.perf_counter() - t0
+    fx, fy, cx, cy = synth.intrinsics(W, H)
+    pkw = dict(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy, voxelSize=vox)
+    if args.swapping:
+        pkw.update(use_swapping=1, swap_transfer_blocks=args.swap_transfer_blocks)
+    tf = TopFu(default_params(**pkw), device=local_rank)
+    recs = []
+    for k in range(warm):
+        recs.append(tf.fuse_frames(stream.frame_ptr(k * F), w2c[k * F:(k + 1) * F]))
+    tf.reset_totals()
+    if dist is not None:
+        dist.barrier()
+    step_s = []
+    t0 = time.perf_counter()
+    for k in range(warm, warm + steps):
+        ts = time.perf_counter()
+        recs.append(tf.fuse_frames(stream.frame_ptr(k * F), w2c[k * F:(k + 1) * F]))
+        step_s.append(time.perf_counter() - ts)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tot = tf.totals()
+    rec = np.concatenate(recs)
+    timed = rec[warm * F:]
+    nb = tf.params().n_blocks
+    fails = rec["alloc_failed_type1"].astype(np.int64) + rec["alloc_failed_type2"]
+    first_fail = int(np.argmax(fails > 0)) if (fails > 0).any() else None
+    # steps whose frames all come after the first failure: the saturated-VBA rate
+    sat_steps = [i for i in range(steps) if first_fail is not None and (warm + i) * F >= first_fail]
+    sat_s = sum(step_s[i] for i in sat_steps)
+    elapsed_max, total_frames = elapsed, float(steps * F)
+    if dist is not None:
+        import torch
+        elapsed_max, total_frames = combine_ranks(elapsed, steps * F, f"cuda:{local_rank}", world)
+    if rank == 0:
+        late = timed[-min(len(timed), 10 * F):]
+        allocated = nb - 1 - rec["lastFreeBlockId"]
+        out = {
+            "metric": f"engine-level fused frames/sec (AllocateSceneFromDepth + IntegrateIntoScene) @{W}x{H}, "
+                      f"{vox * 1000:g} mm voxel hash, saturating hash stress" + (" (swapping scene)" if args.swapping else ""),
+            "value": round(total_frames / elapsed_max, 2), "unit": "frames/s", "n_gpus": world, "steps": steps,
+            "warmup": warm, "ms_per_step": round(elapsed_max / steps * 1000.0, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"C5E: seed-{seed} walk through the tiled hall (synth.render_hall), <= 1 cm / 0.5 deg "
+                                   f"per frame, unconfined; {W}x{H}, {vox * 1000:g} mm voxels, reference capacities",
+                       "step": f"one tf_scene_fuse_frames batch of {F} frames resident in HBM", "frames_per_step": F,
+                       "capacity": {"n_blocks": nb, "n_buckets": tf.params().n_buckets, "n_excess": tf.params().n_excess},
+                       "swapping": (f"on: <= {args.swap_transfer_blocks} blocks per direction per frame")
+                                   if args.swapping else "off", "parallelism": f"replicas{world}"},
+            "ms_per_frame": round(elapsed_max / (steps * F) * 1000.0, 5),
+            "first_failure_frame": first_fail,
+            "saturated_frames_per_sec": round(len(sat_steps) * F / sat_s, 2) if sat_steps else None,
+            "saturated_frames": len(sat_steps) * F,
+            "allocated_blocks_last": int(allocated[-1]),
+            "allocated_blocks_at": {str(k): int(allocated[k]) for k in range(0, n, max(1, n // 10))},
+            "lastFreeExcessListId_last": int(rec["lastFreeExcessListId"][-1]),
+            "frames_with_failures_timed": int((fails[warm * F:] > 0).sum()),
+            "frames_with_failures_last_10_steps_frac": round(float((late["alloc_failed_type1"] + late["alloc_failed_type2"] > 0).mean()), 4),
+            "failed_type1_per_frame_timed": round(float(timed["alloc_failed_type1"].mean()), 2),
+            "failed_type2_per_frame_timed": round(float(timed["alloc_failed_type2"].mean()), 2),
+            "failed_totals_timed": {"type1": int(tot["alloc_failed_type1"]), "type2": int(tot["alloc_failed_type2"])},
+            "visible_blocks_mean_timed": round(float(timed["noVisibleEntries"].mean()), 1),
+            "swapped_out_per_frame": round(float(timed["swapped_out"].mean()), 2) if args.swapping else None,
+            "swapped_in_merged_per_frame": round(float(timed["swapped_in_merged"].mean()), 2) if args.swapping else None,
+            "swap_realloc_per_frame": round(float(timed["swap_realloc"].mean()), 2) if args.swapping else None,
+            "render_s": round(t_render, 2),
+        }
+        print(json.dumps(out))
+    tf.close()
+    stream.free()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.config == "C5E":

@@ -66,3 +66,15 @@ def test_single_rank_passthrough():
     sys.path.insert(0, ROOT)
     import bench
     assert bench.combine_ranks(0.5, 10, "cpu", 1) == (0.5, 10.0)
+
+
+def test_every_bench_config_has_a_runner():
+    """Each --config choice of bench.py dispatches to a function the module defines (a config
+    whose runner went missing would only fail on the GPU box)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import inspect
+    src = inspect.getsource(bench.main)
+    for cfg, fn in (("C3I", "c3_integrate"), ("C3R", "c3_raycast"), ("C5E", "c5e_bench")):
+        assert fn in src, (cfg, fn)
+        assert callable(getattr(bench, fn, None)), fn
