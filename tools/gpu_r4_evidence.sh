@@ -41,7 +41,8 @@ run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE
 cd $R
 for k in k_icp_frame k_raycast_pair k_integrate k_alloc_requests k_alloc_apply k_icp_maps_end; do
   extra=""; [ "$k" = "k_icp_frame" ] && extra="--full"
-  python3 tools/pmc_kernel_summary.py $P $k $extra -o $O/pmc_kernel_c2_$k.json > /dev/null
+  python3 tools/pmc_kernel_summary.py $P $k $extra -o $O/pmc_kernel_c2_$k.json \
+    --source "tools/gpu_r4_evidence.sh: rocprofv3 --pmc passes (fetch, write, occ, inst, lds, tcc) over bench.py $ARGS (C2), averaged per dispatch by tools/pmc_kernel_summary.py" > /dev/null
 done
 python3 -c "
 import json

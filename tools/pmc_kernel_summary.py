@@ -20,6 +20,7 @@ Derived:
   traffic            = FETCH_SIZE x 1024 x 2 (wide reads, pmc_traffic.py) + WRITE_SIZE x 1024
 
     python tools/pmc_kernel_summary.py gpurun_out/pmck_TAG KERNEL_SUBSTRING [--top-quartile] [--full] [-o OUT.json]
+        [--source TEXT]   (the recipe that produced the passes, recorded in "source")
     python tools/pmc_kernel_summary.py --from-json profiles/rNN/pmc_kernel_X.json [-o OUT.json]
         (re-derive from the "raw" averages a summary already holds)
 """
@@ -101,6 +102,11 @@ def collect(root, kern, top=False, full=False):
 def main():
     args = sys.argv[1:]
     out_path = None
+    source = None
+    if "--source" in args:
+        i = args.index("--source")
+        source = args[i + 1]
+        del args[i:i + 2]
     if "-o" in args:
         i = args.index("-o")
         out_path = args[i + 1]
@@ -115,7 +121,7 @@ def main():
         root, kern = args[0], args[1]
         avg = collect(root, kern, "--top-quartile" in args, "--full" in args)
         res = derive(kern, avg)
-        res["source"] = os.path.relpath(root)
+        res["source"] = source or os.path.relpath(root)
     text = json.dumps(res, indent=1)
     if out_path:
         open(out_path, "w").write(text + "\n")
