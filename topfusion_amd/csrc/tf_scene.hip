@@ -439,12 +439,13 @@ __device__ __forceinline__ int4 block_sum4(int4 v)
 // S(k) > v0 nothing succeeds any more).  A success takes allocList[v0 - S(k)] and, for type 2,
 // excessList[e0 - q(k)].  Without exhaustion S(k) is k's rank among all requests.  So every
 // request is decided in parallel from the chunk prefix sums, with the serial loop's results.
-__device__ __forceinline__ void alloc_apply_chunk(const AllocArgs& a, TfDevState* __restrict__ st, int n_chunks,
-                                                  const int* __restrict__ counts, unsigned char* __restrict__ allocType,
-                                                  int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
-                                                  unsigned char* __restrict__ visType, const int* __restrict__ allocList,
-                                                  const int* __restrict__ excessList, int n_total)
+__global__ void __launch_bounds__(256)
+k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int* __restrict__ counts,
+              unsigned char* __restrict__ allocType, int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
+              unsigned char* __restrict__ visType, const int* __restrict__ allocList,
+              const int* __restrict__ excessList, int n_total)
 {
+    if (st->abort) return;
     // this chunk's request types, loaded before (and in flight with) the counts prefix
     const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
     unsigned long long lo = 0, hi = 0;
@@ -550,76 +551,6 @@ k_alloc_discard(TfDevState* __restrict__ st, const int* __restrict__ counts, uns
 // buildVisibleList_device<false> (SceneReconstructionEngine_host.cu:434-479) with
 // checkBlockVisibility<false> (SceneReconstructionEngine.hpp:300-375), ordered compaction
 // ---------------------------------------------------------------------------------------
-// One chunk's final visible types: type 4 (a type 3 that failed checkBlockVisibility,
-// k_set_type3) becomes 0, written back; with swapping every listed entry not in active memory
-// becomes "needed" (buildVisibleList_device<true>, :466-469).  Returns this thread's count of
-// listed entries and leaves the cleaned 16 types in lo / hi.
-__device__ __forceinline__ int vis_chunk_clean(unsigned char* __restrict__ visType, unsigned char* __restrict__ swapState,
-                                               int base, int n_total, unsigned long long& lo, unsigned long long& hi)
-{
-    int cnt = 0;
-    lo = hi = 0;
-    if (base >= n_total) return 0;
-    load16(visType + base, &lo, &hi);
-    bool dirty = false;
-    for (int i = 0; i < 16; ++i) {
-        unsigned t = byte16(lo, hi, i);
-        if (t == 4) {
-            if (i < 8) lo &= ~(0xffull << (8 * i)); else hi &= ~(0xffull << (8 * (i - 8)));
-            t = 0;
-            dirty = true;
-        }
-        cnt += t > 0;
-    }
-    if (dirty) *(uint4*)(visType + base) = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
-    if (swapState) {
-        unsigned long long slo, shi;
-        load16(swapState + base, &slo, &shi);
-        bool sdirty = false;
-        for (int i = 0; i < 16; ++i) {
-            if (byte16(lo, hi, i) > 0 && byte16(slo, shi, i) != 2 && byte16(slo, shi, i) != 1) {
-                if (i < 8) slo = (slo & ~(0xffull << (8 * i))) | (1ull << (8 * i));
-                else shi = (shi & ~(0xffull << (8 * (i - 8)))) | (1ull << (8 * (i - 8)));
-                sdirty = true;
-            }
-        }
-        if (sdirty) *(uint4*)(swapState + base) = make_uint4((unsigned)slo, (unsigned)(slo >> 32), (unsigned)shi, (unsigned)(shi >> 32));
-    }
-    return cnt;
-}
-
-// the frame's allocation outcome into the free-list counters (k_vis_count's, or the fused
-// k_vis_apply's block 0, once every k_alloc_apply workgroup is done)
-__device__ __forceinline__ void alloc_counters_settle(TfDevState* __restrict__ st)
-{
-    // the counters drop by the successful requests (failed ones restored them, :378, :400-401)
-    const int f1 = st->alloc_fail[0], f2 = st->alloc_fail[1];
-    st->lastFreeBlockId -= st->pad_[0] - f1 - f2;
-    st->lastFreeExcessListId -= st->pad_[1] - f2;
-    st->tot_alloc_fail1 += f1;
-    st->tot_alloc_fail2 += f2;
-}
-// allocateVoxelBlocksList_device (above) for this workgroup's chunk, then (the frame path) the
-// chunk's visible-type count when it holds bucket entries only
-__global__ void __launch_bounds__(256)
-k_alloc_apply(AllocArgs a, TfDevState* __restrict__ st, int n_chunks, const int* __restrict__ counts,
-              unsigned char* __restrict__ allocType, int* __restrict__ winnerKey, TfHashEntry* __restrict__ hash,
-              unsigned char* __restrict__ visType, const int* __restrict__ allocList,
-              const int* __restrict__ excessList, int n_total, int* __restrict__ visCounts, int mixed,
-              unsigned char* __restrict__ swapState)
-{
-    if (st->abort) return;
-    alloc_apply_chunk(a, st, n_chunks, counts, allocType, winnerKey, hash, visType, allocList, excessList, n_total);
-    // the fused count (k_vis_apply_fused): a chunk of bucket entries only is final now
-    if (visCounts && (int)blockIdx.x < mixed) {
-        __syncthreads();                       // (this workgroup's type-1 failures wrote its types)
-        unsigned long long lo, hi;
-        const int cnt = vis_chunk_clean(visType, swapState, blockIdx.x * CHUNK + threadIdx.x * 16, n_total, lo, hi);
-        const int tot = block_sum(cnt);
-        if (threadIdx.x == 0) visCounts[blockIdx.x] = tot;
-    }
-}
-
 __global__ void __launch_bounds__(256)
 k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
             unsigned char* __restrict__ visType, int* __restrict__ counts, int* __restrict__ allocCounts,
@@ -631,71 +562,49 @@ k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restric
         // frame's requests, and (without exhaustion) the free-list counters drop by the totals
         allocCounts[2 * blockIdx.x] = 0;
         allocCounts[2 * blockIdx.x + 1] = 0;
-        if (blockIdx.x == 0) alloc_counters_settle(st);
-    }
-    unsigned long long lo, hi;
-    const int cnt = vis_chunk_clean(visType, swapState, blockIdx.x * CHUNK + threadIdx.x * 16, v.n_total, lo, hi);
-    int tot = block_sum(cnt);
-    if (threadIdx.x == 0) counts[blockIdx.x] = tot;
-}
-
-// Fused count (round 4, the frame path): k_alloc_apply's workgroups count their own chunk when
-// it holds bucket entries only (nothing but its own workgroup writes a bucket chunk's types
-// during the apply pass: a type-2 success marks an excess entry, a type-1 failure its own
-// entry), so k_vis_count's launch is gone; here the chunks from `mixed` on (those with excess
-// entries, whose types any apply workgroup may have set) are cleaned by their own workgroup and
-// counted by every later one, which reads them again (a type 4 not yet cleaned counts as 0).
-// The last chunk's workgroup has the whole count.  Same list, same counters.
-__device__ __forceinline__ int vis_count_range(const unsigned char* __restrict__ visType, int c0, int c1, int n_total)
-{
-    int cnt = 0;
-    for (int h = c0; h < c1; ++h) {
-        const int base = h * CHUNK + threadIdx.x * 16;
-        if (base >= n_total) break;
-        unsigned long long lo, hi;
-        load16(visType + base, &lo, &hi);
-        for (int i = 0; i < 16; ++i) { const unsigned t = byte16(lo, hi, i); cnt += (t > 0 && t != 4) ? 1 : 0; }
-    }
-    return cnt;
-}
-__global__ void __launch_bounds__(256)
-k_vis_apply_fused(VisArgs v, TfDevState* __restrict__ st, int n_chunks, int mixed, const int* __restrict__ counts,
-                  unsigned char* __restrict__ visType, int* __restrict__ visibleIds, int* __restrict__ allocCounts,
-                  unsigned char* __restrict__ swapState)
-{
-    if (st->abort) return;
-    const int c = (int)blockIdx.x;
-    if (threadIdx.x == 0) {
-        allocCounts[2 * c] = 0;
-        allocCounts[2 * c + 1] = 0;
-        if (c == 0) alloc_counters_settle(st);
-    }
-    const int base = c * CHUNK + threadIdx.x * 16;
-    unsigned long long lo = 0, hi = 0;
-    int cnt;
-    if (c >= mixed) cnt = vis_chunk_clean(visType, swapState, base, v.n_total, lo, hi);
-    else {
-        if (base < v.n_total) load16(visType + base, &lo, &hi);       // (cleaned by k_alloc_apply)
-        cnt = 0;
-        for (int i = 0; i < 16; ++i) cnt += byte16(lo, hi, i) > 0;
-    }
-    int pre = 0;
-    for (int h = threadIdx.x; h < min(c, mixed); h += 256) pre += counts[h];
-    if (c > mixed) pre += vis_count_range(visType, mixed, c, v.n_total);
-    pre = block_sum(pre);
-    int tmp;
-    int r = pre + block_excl_scan(cnt, &tmp);
-    if (c == n_chunks - 1 && threadIdx.x == 0) {
-        const int all = pre + tmp;
-        st->noVisibleEntries = all < v.cap ? all : v.cap;
-    }
-    if (!cnt) return;
-    for (int i = 0; i < 16; ++i) {
-        if (byte16(lo, hi, i) > 0) {
-            if (r < v.cap) visibleIds[r] = base + i;
-            r++;
+        if (blockIdx.x == 0) {
+            // the counters drop by the successful requests (failed ones restored them, :378, :400-401)
+            const int f1 = st->alloc_fail[0], f2 = st->alloc_fail[1];
+            st->lastFreeBlockId -= st->pad_[0] - f1 - f2;
+            st->lastFreeExcessListId -= st->pad_[1] - f2;
+            st->tot_alloc_fail1 += f1;
+            st->tot_alloc_fail2 += f2;
         }
     }
+    const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
+    int cnt = 0;
+    if (base < v.n_total) {
+        unsigned long long lo, hi;
+        load16(visType + base, &lo, &hi);
+        bool dirty = false;
+        for (int i = 0; i < 16; ++i) {
+            unsigned t = byte16(lo, hi, i);
+            if (t == 4) {              // type 3 that failed checkBlockVisibility (k_set_type3)
+                if (i < 8) lo &= ~(0xffull << (8 * i)); else hi &= ~(0xffull << (8 * (i - 8)));
+                t = 0;
+                dirty = true;
+            }
+            cnt += t > 0;
+        }
+        if (dirty) *(uint4*)(visType + base) = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
+        if (swapState) {
+            // buildVisibleList_device<true> (SceneReconstructionEngine_host.cu:466-469): every
+            // listed entry not already in active memory (state 2) becomes "needed" (1)
+            unsigned long long slo, shi;
+            load16(swapState + base, &slo, &shi);
+            bool sdirty = false;
+            for (int i = 0; i < 16; ++i) {
+                if (byte16(lo, hi, i) > 0 && byte16(slo, shi, i) != 2 && byte16(slo, shi, i) != 1) {
+                    if (i < 8) slo = (slo & ~(0xffull << (8 * i))) | (1ull << (8 * i));
+                    else shi = (shi & ~(0xffull << (8 * (i - 8)))) | (1ull << (8 * (i - 8)));
+                    sdirty = true;
+                }
+            }
+            if (sdirty) *(uint4*)(swapState + base) = make_uint4((unsigned)slo, (unsigned)(slo >> 32), (unsigned)shi, (unsigned)(shi >> 32));
+        }
+    }
+    int tot = block_sum(cnt);
+    if (threadIdx.x == 0) counts[blockIdx.x] = tot;
 }
 
 __global__ void __launch_bounds__(256)
@@ -773,27 +682,14 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch, int onl
     if (only_update)   // allocateVoxelBlocksList_device is skipped (SceneReconstructionEngine_host.cu:162-168)
         hipLaunchKernelGGL(k_alloc_discard, dim3(c->alloc_chunks), dim3(256), 0, c->stream, c->st, c->allocCounts,
                            c->allocType, c->winnerKey, c->n_total);
-#ifndef TF_VIS_FUSE_MAX
-#define TF_VIS_FUSE_MAX (-1)      // (the fused count: 64; pending its GPU A/B)
-#endif
-    // the fused count (k_vis_apply_fused) while the chunks holding excess entries are few (each
-    // later workgroup re-reads them)
-    const int mixed = c->p.n_buckets / CHUNK;
-    const bool fused = !only_update && c->vis_chunks - mixed <= TF_VIS_FUSE_MAX;
-    unsigned char* swap_st = swapping ? c->swapState : nullptr;
-    if (!only_update)
+    else
         hipLaunchKernelGGL(k_alloc_apply, dim3(c->alloc_chunks), dim3(256), 0, c->stream, a, c->st, c->alloc_chunks,
                            c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
-                           c->n_total, fused ? c->visCounts : nullptr, mixed, swap_st);
-    if (fused) {
-        hipLaunchKernelGGL(k_vis_apply_fused, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks, mixed,
-                           c->visCounts, c->visType, c->visibleIds, c->allocCounts, swap_st);
-    } else {
-        hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
-                           c->visCounts, c->allocCounts, swap_st);
-        hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
-                           c->visCounts, c->visType, c->visibleIds);
-    }
+                           c->n_total);
+    hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
+                       c->visCounts, c->allocCounts, swapping ? c->swapState : nullptr);
+    hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
+                       c->visCounts, c->visType, c->visibleIds);
     if (swapping) return tfk_swap_realloc(c);      // reAllocateSwappedOutVoxelBlocks (:184-189)
     if (c->p.use_swapping)                         // (an onlyUpdateVisibleList pass reallocates nothing)
         return hipMemsetAsync(&c->st->swap_realloc, 0, sizeof(int), c->stream);
