@@ -1120,7 +1120,7 @@ extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12]
     for (int i = 0; i < iters && e == hipSuccess; ++i)
         e = stage == TF_STAGE_INTEGRATE ? tfk_integrate(c)
           : stage == TF_STAGE_EXPECTED_DEPTHS ? tfk_expected_depths(c, 1, 1)
-          : stage == TF_STAGE_RAYCAST_ICP ? tfk_raycast(c, 1) : tfk_raycast_pair(c);
+          : stage == TF_STAGE_RAYCAST_ICP ? tfk_raycast(c, 1) : tfk_raycast_pair_ordered(c);
     if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
     if (e == hipSuccess) e = hipEventSynchronize(e1);
     float ms = 0.f;

@@ -453,6 +453,9 @@ hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr = TfAhead{}, TfAhead bil = Tf
                             int ljf = 0);
 #define TF_LJF_MAX 1024          // tiles per XCD region the longest-first ordering sorts (one LDS sort)
 hipError_t tfk_tile_order_init(tf_ctx* c);   // the XCD-swizzled order, zero costs
+// the raycast pair on its own (tf_time_stage, C3R) with the frame path's tile order: the pair
+// launch, then the order sort the frame path runs in k_icp_maps_end's grid
+hipError_t tfk_raycast_pair_ordered(tf_ctx* c);
 // the i-th tile of XCD x's share (-1: none), and the share's size; per = slots / 8
 __host__ __device__ __forceinline__ int tf_tile_of(int x, int i, int n, int tx, int ty, int per, int rows)
 {

@@ -981,6 +981,12 @@ k_icp_maps_end(IcpMapArgs a, ResetArgs r, int gx, int nmaps, PyrArgs pyr, int py
     else pyr_normals_block<256>(pyr, (b - nmaps - TF_END_BLOCKS) % pyr_gx, (b - nmaps - TF_END_BLOCKS) / pyr_gx, L.pn);
 }
 
+__global__ void __launch_bounds__(256) k_tile_sort(TileSortArgs ts)
+{
+    __shared__ unsigned keys[TF_LJF_MAX];
+    tile_sort_block(ts, (int)blockIdx.x, keys);
+}
+
 // the XCD-swizzled order (xcd_tile) and zero costs: a new context's first frames
 hipError_t tfk_tile_order_init(tf_ctx* c)
 {
@@ -1530,6 +1536,18 @@ __device__ __forceinline__ int pair_body(PairLds& L, RayArgs ai, RayArgs ar, TfD
 // projection): the renderImage half reads the range-image snapshot (render_snapshot).
 // fuse_ed: CreateExpectedDepths' fill runs in this grid (frame path; W <= ED_PAIR_W)
 int tfk_ed_fused(const tf_ctx* c) { return c->W <= ED_PAIR_W; }
+
+hipError_t tfk_raycast_pair_ordered(tf_ctx* c)
+{
+    hipError_t e = tfk_raycast_pair(c, TfAhead{}, TfAhead{}, 0, 0, 1);
+    if (e != hipSuccess || !c->tile_ljf) return e;
+    TileSortArgs ts;
+    ts.cost = c->tile_cost; ts.order = c->tile_order;
+    ts.tx = (c->W + 15) / 16; ts.ty = (c->H + 15) / 16; ts.n = ts.tx * ts.ty;
+    ts.nb = c->tile_slots; ts.rows = c->tile_rows;
+    hipLaunchKernelGGL(k_tile_sort, dim3(16), dim3(256), 0, c->stream, ts);
+    return hipGetLastError();
+}
 
 hipError_t tfk_raycast_pair(tf_ctx* c, TfAhead pyr, TfAhead bil, size_t pitch, int fuse_ed, int ljf)
 {
