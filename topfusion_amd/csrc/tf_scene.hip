@@ -902,9 +902,40 @@ __device__ __forceinline__ void integ_apply_pair(uint4 v, uint4 v2, const float 
 }
 
 template <bool WITH_ED, bool RGB>
+__device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+                                           const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed,
+                                           long long* __restrict__ cnt);
+#ifdef TF_INTEG_TIMELINE
+// diagnostic builds only (tools/integ_timeline.py): per workgroup of the last frame-path integrate
+// launch, [start, end] on the 100 MHz clock
+__device__ unsigned long long tf_integ_tl[4096 * 2];
+extern "C" int tf_debug_integ_timeline(void* host, size_t bytes)
+{
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(tf_integ_tl), bytes < sizeof(tf_integ_tl) ? bytes : sizeof(tf_integ_tl), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
+template <bool WITH_ED, bool RGB>
 __global__ void __launch_bounds__(256)
 k_integrate(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
             const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed, long long* __restrict__ cnt)
+{
+#ifdef TF_INTEG_TIMELINE
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    integ_body<WITH_ED, RGB>(a, st, hash, visibleIds, vba, ed, cnt);
+    __syncthreads();
+    if (WITH_ED && threadIdx.x == 0 && blockIdx.x < 4096) {
+        tf_integ_tl[2 * blockIdx.x] = t0;
+        tf_integ_tl[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#else
+    integ_body<WITH_ED, RGB>(a, st, hash, visibleIds, vba, ed, cnt);
+#endif
+}
+template <bool WITH_ED, bool RGB>
+__device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+                                           const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed,
+                                           long long* __restrict__ cnt)
 {
     // WITH_ED: the first TF_ED_BLOCKS workgroups run CreateExpectedDepths' projection pass (it
     // reads only the visible list and the pose; integration writes only voxels): one launch
