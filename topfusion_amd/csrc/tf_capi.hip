@@ -564,6 +564,10 @@ struct RgbScope {
     ~RgbScope() { c->rgb_cur = nullptr; }
 };
 
+#ifdef TF_DIAG_NOP_AFTER_ICP
+__global__ void k_diag_nop() {}
+#endif
+
 static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, int slot,
                                const TfFramePlan* plan = nullptr)
 {
@@ -580,6 +584,11 @@ static tf_status enqueue_frame(tf_ctx* c, const uint16_t* depth, size_t pitch, i
     // persistent ICP, setToType3 / the renderImage snapshot run in its tail
     const bool t3_fold = c->icp_persistent != 0;
     STAGE(TF_STAGE_ICP, tfk_icp(c, 1, 1, t3_fold));
+#ifdef TF_DIAG_NOP_AFTER_ICP
+    // diagnostic builds only: an empty launch between the ICP and the allocation, to tell in a
+    // kernel trace which side of that boundary its dispatch gap belongs to
+    hipLaunchKernelGGL(k_diag_nop, dim3(1), dim3(64), 0, c->stream);
+#endif
     STAGE(TF_STAGE_ALLOC, tfk_alloc(c, t3_fold ? 2 : 1, plan->alloc_bil, pitch));   // topfu.cpp:202 / 281
     // (+ CreateExpectedDepths' projection pass in the same grid)
     STAGE(TF_STAGE_INTEGRATE, tfk_integrate(c, 1, 1));              // topfu.cpp:203 / 282 (+ frame-0 prev_ = curr_)

@@ -484,7 +484,7 @@ hipError_t tfk_expected_depths(tf_ctx* c, int project_done = 0, int keep_bins = 
 static inline int ed_nrows(int H) { const int n = (H - 1) / TF_SUBSAMPLE + 1 + ED_XROWS; return n < H ? n : H; }
 #define ED_LDS_MAX_N 16384       // k_ed_fill: per-/8-row LDS reduction up to this many visible entries
 hipError_t ed_spill_all(tf_ctx* c);   // mark the whole range buffer for clearing by the next projection pass
-#define TF_INTEG_WG 2048         // workgroups of the integration pass (grid-stride)
+#define TF_INTEG_WG 2560         // workgroups of the stand-alone integration pass (grid-stride; 2 rounds of 5 per CU)
 #define TF_INTEG_WG_FRAME 768    // ... in the frame path (C2-size lists: 3 resident rounds of 256 WGs instead of 2048)
 hipError_t tfk_frame0_matrices(tf_ctx* c);
 // swapping (tf_swap.hip): reallocation of listed swapped-out entries (after the visible list),

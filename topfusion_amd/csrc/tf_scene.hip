@@ -16,7 +16,12 @@
 #include "tf_reset.h"
 #include "tf_vis.h"
 
+#ifndef TF_INTEG_STREAM_BLOCKS
 #define TF_INTEG_STREAM_BLOCKS 16384   // 32 MiB of voxels
+#endif
+#ifndef TF_INTEG_NT_STORES
+#define TF_INTEG_NT_STORES 0
+#endif
 #define CHUNK 4096          // hash entries per workgroup in the scan passes (256 thr x 16)
 
 // byte i (0..15) of a 16-byte group held as two 64-bit words (no dynamic register indexing)
@@ -932,6 +937,17 @@ k_integrate(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restr
     integ_body<WITH_ED, RGB>(a, st, hash, visibleIds, vba, ed, cnt);
 #endif
 }
+// the stand-alone depth-only pass (stage entry points, C3I): its own register budget, so that
+// TF_INTEG_PASS_WAVES waves per SIMD are resident on a list of millions of blocks
+#ifndef TF_INTEG_PASS_WAVES
+#define TF_INTEG_PASS_WAVES 5
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_INTEG_PASS_WAVES)))
+k_integrate_pass(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+                 const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed, long long* __restrict__ cnt)
+{
+    integ_body<false, false>(a, st, hash, visibleIds, vba, ed, cnt);
+}
 template <bool WITH_ED, bool RGB>
 __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
                                            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed,
@@ -1040,7 +1056,7 @@ __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__
             const TfHashEntry nne = hash[nid1], nne2 = hash[nid2];
             const int nn1 = visibleIds[min(i + 3 * step, n - 1)], nn2 = visibleIds[min(i + 3 * step + stride, n - 1)];
             // pass k: update
-            integ_apply_pair<RGB>(v, v2, dm, z, ok, e, e2, vx, vy, vz, a, p, p2, rw, stream, Mr, lin, &n_rd, &n_wr);
+            integ_apply_pair<RGB>(v, v2, dm, z, ok, e, e2, vx, vy, vz, a, p, p2, rw, stream || TF_INTEG_NT_STORES, Mr, lin, &n_rd, &n_wr);
             e = ne; e2 = ne2; ne = nne; ne2 = nne2; nid1 = nn1; nid2 = nn2;
             v = vn; v2 = vn2; p = pn; p2 = pn2;
 #pragma unroll
@@ -1084,8 +1100,9 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
         for (int row = 0; row < 4; ++row)
             a.D[4 * col + row] = row < 3 ? d[4 * row + col] : (col == 3 ? 1.0f : 0.0f);
     EdArgs ed = {};
-    // 2048 workgroups, 8 per CU (7 are resident at once under the SGPR budget): measured faster
-    // on the C3I scene than a grid of exactly the resident count (2.43 vs 2.75 ms)
+    // stand-alone: 2560 workgroups, two rounds of the 5 per CU that k_integrate_pass's register
+    // budget keeps resident (C3I 2.354 -> 2.317 ms against 2048 at 4 per CU; one round of exactly
+    // the resident count: 2.43 ms; profiles/r04/ab_integ_pass_waves.txt)
     const int nwg = frame_path ? c->integ_wg_frame : TF_INTEG_WG;
     long long* count = (frame_path ? c->count_lanes : 1) ? c->integ_cnt : nullptr;
     const dim3 b(256);
@@ -1097,7 +1114,7 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
     } else {
         const dim3 g(nwg);
         if (rgb) tf_launch(c, k_integrate<false, true>, g, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
-        else tf_launch(c, k_integrate<false, false>, g, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
+        else tf_launch(c, k_integrate_pass, g, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
     }
     return hipGetLastError();
 }
