@@ -785,23 +785,38 @@ __device__ __forceinline__ unsigned integ_u8(float v)
 // computeUpdatedVoxelColorInfo (SceneReconstructionEngine.hpp:116-148) on one colour word
 // (r | g << 8 | b << 16 | w << 24) with interpolateBilinear (PixelUtils.hpp:8-32) of the RGB image;
 // canonical arithmetic.  A NaN image position (pc.z == 0: undefined in the reference) is skipped.
-__device__ __forceinline__ unsigned integ_colour(unsigned clr, float px, float py, float pz, const float* Mr,
-                                                 const IntegArgs& a)
+// its two halves: the image position and the four bilinear samples (issued, not waited for),
+// then the running average once they have arrived.  Every sample of an in-image position is in
+// bounds (x0 <= W - 2, y0 <= H - 2), so the four loads are unconditional and a zero weight
+// selects the reference's zero sample instead.
+struct IntegRgbTap {
+    uchar4 A, B, C, D;
+    float dx, dy;
+    bool ok;
+};
+__device__ __forceinline__ void integ_colour_fetch(float px, float py, float pz, const float* Mr, const IntegArgs& a,
+                                                   IntegRgbTap& t)
 {
     float pc[3];
     tf_m4v3(Mr, px, py, pz, 1.0f, pc);
     const float ix = a.rfx * pc[0] / pc[2] + a.rcx;
     const float iy = a.rfy * pc[1] / pc[2] + a.rcy;
-    if (!(ix >= 1 && ix <= (float)(a.W - 2) && iy >= 1 && iy <= (float)(a.H - 2))) return clr;
-    const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
-    const float dx = ix - (float)x0, dy = iy - (float)y0;
+    t.ok = ix >= 1 && ix <= (float)(a.W - 2) && iy >= 1 && iy <= (float)(a.H - 2);
+    const int x0 = t.ok ? (int)floorf(ix) : 1, y0 = t.ok ? (int)floorf(iy) : 1;
+    t.dx = ix - (float)x0; t.dy = iy - (float)y0;
     const uchar4* r0 = (const uchar4*)((const char*)a.rgb + (size_t)y0 * a.rgb_pitch);
     const uchar4* r1 = (const uchar4*)((const char*)r0 + a.rgb_pitch);
+    t.A = r0[x0]; t.B = r0[x0 + 1]; t.C = r1[x0]; t.D = r1[x0 + 1];
+}
+__device__ __forceinline__ unsigned integ_colour_apply(unsigned clr, const IntegRgbTap& t, const IntegArgs& a)
+{
+    if (!t.ok) return clr;
+    const float dx = t.dx, dy = t.dy;
     const uchar4 z4 = make_uchar4(0, 0, 0, 0);
-    const uchar4 A = r0[x0];
-    const uchar4 B = (dx != 0) ? r0[x0 + 1] : z4;
-    const uchar4 C = (dy != 0) ? r1[x0] : z4;
-    const uchar4 D = (dx != 0 && dy != 0) ? r1[x0 + 1] : z4;
+    const uchar4 A = t.A;
+    const uchar4 B = (dx != 0) ? t.B : z4;
+    const uchar4 C = (dy != 0) ? t.C : z4;
+    const uchar4 D = (dx != 0 && dy != 0) ? t.D : z4;
     const float oldW = (float)(clr >> 24);
     const float ax = 1.0f - dx, ay = 1.0f - dy;
     const float av[3] = { (float)A.x, (float)A.y, (float)A.z }, bv[3] = { (float)B.x, (float)B.y, (float)B.z };
@@ -894,13 +909,19 @@ __device__ __forceinline__ void integ_apply_pair(uint4 v, uint4 v2, const float 
             for (int k = 0; k < 4; ++k) gate |= (integ_colour_gate(eta[4 * b + k], a) ? 1u : 0u) << k;
             if (!gate) continue;                   // most lanes: no voxel in the colour band
             uint4* cp = (uint4*)(a.vba_rgb + (size_t)h.ptr * TF_BLK3 + lin);
-            uint4 c4 = *cp;
-            unsigned cw[4] = { c4.x, c4.y, c4.z, c4.w };
+            const uint4 c4 = *cp;
             const int gx = h.x * TF_BLK, gy = h.y * TF_BLK, gz = h.z * TF_BLK;
             const float py = (float)(gy + vy) * a.voxelSize, pz = (float)(gz + vz) * a.voxelSize;
+            // the colour word and every gated voxel's samples in flight together: one round
+            // trip per block, not one per voxel
+            IntegRgbTap tap[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (gate & (1u << k)) cw[k] = integ_colour(cw[k], (float)(gx + vx + k) * a.voxelSize, py, pz, Mr, a);
+                if (gate & (1u << k)) integ_colour_fetch((float)(gx + vx + k) * a.voxelSize, py, pz, Mr, a, tap[k]);
+            unsigned cw[4] = { c4.x, c4.y, c4.z, c4.w };
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (gate & (1u << k)) cw[k] = integ_colour_apply(cw[k], tap[k], a);
             *cp = make_uint4(cw[0], cw[1], cw[2], cw[3]);
         }
     }
@@ -936,6 +957,17 @@ k_integrate(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restr
 #else
     integ_body<WITH_ED, RGB>(a, st, hash, visibleIds, vba, ed, cnt);
 #endif
+}
+// the frame path with the colour TSDF: its own register budget (TF_INTEG_RGB_WAVES waves per
+// SIMD), so that the frame grid's workgroups are resident together
+#ifndef TF_INTEG_RGB_WAVES
+#define TF_INTEG_RGB_WAVES 3
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TF_INTEG_RGB_WAVES)))
+k_integrate_rgb(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+                const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed, long long* __restrict__ cnt)
+{
+    integ_body<true, true>(a, st, hash, visibleIds, vba, ed, cnt);
 }
 // the stand-alone depth-only pass (stage entry points, C3I): its own register budget, so that
 // TF_INTEG_PASS_WAVES waves per SIMD are resident on a list of millions of blocks
@@ -1109,7 +1141,7 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
     if (with_ed) {
         tf_ed_args(c, &ed);
         const dim3 ge(nwg + TF_ED_BLOCKS);
-        if (rgb) tf_launch(c, k_integrate<true, true>, ge, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
+        if (rgb) tf_launch(c, k_integrate_rgb, ge, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
         else tf_launch(c, k_integrate<true, false>, ge, b, 0, a, c->st, c->hash, c->visibleIds, c->vba, ed, count);
     } else {
         const dim3 g(nwg);
