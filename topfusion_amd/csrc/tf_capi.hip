@@ -151,7 +151,7 @@ static void ctx_free(tf_ctx* c)
     }
     if (c->caller_ev) (void)hipEventDestroy(c->caller_ev);
     void* bufs[] = { c->hash, c->excessList, c->vba_guard, c->allocList, c->bgrid, c->allocType, c->winnerKey, c->allocCounts,
-                     c->visCounts, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
+                     c->visCounts, c->visAgg, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->edBins, c->edBinCnt, c->edDone, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
                      c->vba_rgb_guard, c->rgb_in, c->integ_cnt, c->fuse_pose, c->fuse_rec, c->tile_cost, c->tile_order };
@@ -261,6 +261,12 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     ALLOC(c->winnerKey, sizeof(int) * ntot_pad);
     ALLOC(c->allocCounts, sizeof(int) * 2 * (size_t)c->alloc_chunks);
     ALLOC(c->visCounts, sizeof(int) * (size_t)c->vis_chunks);
+    ALLOC(c->visAgg, sizeof(unsigned long long) * (size_t)c->vis_chunks);
+    {   // TFUSION_VIS_FUSED=0: the two-launch visible-list build (A/B)
+        const char* env = getenv("TFUSION_VIS_FUSED");
+        c->vis_fused = !(env && env[0] == '0');
+        c->vis_gen = 0;
+    }
     ALLOC(c->visibleIds, sizeof(int) * (size_t)pin->vis_capacity);
     ALLOC(c->visType, ntot_pad);
     ALLOC(c->range, sizeof(float) * 2 * npx);
@@ -379,6 +385,7 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)c->vba_guard, 0x7fff, TF_BLK3, c->stream);   // Voxel_s()
     if (e == hipSuccess) e = hipMemsetAsync(c->icp_tagged, 0, sizeof(unsigned long long) * TF_ICP_TAG_WORDS, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->integ_cnt, 0, sizeof(long long) * 2 * TF_INTEG_WG, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->visAgg, 0, sizeof(unsigned long long) * (size_t)c->vis_chunks, c->stream);   // no tag yet
     if (e == hipSuccess) e = hipMemsetAsync(c->allocType, 0, ntot_pad, c->stream);
     if (e == hipSuccess) e = hipMemsetAsync(c->winnerKey, 0xff, sizeof(int) * ntot_pad, c->stream);
     // the request pass counts into these; every frame's k_vis_count returns them to zero

@@ -292,6 +292,9 @@ struct tf_ctx {
     int* winnerKey;          // per-entry last-writer key (pixel*64+step), replaces blockCoords races
     int* allocCounts;        // per-chunk counts (2 ints per chunk)
     int* visCounts;
+    unsigned long long* visAgg;   // [vis_chunks] k_vis_build's tagged chunk counts (generation << 32 | count)
+    unsigned vis_gen;        // k_vis_build launches so far (the tag of the next one's counts)
+    int vis_fused;           // one k_vis_build launch instead of k_vis_count + k_vis_apply (TFUSION_VIS_FUSED)
     // RenderState_VH
     int* visibleIds;
     unsigned char* visType;

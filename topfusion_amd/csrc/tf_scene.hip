@@ -556,12 +556,13 @@ k_alloc_discard(TfDevState* __restrict__ st, const int* __restrict__ counts, uns
 // buildVisibleList_device<false> (SceneReconstructionEngine_host.cu:434-479) with
 // checkBlockVisibility<false> (SceneReconstructionEngine.hpp:300-375), ordered compaction
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
-k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
-            unsigned char* __restrict__ visType, int* __restrict__ counts, int* __restrict__ allocCounts,
-            unsigned char* __restrict__ swapState)
+// one chunk of the count pass: allocation counters reset, type 4 -> 0, swap states marked; the
+// thread's 16 types after the clean-up in lo / hi, its count of listed entries returned
+__device__ __forceinline__ int vis_count_chunk(const VisArgs& v, TfDevState* __restrict__ st,
+                                               unsigned char* __restrict__ visType, int* __restrict__ allocCounts,
+                                               unsigned char* __restrict__ swapState, unsigned long long& lo_out,
+                                               unsigned long long& hi_out)
 {
-    if (st->abort) return;
     if (threadIdx.x == 0) {
         // this frame's allocation is done: its chunk counters go back to zero for the next
         // frame's requests, and (without exhaustion) the free-list counters drop by the totals
@@ -578,6 +579,7 @@ k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restric
     }
     const int base = blockIdx.x * CHUNK + threadIdx.x * 16;
     int cnt = 0;
+    lo_out = 0; hi_out = 0;
     if (base < v.n_total) {
         unsigned long long lo, hi;
         load16(visType + base, &lo, &hi);
@@ -591,6 +593,7 @@ k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restric
             }
             cnt += t > 0;
         }
+        lo_out = lo; hi_out = hi;
         if (dirty) *(uint4*)(visType + base) = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
         if (swapState) {
             // buildVisibleList_device<true> (SceneReconstructionEngine_host.cu:466-469): every
@@ -608,6 +611,17 @@ k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restric
             if (sdirty) *(uint4*)(swapState + base) = make_uint4((unsigned)slo, (unsigned)(slo >> 32), (unsigned)shi, (unsigned)(shi >> 32));
         }
     }
+    return cnt;
+}
+
+__global__ void __launch_bounds__(256)
+k_vis_count(VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+            unsigned char* __restrict__ visType, int* __restrict__ counts, int* __restrict__ allocCounts,
+            unsigned char* __restrict__ swapState)
+{
+    if (st->abort) return;
+    unsigned long long lo, hi;
+    const int cnt = vis_count_chunk(v, st, visType, allocCounts, swapState, lo, hi);
     int tot = block_sum(cnt);
     if (threadIdx.x == 0) counts[blockIdx.x] = tot;
 }
@@ -638,6 +652,55 @@ k_vis_apply(VisArgs v, TfDevState* __restrict__ st, int n_chunks, const int* __r
     for (int i = 0; i < 16; ++i) {
         if (byte16(lo, hi, i) > 0) {
             if (r < v.cap) visibleIds[r] = base + i;
+            r++;
+        }
+    }
+}
+
+// k_vis_count + k_vis_apply in one launch: each workgroup counts its chunk, publishes the count
+// tagged with this launch's generation (agent scope: the readers are on every XCD), waits for
+// the counts of every lower chunk and compacts its own entries at their sum -- the same list in
+// the same order.  A workgroup waits only on lower-indexed ones, which were dispatched before it,
+// so the wait always ends; a bounded spin still turns a lost count into the frame's sticky error.
+// The last workgroup, which has waited on all the others, writes noVisibleEntries.
+__global__ void __launch_bounds__(256)
+k_vis_build(VisArgs v, TfDevState* __restrict__ st, unsigned char* __restrict__ visType,
+            int* __restrict__ allocCounts, unsigned char* __restrict__ swapState, unsigned long long* __restrict__ agg,
+            unsigned gen, int* __restrict__ visibleIds)
+{
+    if (st->abort) return;
+    unsigned long long lo, hi;
+    const int cnt = vis_count_chunk(v, st, visType, allocCounts, swapState, lo, hi);
+    int own;
+    int r = block_excl_scan(cnt, &own);
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&agg[blockIdx.x], ((unsigned long long)gen << 32) | (unsigned)own, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    int pre = 0;
+    bool lost = false;
+    for (int h = threadIdx.x; h < (int)blockIdx.x; h += 256) {
+        unsigned long long x;
+        unsigned spins = 0;
+        while (((x = __hip_atomic_load(&agg[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != gen) {
+            if (++spins > (1u << 22)) { lost = true; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        pre += (int)(unsigned)x;
+    }
+    pre = block_sum(pre);
+    if (__syncthreads_or(lost)) {
+        if (threadIdx.x == 0) st->icp_ok = -2;           // the frame end: a sticky HIP error
+        return;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        const int all = pre + own;
+        st->noVisibleEntries = all < v.cap ? all : v.cap;
+    }
+    if (!cnt) return;
+    r += pre;
+    for (int i = 0; i < 16; ++i) {
+        if (byte16(lo, hi, i) > 0) {
+            if (r < v.cap) visibleIds[r] = blockIdx.x * CHUNK + threadIdx.x * 16 + i;
             r++;
         }
     }
@@ -691,10 +754,15 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch, int onl
         hipLaunchKernelGGL(k_alloc_apply, dim3(c->alloc_chunks), dim3(256), 0, c->stream, a, c->st, c->alloc_chunks,
                            c->allocCounts, c->allocType, c->winnerKey, c->hash, c->visType, c->allocList, c->excessList,
                            c->n_total);
-    hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
-                       c->visCounts, c->allocCounts, swapping ? c->swapState : nullptr);
-    hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
-                       c->visCounts, c->visType, c->visibleIds);
+    if (c->vis_fused) {
+        hipLaunchKernelGGL(k_vis_build, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->visType,
+                           c->allocCounts, swapping ? c->swapState : nullptr, c->visAgg, ++c->vis_gen, c->visibleIds);
+    } else {
+        hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
+                           c->visCounts, c->allocCounts, swapping ? c->swapState : nullptr);
+        hipLaunchKernelGGL(k_vis_apply, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->vis_chunks,
+                           c->visCounts, c->visType, c->visibleIds);
+    }
     if (swapping) return tfk_swap_realloc(c);      // reAllocateSwappedOutVoxelBlocks (:184-189)
     if (c->p.use_swapping)                         // (an onlyUpdateVisibleList pass reallocates nothing)
         return hipMemsetAsync(&c->st->swap_realloc, 0, sizeof(int), c->stream);
