@@ -8,10 +8,11 @@ renderImage raycast, CreateExpectedDepths and the CreateICPMaps raycast.  Frames
 the synthetic 640x480 orbit sequence (topfusion_amd/synth.py, seed 7 + rank), uploaded
 to HBM before the timed region.  One process per GPU; each rank tracks its own
 independent stream (replicas, weak scaling) and the per-rank frame counts / times are
-combined with one RCCL all-reduce.
+combined by RCCL all-reduces (topfusion_amd/replicas.py: librccl through ctypes on the
+product's own HIP runtime; no torch in a GPU process).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    python bench.py [--gpus N] [--steps K] [--warmup W]       (N > 1: this process starts N ranks)
+    torchrun --nproc-per-node N bench.py --gpus N ...          (each rank started by torchrun)
 """
 import argparse
 import json
@@ -86,6 +87,12 @@ def parse():
                     help="timed region: HIP events around the dominant kernel on every N-th frame only "
                          "(an event pair is a few us of dispatch gap; 1 = every frame)")
     ap.add_argument("--breakdown-frames", type=int, default=64, help="frames of the per-stage timing pass")
+    ap.add_argument("--collective", choices=["rccl", "file"], default="rccl",
+                    help="N > 1: how the ranks combine their numbers -- RCCL all-reduces (default) or the host-side "
+                         "file group (topfusion_amd/replicas.py)")
+    ap.add_argument("--standin", action="store_true",
+                    help="CPU stand-in workload (tests): each rank runs the oracle over a few 80x60 orbit frames; "
+                         "same launcher and line, file collective, no GPU")
     return ap.parse_args()
 
 
@@ -224,20 +231,6 @@ def cpu_baseline_protocol(frames, first, params_kw, seconds, nt):
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
             "cores_note": ("OMP_NUM_THREADS: the GPU pool gives a one-GPU job a share of the host's CPUs (16 of the "
                            "machine's, which the 8 GPUs' jobs share); nproc / affinity show the whole machine")}
-
-
-def combine_ranks(elapsed, frames, device, world):
-    """Whole-job numbers from per-rank ones: the slowest rank's time (MAX) and the frames of all
-    ranks (SUM); one small all-reduce per op over RCCL (gloo in the CPU tests)."""
-    if world <= 1:
-        return float(elapsed), float(frames)
-    import torch
-    import torch.distributed as dist
-    mx = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-    sm = torch.tensor([float(frames)], dtype=torch.float64, device=device)
-    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-    return float(mx[0]), float(sm[0])
 
 
 def c3_scene():
@@ -437,18 +430,8 @@ def c5e_bench(args):
     and every later frame's new blocks fail silently (SceneReconstructionEngine_host.cu:358-413).
     A step is one tf_scene_fuse_frames batch of F frames; the per-frame records give the allocated
     blocks, the failed requests and (swapping) the evictions / merges of every frame."""
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:                      # torch's HIP runtime first (it must initialise before the product's)
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+    rank, local_rank, world, rep = rank_setup(args)
     from topfusion_amd import TopFu, default_params, synth
-    from topfusion_amd import _lib as L
-    L.check(L.load().tf_set_device(local_rank), "tf_set_device")
     F = args.frames_per_step or 1000
     steps = args.steps if args.steps is not None else 50
     warm = args.warmup if args.warmup is not None else 1
@@ -469,16 +452,16 @@ def c5e_bench(args):
     for k in range(warm):
         recs.append(tf.fuse_frames(stream.frame_ptr(k * F), w2c[k * F:(k + 1) * F]))
     tf.reset_totals()
-    if dist is not None:
-        dist.barrier()
+    device_sync()
+    rep.barrier()
     step_s = []
     t0 = time.perf_counter()
     for k in range(warm, warm + steps):
         ts = time.perf_counter()
         recs.append(tf.fuse_frames(stream.frame_ptr(k * F), w2c[k * F:(k + 1) * F]))
         step_s.append(time.perf_counter() - ts)
-    if dist is not None:
-        dist.barrier()
+    device_sync()
+    rep.barrier()
     elapsed = time.perf_counter() - t0
     tot = tf.totals()
     rec = np.concatenate(recs)
@@ -489,10 +472,7 @@ def c5e_bench(args):
     # steps whose frames all come after the first failure: the saturated-VBA rate
     sat_steps = [i for i in range(steps) if first_fail is not None and (warm + i) * F >= first_fail]
     sat_s = sum(step_s[i] for i in sat_steps)
-    elapsed_max, total_frames = elapsed, float(steps * F)
-    if dist is not None:
-        import torch
-        elapsed_max, total_frames = combine_ranks(elapsed, steps * F, f"cuda:{local_rank}", world)
+    elapsed_max, total_frames, multi = rep.summary(elapsed, steps * F)
     if rank == 0:
         late = timed[-min(len(timed), 10 * F):]
         allocated = nb - 1 - rec["lastFreeBlockId"]
@@ -525,16 +505,75 @@ def c5e_bench(args):
             "swapped_in_merged_per_frame": round(float(timed["swapped_in_merged"].mean()), 2) if args.swapping else None,
             "swap_realloc_per_frame": round(float(timed["swap_realloc"].mean()), 2) if args.swapping else None,
             "render_s": round(t_render, 2),
+            "multi_gpu": multi if world > 1 else None,
         }
         print(json.dumps(out))
     tf.close()
     stream.free()
-    if dist is not None:
-        dist.destroy_process_group()
+    rep.close()
+
+
+def rank_setup(args):
+    """This process's rank, local rank and world (torchrun's or replicas.launch's environment), the
+    product library on device LOCAL_RANK, and the ranks' collective (topfusion_amd/replicas.py).
+    Exits non-zero when the world differs from --gpus or the node has too few devices."""
+    from topfusion_amd import replicas
+    rank, local_rank, world = replicas.world_from_env()
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launch has WORLD_SIZE {world}")
+    if not args.standin:
+        from topfusion_amd import _lib as L
+        lib = L.load()
+        n_dev = L.device_count()
+        if os.environ.get("TFUSION_RANK_DEVICE_MODULO") == "1" and n_dev > 0:
+            local_rank %= n_dev          # tests only: several ranks on a one-GPU box
+        if local_rank >= n_dev:
+            sys.exit(f"bench.py: rank {rank} needs HIP device {local_rank}, the node has {n_dev}")
+        L.check(lib.tf_set_device(local_rank), "tf_set_device")
+    rep = replicas.Replicas(rank, local_rank, world, kind="file" if args.standin else args.collective)
+    return rank, local_rank, world, rep
+
+
+def standin(args):
+    """CPU stand-in for the launcher tests: each rank runs the oracle (test infrastructure; never a
+    measured GPU number) over a few frames of its own 80x60 orbit stream (seed 7 + rank), then
+    the ranks combine their numbers exactly as the GPU path does, over the file collective."""
+    rank, local_rank, world, rep = rank_setup(args)
+    from oracle import oracle as O
+    from topfusion_amd import synth
+    W, H, n = 80, 60, max(1, args.steps or 2)
+    fx, fy, cx, cy = synth.intrinsics(W, H)
+    frames = synth.orbit_sequence(n, W, H, seed=7 + rank)
+    o = O.Oracle(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy)
+    rep.barrier()
+    t0 = time.perf_counter()
+    ok = sum(bool(o(f)) for f in frames)
+    rep.barrier()
+    elapsed = time.perf_counter() - t0
+    emax, total, multi = rep.summary(elapsed, n)
+    if rank == 0:
+        print(json.dumps({"metric": "stand-in: oracle frames/sec @80x60 (launcher test, not a GPU number)",
+                          "value": round(total / emax, 4), "unit": "frames/s", "n_gpus": world, "steps": n,
+                          "warmup": 0, "ms_per_step": round(emax / n * 1000, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                          "config": {"workload": "standin", "parallelism": f"replicas{world}"},
+                          "frames_ok_rank0": ok, "frame_sum_rank0": int(frames.astype(np.int64).sum()),
+                          "multi_gpu": multi}))
+    rep.close()
 
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and args.config in ("C3I", "C3R"):
+        sys.exit(f"bench.py: --config {args.config} times one stage on one GPU; run it with --gpus 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one fresh process per GPU, started before anything here touches a GPU
+        from topfusion_amd import replicas
+        sys.exit(replicas.launch(os.path.abspath(__file__), sys.argv[1:], args.gpus))
+    if args.standin:
+        return standin(args)
     if args.config == "C5E":
         return c5e_bench(args)
     if args.config == "C3I":
@@ -545,21 +584,8 @@ def main():
         if args.steps is None:
             args.steps = 20
         return c3_raycast(args)
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        # RCCL for the two per-rank numbers only: torch's HIP runtime (its wheel bundles its own
-        # libamdhip64) must initialise before the product's /opt/rocm one; frames, fusion and
-        # timing all run on the product's runtime
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+    rank, local_rank, world, rep = rank_setup(args)
     from topfusion_amd import TopFu, default_params, synth
-    from topfusion_amd import _lib as L
-    L.check(L.load().tf_set_device(local_rank), "tf_set_device")
 
     cfg = CONFIGS[args.config]
     if args.steps is None:
@@ -579,7 +605,6 @@ def main():
         pkw.update(voxel_rgb=1)            # rgb_intr 0 / depth_to_rgb 0: the colour camera registered with the depth one
     n_breakdown = 0 if args.no_profile else min(args.breakdown_frames, args.steps * F)
     n_frames = (args.warmup + args.steps) * F
-    device = f"cuda:{local_rank}"
     seed = (13 if cfg["walk"] else 7) + rank
     dev = (walk_frames if cfg["walk"] else orbit_frames)(n_frames, W, H, seed)
     frame_bytes = W * H * 2
@@ -614,15 +639,13 @@ def main():
     tf.profile(not args.no_profile, stages=[dominant], every=args.profile_every)
     tf.reset_totals()
     device_sync()
-    if world > 1:
-        dist.barrier()
+    rep.barrier()
     t0 = time.perf_counter()
     oks = []
     for k in range(args.steps):
         oks.append(run(tf, (args.warmup + k) * F, F))
     device_sync()
-    if world > 1:
-        dist.barrier()
+    rep.barrier()
     elapsed = time.perf_counter() - t0
     ok = np.concatenate(oks)
     prof_timed = tf.profile_read() if not args.no_profile else {}
@@ -666,7 +689,7 @@ def main():
     c1_gpu = None
     if rgb is None:
         c1 = []
-        for rep in range(6):
+        for _ in range(6):
             t1 = TopFu(default_params(**pkw), device=local_rank)
             device_sync()
             ts = time.perf_counter()
@@ -675,7 +698,7 @@ def main():
             t1.close()
         c1_gpu = 1000.0 * sorted(c1[1:])[2]
     total_steps_frames = args.steps * F
-    elapsed_max, total_frames = combine_ranks(elapsed, total_steps_frames, device, world)
+    elapsed_max, total_frames, multi = rep.summary(elapsed, total_steps_frames)
 
     if rank == 0:
         value = total_frames / elapsed_max
@@ -730,7 +753,7 @@ def main():
                                             "gathers hit L2, so PMC traffic is a fraction of the algorithmic bytes")
         stream_gbs = round(hbm_stream_copy(), 1)
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:        # (rank 0 at N = 1 only)
             # all cores: the OpenMP build of the oracle; 1 thread: the serial build (reported
             # beside); BASELINE.md protocol: one warm-up frame, then the median of 5 repeats of a
             # bounded sample of the same stream
@@ -811,14 +834,14 @@ def main():
             "roofline_stages": roof_all,
             "icp_schedule": "persistent" if tf.icp_persistent() else "per_iteration",
             "cpu_baseline": cpu,
+            "multi_gpu": multi if world > 1 else None,
         }
         print(json.dumps(out))
     tf.close()
     dev.free()
     if rgb is not None:
         rgb.free()
-    if world > 1:
-        dist.destroy_process_group()
+    rep.close()
 
 
 if __name__ == "__main__":

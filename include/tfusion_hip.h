@@ -22,8 +22,11 @@
  * counts it): the caller sees the frame's normal result.  (2) A bounded spin past the ICP that
  * times out leaves the frame half done: the context is in error from then on -- that frame's
  * call, or the next call that synchronises with the device if the frame's call had already
- * returned (per-call frames return on their ICP verdict), and every later call returns
- * TF_HIP_ERROR until tf_reset.
+ * returned (per-call frames return on their ICP verdict), and every later call that
+ * synchronises with the device (downloads, uploads, stage / engine / visualisation calls,
+ * tf_scene_fuse_frames, stats and pose queries) returns TF_HIP_ERROR until tf_reset.  The same
+ * holds for an engine-level call whose visible-list build loses a wait (k_vis_build), which has
+ * no frame end to report it.  An engine batch on a context halted by a failed frame no-ops.
  */
 #ifndef TFUSION_HIP_H
 #define TFUSION_HIP_H

@@ -1,15 +1,21 @@
-"""Multi-process (world_size 2, gloo, CPU) coverage of the N>1 path: bench.py's replicas
-semantics -- each rank tracks its own independent stream (seed 7 + rank), the whole-job
-numbers are MAX over rank times and SUM over rank frames (bench.combine_ranks)."""
+"""Multi-process (world_size 2, CPU) coverage of the N>1 path (SURVEY §8e replicas, BASELINE
+configs[3]): `bench.py --gpus N` starts its own ranks (topfusion_amd/replicas.launch), or runs as
+one rank of a torchrun launch; every rank tracks its own stream (seed 7 + rank) and the job's
+numbers are the MAX of the rank times and the SUM of the rank frames.  The CPU runs use the
+`--standin` workload (the oracle on an 80x60 stream) and the file collective; the RCCL
+collective itself is covered on the GPU (tests/test_gpu_replicas.py)."""
+import ctypes
+import json
 import os
 import socket
+import subprocess
 import sys
+import textwrap
 
-import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def _free_port():
@@ -20,58 +26,131 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TFUSION_RDZV_DIR", "TFUSION_LAUNCHED"):
+        env.pop(k, None)
+    return env
+
+
+def _line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out                      # rank 0 prints the one line
+    return json.loads(lines[0])
+
+
+def _check_line(d, world):
+    m = d["multi_gpu"]
+    assert d["n_gpus"] == world and m["world"] == world and m["collective_nranks"] == world
+    assert d["config"]["parallelism"] == f"replicas{world}"
+    assert len(m["per_rank_frames_per_sec"]) == world
+    assert m["per_rank_frames"] == [d["steps"]] * world
+    emax = max(m["per_rank_elapsed_s"])
+    assert d["value"] == pytest.approx(sum(m["per_rank_frames"]) / emax, rel=1e-3)   # SUM frames / MAX time
+    for fps, e, f in zip(m["per_rank_frames_per_sec"], m["per_rank_elapsed_s"], m["per_rank_frames"]):
+        assert fps == pytest.approx(f / e, rel=1e-2)
+    assert "efficiency" not in json.dumps(d)         # the driver computes scaling itself
+
+
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2`: the parent starts two ranks; one line with n_gpus 2."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--standin", "--steps", "2"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    d = _line(r.stdout)
+    _check_line(d, 2)
+    assert d["multi_gpu"]["collective"] == "file"
+
+
+def test_bench_under_torchrun():
+    """The driver's torchrun form: each rank started by torch.distributed.run; the ranks meet in
+    a directory named after the agent process."""
+    port = _free_port()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--standin", "--steps", "2"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check_line(_line(r.stdout), 2)
+
+
+def test_world_mismatch_exits_nonzero():
+    env = _env()
+    env.update(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--standin"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE 3" in r.stderr
+
+
+def test_launcher_stops_the_job_when_a_rank_fails(tmp_path):
+    """A failing rank ends the job with its status; the other rank (blocked forever) is stopped."""
+    from topfusion_amd import replicas
+    script = tmp_path / "rank.py"
+    script.write_text(textwrap.dedent("""
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(7)
+        time.sleep(600)
+    """))
+    import time
+    t0 = time.monotonic()
+    assert replicas.launch(str(script), [], 2) == 7
+    assert time.monotonic() - t0 < 60
+
+
+def _fg_worker(rank, world, path, q):
     sys.path.insert(0, ROOT)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    import torch.distributed as dist
-    import bench
-    from oracle import oracle as O
-    from topfusion_amd import synth
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        # replica: an independent 80x60 stream per rank through the CPU oracle
-        W, H = 80, 60
-        fx, fy, cx, cy = synth.intrinsics(W, H)
-        frames = synth.orbit_sequence(3, W, H, seed=7 + rank)
-        o = O.Oracle(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy)
-        n_ok = sum(bool(o(f)) for f in frames)
-        elapsed = 1.0 + rank                  # deterministic stand-in times
-        emax, total = bench.combine_ranks(elapsed, len(frames), "cpu", world)
-        q.put((rank, emax, total, n_ok, int(frames.astype(np.int64).sum())))
-    finally:
-        dist.destroy_process_group()
+    from topfusion_amd import replicas
+    g = replicas.FileGroup(rank, world, path)
+    mx = g.allreduce([1.0 + rank, -rank], "max")
+    sm = g.allreduce([1.0 + rank, 10.0], "sum")
+    ag = g.allgather([rank, rank * 2])
+    g.barrier()
+    g.close()
+    q.put((rank, mx, sm, ag))
 
 
-def test_replicas_combine_world2():
-    world = 2
+def test_file_group_collectives(tmp_path):
+    import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_fg_worker, args=(r, 3, str(tmp_path), q)) for r in range(3)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
+    res = sorted(q.get(timeout=120) for _ in range(3))
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res.sort()
-    for rank, emax, total, n_ok, _ in res:
-        assert emax == 2.0                     # slowest rank
-        assert total == 6.0                    # frames of all ranks
-        assert n_ok >= 1
-    assert res[0][4] != res[1][4]              # independent streams (seed 7 + rank)
+    for rank, mx, sm, ag in res:
+        assert mx == [3.0, 0.0]
+        assert sm == [6.0, 30.0]
+        assert ag == [[0, 0], [1, 2], [2, 4]]
 
 
 def test_single_rank_passthrough():
-    sys.path.insert(0, ROOT)
-    import bench
-    assert bench.combine_ranks(0.5, 10, "cpu", 1) == (0.5, 10.0)
+    from topfusion_amd import replicas
+    rep = replicas.Replicas(0, 0, 1)
+    emax, total, multi = rep.summary(0.5, 10)
+    assert (emax, total) == (0.5, 10.0) and multi["world"] == 1
+    rep.close()
+
+
+def test_rccl_symbols_present():
+    """The RCCL entry points RcclGroup binds exist in /opt/rocm/lib/librccl.so (loaded, not called:
+    no GPU here)."""
+    from topfusion_amd import replicas
+    if not os.path.exists(replicas.RCCL_PATH):
+        pytest.skip("no librccl in this image")
+    lib = ctypes.CDLL(replicas.RCCL_PATH)
+    for f in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclAllGather", "ncclCommCount",
+              "ncclCommDestroy", "ncclGetErrorString"):
+        assert hasattr(lib, f), f
+    assert ctypes.sizeof(replicas._UniqueId) == 128
 
 
 def test_every_bench_config_has_a_runner():
     """Each --config choice of bench.py dispatches to a function the module defines (a config
     whose runner went missing would only fail on the GPU box)."""
-    sys.path.insert(0, ROOT)
     import bench
     import inspect
     src = inspect.getsource(bench.main)

@@ -68,13 +68,41 @@ def test_error_past_icp_is_sticky(monkeypatch, mode):
         with pytest.raises(L.TfError) as ei:
             g(dev.ptr + 3 * fb)                            # reported by the next call
         assert ei.value.status == L.TF_HIP_ERROR
-    for call in (g.stats, g.getCameraPose, lambda: g(dev.ptr)):
-        with pytest.raises(L.TfError) as ei:               # sticky: every call until tf_reset
-            call()
+    I = np.tile(np.eye(4, dtype=np.float32)[:3], (2, 1, 1))
+    for call in (g.stats, g.getCameraPose, lambda: g(dev.ptr), g.hash, g.vba,
+                 lambda: g.fuse_frames(dev.ptr, I)):
+        with pytest.raises(L.TfError) as ei:               # sticky: every call until tf_reset (ADVICE r4:
+            call()                                         # downloads and engine batches too)
         assert ei.value.status == L.TF_HIP_ERROR
     g.reset()
     ok = g.process_frames(dev.ptr, N)                      # the context works again
     assert ok.all()
     assert g.stats()["frame_counter"] == N
+    g.close()
+    dev.free()
+
+
+def test_vis_build_lost_wait_is_sticky_on_engine_path(monkeypatch):
+    """TFUSION_VIS_FAULT=l: the l-th k_vis_build launch's wait for the lower chunks' counts fails.
+    An engine-level batch (tf_scene_fuse_frames) has no frame end, so the kernel itself marks the
+    context in error: the batch and every later call report TF_HIP_ERROR until tf_reset
+    clears it."""
+    from topfusion_amd import TopFu, default_params, _lib as L
+    monkeypatch.setenv("TFUSION_VIS_FAULT", "2")
+    fx, fy, cx, cy = synth.intrinsics(W, H)
+    g = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy))
+    frames = np.stack([synth.room_corner(W, H, seed=42 + k) for k in range(3)])
+    dev = DeviceFrames(frames)
+    I = np.tile(np.eye(4, dtype=np.float32)[:3], (3, 1, 1))
+    with pytest.raises(L.TfError) as ei:
+        g.fuse_frames(dev.ptr, I)
+    assert ei.value.status == L.TF_HIP_ERROR
+    for call in (g.stats, g.hash, lambda: g.fuse_frames(dev.ptr, I[:1])):
+        with pytest.raises(L.TfError) as ei:
+            call()
+        assert ei.value.status == L.TF_HIP_ERROR
+    g.reset()
+    rec = g.fuse_frames(dev.ptr, I)                        # the fault fired once: the context works again
+    assert (rec["noVisibleEntries"] > 0).all()
     g.close()
     dev.free()

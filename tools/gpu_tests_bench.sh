@@ -6,7 +6,7 @@ cd $R
 TAG=${1:-t}; shift || true
 SEL=${@:-tests}
 mkdir -p gpurun_out/$TAG
-timeout -k 10 700 python -u -m pytest $SEL -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/$TAG/tests.log 2>&1 || { tail -40 gpurun_out/$TAG/tests.log; exit 1; }
+timeout -k 10 700 python -u -m pytest $SEL -m gpu -x -q -rs --timeout 400 --timeout-method thread > gpurun_out/$TAG/tests.log 2>&1 || { tail -40 gpurun_out/$TAG/tests.log; exit 1; }
 tail -1 gpurun_out/$TAG/tests.log
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/$TAG/bench.log 2>&1 || { tail -20 gpurun_out/$TAG/bench.log; exit 1; }
 python -c "

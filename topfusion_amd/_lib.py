@@ -192,6 +192,13 @@ def check(status, where, allow=(TF_OK,)):
     return status
 
 
+def device_count():
+    """HIP devices visible to this process (tf_device_count)."""
+    n = ctypes.c_int(0)
+    check(load().tf_device_count(ctypes.byref(n)), "tf_device_count")
+    return n.value
+
+
 def default_params(**kw):
     p = TfParams()
     check(load().tf_default_params(ctypes.byref(p)), "tf_default_params")

@@ -199,6 +199,17 @@ static tf_status sync_state(tf_ctx* c)
     return TF_OK;
 }
 
+// the end of every synchronous entry point: wait for the stream, then report a context left in
+// error by a device-side failure past an ICP (tf_reset.h: frame_ok -3) or by an engine-level
+// launch's failed wait (k_vis_build) -- TF_HIP_ERROR from every call until tf_reset
+static tf_status sync_checked(tf_ctx* c)
+{
+    TF_CHECK(hipMemcpyAsync(&c->st_host->sticky_error, &c->st->sticky_error, sizeof(int), hipMemcpyDeviceToHost,
+                            c->stream));
+    TF_CHECK(hipStreamSynchronize(c->stream));
+    return c->st_host->sticky_error ? TF_HIP_ERROR : TF_OK;
+}
+
 // TopFu::reset (topfu.cpp:141-152): pose history -> [I], ResetScene.  The render state
 // (visible list / types / range image) is deliberately left as is, like the reference.
 __global__ void k_host_reset(TfDevState* st)
@@ -366,6 +377,9 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         // (past the ICP: the sticky-error path)
         env = getenv("TFUSION_FILL_FAULT");
         c->fill_fault_launch = env ? atoll(env) : 0;
+        // TFUSION_VIS_FAULT=launch: that k_vis_build launch's wait for the lower chunks' counts fails
+        env = getenv("TFUSION_VIS_FAULT");
+        c->vis_fault_launch = env ? atoll(env) : 0;
     }
     {   // TFUSION_PERCALL_EARLY=0: per-call frames wait for the whole frame; TFUSION_PERCALL_DEFER=0:
         // they enqueue all their launches (A/B)
@@ -953,8 +967,7 @@ extern "C" tf_status tf_render_image_type(tf_ctx* c, int type, uint8_t* dev_rgba
         TF_CHECK(hipMemcpy2DAsync(dev_rgba, pitch, c->grey, (size_t)c->W * 4, (size_t)c->W * 4, c->H,
                                   hipMemcpyDeviceToDevice, c->stream));
     }
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_get_pose(tf_ctx* c, float rt[12])
@@ -1014,8 +1027,7 @@ extern "C" tf_status tf_stage_preprocess(tf_ctx* c, const uint16_t* dev_depth, s
     TF_CHECK(clear_abort(c));
     TF_CHECK(tfk_preprocess(c, dev_depth, pitch, c->stream, c->d0_buf[0]));
     c->depth_pyr[0] = c->d0_buf[0];
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_stage_preprocess_host(tf_ctx* c, const uint16_t* host_depth, size_t pitch)
@@ -1052,8 +1064,7 @@ extern "C" tf_status tf_stage_alloc(tf_ctx* c, const float pose_rt[12])
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_alloc(c));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_stage_integrate(tf_ctx* c, const float pose_rt[12])
@@ -1064,8 +1075,7 @@ extern "C" tf_status tf_stage_integrate(tf_ctx* c, const float pose_rt[12])
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_integrate(c));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_stage_expected_depths(tf_ctx* c, const float pose_rt[12])
@@ -1076,8 +1086,7 @@ extern "C" tf_status tf_stage_expected_depths(tf_ctx* c, const float pose_rt[12]
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_expected_depths(c));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_stage_raycast(tf_ctx* c, const float invM_rt[12], int update_visible)
@@ -1088,8 +1097,7 @@ extern "C" tf_status tf_stage_raycast(tf_ctx* c, const float invM_rt[12], int up
     tf_status s = set_pose_in(c, invM_rt, 0);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_raycast(c, update_visible));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_stage_icp_maps(tf_ctx* c, const float invM_rt[12])
@@ -1100,8 +1108,7 @@ extern "C" tf_status tf_stage_icp_maps(tf_ctx* c, const float invM_rt[12])
     tf_status s = set_pose_in(c, invM_rt, 0);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_icp_maps(c));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
@@ -1112,8 +1119,7 @@ extern "C" tf_status tf_stage_render_grey(tf_ctx* c, const float invM_rt[12])
     tf_status s = set_pose_in(c, invM_rt, 0);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_render_type(c, TF_RENDER_SHADED_GREYSCALE));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_time_stage(tf_ctx* c, int stage, const float pose_rt[12], int iters, float* ms_per_iter)
@@ -1156,8 +1162,7 @@ extern "C" tf_status tf_stage_reset_scene(tf_ctx* c)
     TF_FLUSH(c);
     if (!c) return TF_INVALID_ARG;
     TF_CHECK(tfk_reset_scene(c, 0));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_stage_swap_pyramids(tf_ctx* c)
@@ -1269,8 +1274,7 @@ extern "C" tf_status tf_scene_alloc(tf_ctx* c, const float intr[4], const float 
                                 hipMemcpyHostToDevice, c->stream));
     }
     TF_CHECK(tfk_alloc(c, 0, TfAhead{}, 0, only_update_visible_list ? 1 : 0));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_scene_integrate(tf_ctx* c, const float intr[4], const float pose_rt[12], const float* dists,
@@ -1284,8 +1288,7 @@ extern "C" tf_status tf_scene_integrate(tf_ctx* c, const float intr[4], const fl
     tf_status s = set_pose_in(c, pose_rt, TF_POSE_ALLOC_NOINV);
     if (s != TF_OK) return s;
     TF_CHECK(tfk_integrate(c));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_scene_integrate_rgb(tf_ctx* c, const float intr[4], const float pose_rt[12], const float* dists,
@@ -1304,8 +1307,7 @@ static tf_status scene_swap(tf_ctx* c, int which)
     if (!c->p.use_swapping) return TF_INVALID_ARG;
     TF_CHECK(clear_abort(c));
     TF_CHECK(tfk_swap(c, which));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_scene_swap(tf_ctx* c) { TF_FLUSH(c); return scene_swap(c, 3); }
@@ -1337,8 +1339,7 @@ extern "C" tf_status tf_scene_fuse_frames(tf_ctx* c, const float intr[4], const 
     TF_CHECK(tfk_fuse_frames(c, dev_frames, stride, pitch, n));
     if (records)
         TF_CHECK(hipMemcpyAsync(records, c->fuse_rec, sizeof(tf_fuse_record) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_swap_counts(tf_ctx* c, int counts[3])
@@ -1362,8 +1363,8 @@ extern "C" tf_status tf_swap_save(tf_ctx* c, const char* path)
     if (!host) return TF_OOM;
     hipError_t e = hipMemcpyAsync(host, c->swapFlags, nf, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync((char*)host + nf, c->swapStore, nv, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     tf_status s = tf_from_hip(e);
+    if (s == TF_OK) s = sync_checked(c);
     if (s == TF_OK) {
         FILE* f = fopen(path, "wb");
         if (!f || fwrite(host, 1, nf + nv, f) != nf + nv) s = TF_INVALID_ARG;
@@ -1418,8 +1419,7 @@ extern "C" tf_status tf_vis_render_image(tf_ctx* c, const float intr[4], const f
         const size_t row = (size_t)c->W * 4;
         TF_CHECK(hipMemcpy2DAsync(dev_rgba, step ? step : row, c->grey, row, row, c->H, hipMemcpyDeviceToDevice, c->stream));
     }
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_vis_icp_maps(tf_ctx* c, const float intr[4], const float pose_rt[12], void* points,
@@ -1440,8 +1440,7 @@ extern "C" tf_status tf_vis_icp_maps(tf_ctx* c, const float intr[4], const float
     if (normals)
         TF_CHECK(hipMemcpy2DAsync(normals, normals_step ? normals_step : row, c->prev_nrm[0], row, row, c->H,
                                   hipMemcpyDeviceToDevice, c->stream));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 // ---- state transfer -------------------------------------------------------------------
@@ -1490,8 +1489,7 @@ extern "C" tf_status tf_download(tf_ctx* c, int which, int level, void* host, si
     void* p = buffer_ptr(c, which, level, &n);
     if (!p || n != bytes) return TF_INVALID_ARG;
     TF_CHECK(hipMemcpyAsync(host, p, n, hipMemcpyDeviceToHost, c->stream));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_download_range(tf_ctx* c, int which, size_t offset, void* host, size_t bytes)
@@ -1502,8 +1500,7 @@ extern "C" tf_status tf_download_range(tf_ctx* c, int which, size_t offset, void
     void* p = buffer_ptr(c, which, 0, &n);
     if (!p || offset > n || bytes > n - offset) return TF_INVALID_ARG;
     TF_CHECK(hipMemcpyAsync(host, (const char*)p + offset, bytes, hipMemcpyDeviceToHost, c->stream));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host, size_t bytes)
@@ -1520,8 +1517,7 @@ extern "C" tf_status tf_upload(tf_ctx* c, int which, int level, const void* host
     if (which == TF_BUF_HASH || which == TF_BUF_VBA || which == TF_BUF_VBA_RGB || which == TF_BUF_ALLOC_LIST ||
         which == TF_BUF_EXCESS_LIST)                               // next reset (in-frame ones too): full clear
         TF_CHECK(hipMemcpyAsync((char*)c->st + offsetof(TfDevState, scene_external), &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_set_pose(tf_ctx* c, const float rt[12])
@@ -1529,8 +1525,7 @@ extern "C" tf_status tf_set_pose(tf_ctx* c, const float rt[12])
     TF_FLUSH(c);
     if (!c || !rt) return TF_INVALID_ARG;
     TF_CHECK(hipMemcpyAsync(c->st->pose, rt, sizeof(float) * 12, hipMemcpyHostToDevice, c->stream));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_set_counters(tf_ctx* c, int lastFreeBlockId, int lastFreeExcessListId, int noVisibleEntries)
@@ -1544,8 +1539,7 @@ extern "C" tf_status tf_set_counters(tf_ctx* c, int lastFreeBlockId, int lastFre
     c->st_host->noVisibleEntries = noVisibleEntries;
     c->st_host->scene_external = 1;                                 // next reset: full clear
     TF_CHECK(hipMemcpyAsync(c->st, c->st_host, sizeof(TfDevState), hipMemcpyHostToDevice, c->stream));
-    TF_CHECK(hipStreamSynchronize(c->stream));
-    return TF_OK;
+    return sync_checked(c);
 }
 
 extern "C" tf_status tf_get_totals(tf_ctx* c, tf_totals* t)

@@ -24,7 +24,7 @@ k_fuse_begin(const uint16_t* __restrict__ frame, size_t pitch, int W, int H, flo
         float p[12];
         for (int i = 0; i < 12; ++i) p[i] = pose[i];
         tf_set_pose_matrices(st, p, 2);
-        st->abort = 0;
+        st->abort = st->halt ? 1 : 0;   // a halted context (an earlier frame failed on the device): the frame no-ops
         st->mode = 1;
     }
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);

@@ -394,6 +394,9 @@ struct tf_ctx {
     // ... and the fill_fault_launch-th k_raycast_pair launch's range-image wait fails (TFUSION_FILL_FAULT)
     long long pair_launches;
     long long fill_fault_launch;
+    // ... and the vis_fault_launch-th k_vis_build launch's wait for the lower chunks fails (TFUSION_VIS_FAULT)
+    long long vis_launches;
+    long long vis_fault_launch;
     // engine-level batches (tf_scene_fuse_frames, tf_fuse.hip): the batch's poses and per-frame records
     float* fuse_pose;                    // [fuse_cap][12] world -> camera, row-major [R|t]
     int* fuse_rec;                       // [fuse_cap] tf_fuse_record

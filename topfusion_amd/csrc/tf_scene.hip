@@ -666,7 +666,7 @@ k_vis_apply(VisArgs v, TfDevState* __restrict__ st, int n_chunks, const int* __r
 __global__ void __launch_bounds__(256)
 k_vis_build(VisArgs v, TfDevState* __restrict__ st, unsigned char* __restrict__ visType,
             int* __restrict__ allocCounts, unsigned char* __restrict__ swapState, unsigned long long* __restrict__ agg,
-            unsigned gen, int* __restrict__ visibleIds)
+            unsigned gen, int* __restrict__ visibleIds, int fault)
 {
     if (st->abort) return;
     unsigned long long lo, hi;
@@ -677,7 +677,7 @@ k_vis_build(VisArgs v, TfDevState* __restrict__ st, unsigned char* __restrict__ 
         __hip_atomic_store(&agg[blockIdx.x], ((unsigned long long)gen << 32) | (unsigned)own, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     int pre = 0;
-    bool lost = false;
+    bool lost = fault && blockIdx.x == gridDim.x - 1;   // TFUSION_VIS_FAULT (tests): the last chunk's wait fails
     for (int h = threadIdx.x; h < (int)blockIdx.x; h += 256) {
         unsigned long long x;
         unsigned spins = 0;
@@ -689,7 +689,10 @@ k_vis_build(VisArgs v, TfDevState* __restrict__ st, unsigned char* __restrict__ 
     }
     pre = block_sum(pre);
     if (__syncthreads_or(lost)) {
-        if (threadIdx.x == 0) st->icp_ok = -2;           // the frame end: a sticky HIP error
+        if (threadIdx.x == 0) {
+            st->icp_ok = -2;                             // a frame's end turns this into frame_ok -3
+            st->sticky_error = 1;                        // engine-level calls have no frame end
+        }
         return;
     }
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
@@ -756,7 +759,8 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch, int onl
                            c->n_total);
     if (c->vis_fused) {
         hipLaunchKernelGGL(k_vis_build, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->visType,
-                           c->allocCounts, swapping ? c->swapState : nullptr, c->visAgg, ++c->vis_gen, c->visibleIds);
+                           c->allocCounts, swapping ? c->swapState : nullptr, c->visAgg, ++c->vis_gen, c->visibleIds,
+                           (int)(++c->vis_launches == c->vis_fault_launch));
     } else {
         hipLaunchKernelGGL(k_vis_count, dim3(c->vis_chunks), dim3(256), 0, c->stream, v, c->st, c->hash, c->visType,
                            c->visCounts, c->allocCounts, swapping ? c->swapState : nullptr);
