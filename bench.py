@@ -87,6 +87,10 @@ def parse():
                     help="timed region: HIP events around the dominant kernel on every N-th frame only "
                          "(an event pair is a few us of dispatch gap; 1 = every frame)")
     ap.add_argument("--breakdown-frames", type=int, default=64, help="frames of the per-stage timing pass")
+    ap.add_argument("--pose-algebra", choices=["canonical", "opencv4", "opencv2"], default=None,
+                    help="the ICP iterations' det / solve / Rodrigues (tf_set_pose_algebra): canonical (LDL^T + sinc "
+                         "Rodrigues) or the reference's OpenCV algebra (cv::solve DECOMP_SVD, Affine3f), 3.x-4.x / "
+                         "2.4.9; default: the library's (TFUSION_ICP_SOLVE)")
     ap.add_argument("--collective", choices=["rccl", "file"], default="rccl",
                     help="N > 1: how the ranks combine their numbers -- RCCL all-reduces (default) or the host-side "
                          "file group (topfusion_amd/replicas.py)")
@@ -189,7 +193,7 @@ def cpu_run(frames, params_kw, first, n, omp, start=None):
     return time.perf_counter() - t0
 
 
-def cpu_baseline_protocol(frames, first, params_kw, seconds, nt):
+def cpu_baseline_protocol(frames, first, params_kw, seconds, nt, algebra=0):
     """BASELINE.md CPU protocol on the GPU box's host, on the frames the GPU times: the OpenMP
     build (nt threads) runs frames 0..first-1 untimed (the GPU's warm-up frames), and from a
     copy of that state each timed run processes frames first..first+n-1 -- the first n frames of
@@ -198,6 +202,7 @@ def cpu_baseline_protocol(frames, first, params_kw, seconds, nt):
     (n sized so the 5 runs take about `seconds` / 2 per build).  Plus C1 (the frame-0
     integrate-only path on frame 0 of a fresh context, median of 5 after a warm-up) as ms/frame."""
     from oracle import oracle as O
+    O.set_pose_algebra(algebra)             # the GPU's pose algebra (tf_get_pose_algebra)
     t_w0 = time.perf_counter()
     state = O.Oracle(O.default_params(**params_kw), omp=True)
     for k in range(first):
@@ -574,6 +579,8 @@ def main():
         sys.exit(replicas.launch(os.path.abspath(__file__), sys.argv[1:], args.gpus))
     if args.standin:
         return standin(args)
+    if args.pose_algebra is not None:            # every context this process creates (tf_create reads it)
+        os.environ["TFUSION_ICP_SOLVE"] = args.pose_algebra
     if args.config == "C5E":
         return c5e_bench(args)
     if args.config == "C3I":
@@ -760,7 +767,7 @@ def main():
             first = args.warmup * F
             frames = dev.download(0, min(n_frames, first + 128))
             nt = omp_threads()
-            cpu = cpu_baseline_protocol(frames, first, pkw, args.cpu_seconds, nt)
+            cpu = cpu_baseline_protocol(frames, first, pkw, args.cpu_seconds, nt, tf.pose_algebra())
         out = {
             "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame"
                       + (" (swapping scene)" if args.swapping else "")
@@ -833,6 +840,7 @@ def main():
             "hbm_stream_copy_GBs": stream_gbs,
             "roofline_stages": roof_all,
             "icp_schedule": "persistent" if tf.icp_persistent() else "per_iteration",
+            "pose_algebra": {0: "canonical", 2: "opencv2", 4: "opencv4"}[tf.pose_algebra()],
             "cpu_baseline": cpu,
             "multi_gpu": multi if world > 1 else None,
         }

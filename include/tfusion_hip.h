@@ -196,6 +196,19 @@ void*     tf_get_stream(tf_ctx* ctx);
  * persistent launch per frame (k_icp_frame), 0 for one launch per iteration; the environment
  * variable TFUSION_ICP_PERSISTENT=0 forces the latter */
 tf_status tf_get_schedule(tf_ctx* ctx, int* icp_persistent);
+/* The ICP iterations' pose algebra: estimateTransform's cv::determinant(A), cv::solve(A, b, r,
+ * cv::DECOMP_SVD) and Affine3f Tinc(r) (tfusion/src/projective_icp.cpp:197-209).
+ *   TF_POSE_ALGEBRA_CANONICAL (default): the pivoting LU determinant, an LDL^T solve in double and
+ *     Rodrigues in sinc form -- the fast form (a short serial tail per iteration);
+ *   TF_POSE_ALGEBRA_OPENCV4 / _OPENCV2: OpenCV's own algorithms as OpenCV 3.x-4.x / 2.4.9 publish
+ *     them (Matx_DetOp's LU, JacobiSVD + SVBkSb in float, Affine3::rotation with float rounding of
+ *     every Matx operation), the reference's arithmetic (see DESIGN.md §2 for what the two
+ *     algebras do to a sequence).
+ * The environment variable TFUSION_ICP_SOLVE=svd|opencv4|opencv2 sets it at tf_create.
+ * TF_INVALID_ARG if the algebra's persistent ICP kernel would not fit the schedule chosen. */
+enum { TF_POSE_ALGEBRA_CANONICAL = 0, TF_POSE_ALGEBRA_OPENCV2 = 2, TF_POSE_ALGEBRA_OPENCV4 = 4 };
+tf_status tf_set_pose_algebra(tf_ctx* ctx, int algebra);
+tf_status tf_get_pose_algebra(tf_ctx* ctx, int* algebra);
 
 /* ---- stage entry points (operate on context state; parity tests) ------------- */
 /* computeDists + depthBilateralFilter + depthTruncation + depthBuildPyramid +

@@ -77,6 +77,15 @@ def lib(omp=False):
         L.tfo_tsdf_update.argtypes = [P, P, ctypes.c_float, ctypes.c_float, ctypes.c_int]
         L.tfo_sincos.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.tfo_rodrigues.argtypes = [P, P]
+        L.tfo_rodrigues_direct.argtypes = [P, P]
+        L.tfo_set_pose_algebra.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.tfo_get_pose_algebra.restype = ctypes.c_int
+        L.tfo_cv_det6.argtypes = [P, ctypes.c_int]; L.tfo_cv_det6.restype = ctypes.c_double
+        L.tfo_cv_jacobi_svd.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int]
+        L.tfo_cv_solve_svd6.argtypes = [P, P, P]
+        L.tfo_cv_rodrigues.argtypes = [P, P, ctypes.c_int]
+        L.tfo_cv_svd_stats.argtypes = [P, ctypes.c_int]
+        L.tfo_cv_hypot.argtypes = [ctypes.c_double, ctypes.c_double]; L.tfo_cv_hypot.restype = ctypes.c_double
         L.tfo_point_conv.argtypes = [P, P]
         L.tfo_hash_index.argtypes = [ctypes.c_int] * 4; L.tfo_hash_index.restype = ctypes.c_int
         L.tfo_create.argtypes = [ctypes.POINTER(Params)]; L.tfo_create.restype = P
@@ -114,6 +123,21 @@ def lib(omp=False):
             getattr(L, name).argtypes = [P, ctypes.c_int]; getattr(L, name).restype = P
         _libs[omp] = L
     return _libs[omp]
+
+
+POSE_CANONICAL, POSE_OPENCV2, POSE_OPENCV4 = 0, 2, 4
+POSE_MODES = {"canonical": POSE_CANONICAL, "opencv2": POSE_OPENCV2, "opencv4": POSE_OPENCV4}
+
+
+def set_pose_algebra(mode, libm=False, omp=None):
+    """Test-only: the pose algebra estimateTransform's iterations use (tf_oracle.c, "The
+    reference's own pose algebra"): "canonical" (LDL^T + sinc Rodrigues, the GPU default),
+    "opencv2" / "opencv4" (cv::determinant, cv::solve DECOMP_SVD and Affine3f(rvec, t) as OpenCV
+    2.4.9 / 3.x-4.x publish them), with glibc's (libm=True) or the portable sin / cos / hypot.
+    Applies to the serial and (omp=None) the OpenMP build alike."""
+    m = POSE_MODES[mode] if isinstance(mode, str) else int(mode)
+    for o in ((False, True) if omp is None else (omp,)):
+        lib(o).tfo_set_pose_algebra(m, 1 if libm else 0)
 
 
 def ptr(a):

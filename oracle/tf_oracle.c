@@ -225,6 +225,8 @@ void tfo_rodrigues(const float r[3], float R[9])
     }
 }
 
+void tfo_rodrigues_direct(const float r[3], float R[9]) { rodrigues_sqrt(r, R); }
+
 static void rodrigues_sqrt(const float r[3], float R[9])
 {
     double rx = r[0], ry = r[1], rz = r[2];
@@ -526,6 +528,253 @@ static void solve6(const float Af[36], const float bf[6], float x[6])
     for (int i = 0; i < 6; ++i) x[i] = (float)xs[i];
 }
 
+/* ------------------------------------------------------------------------- */
+/* The reference's own pose algebra: OpenCV (>= 2.4.9, CMakeLists.txt:18; not vendored, absent   */
+/* here).  TEST-ONLY mode (tfo_set_pose_algebra): estimateTransform's cv::determinant(Matx66f),  */
+/* cv::solve(A, b, r, DECOMP_SVD) and cv::Affine3f(rvec, t) (projective_icp.cpp:197-209) as     */
+/* OpenCV's published sources define them, so that the canonical algebra above (LDL^T solve,     */
+/* sinc Rodrigues: what the GPU runs by default) can be measured against it.                    */
+/*   TFO_POSE_OPENCV2 : OpenCV 2.4.9 -- LU pivot floor FLT_EPSILON, norm(Vec3f) in double        */
+/*   TFO_POSE_OPENCV4 : OpenCV 3.x / 4.x -- LU floor 10 FLT_EPSILON, norm(Vec3f) in float        */
+/* Both: Matx_DetOp (operations.hpp / matx.inl.hpp: LU with the reciprocal pivots left on the    */
+/* diagonal, det = 1 / (p * prod)), lapack.cpp's cv::solve DECOMP_SVD path (A transposed into    */
+/* the work matrix, JacobiSVDImpl_<float> with eps 2 FLT_EPSILON / minval FLT_MIN, then          */
+/* SVBkSbImpl_<float> with threshold eps (float)(2 DBL_EPSILON)), and Affine3::rotation(Vec3)     */
+/* (affine.hpp: every Matx operation rounded to float).  The transcendental functions are        */
+/* either glibc's (use_libm = 1: what a host build of the reference calls) or portable           */
+/* restatements the GPU can run bit for bit (use_libm = 0: tfo_sincos and cv_hypot below).       */
+/* ------------------------------------------------------------------------- */
+static int g_pose_algebra = TFO_POSE_CANONICAL, g_pose_libm = 0;
+void tfo_set_pose_algebra(int mode, int use_libm) { g_pose_algebra = mode; g_pose_libm = use_libm; }
+int tfo_get_pose_algebra(void) { return g_pose_algebra; }
+
+/* hypot(x, y) for the Jacobi rotation: sqrt(x^2 + y^2) with the rounding error of the sum of
+   squares corrected by fma (Borges, "An improved algorithm for hypot(a, b)", 2019, fma variant).
+   Inputs here are finite and far from over/underflow (sums of squared float products). */
+double tfo_cv_hypot(double x, double y)
+{
+    if (g_pose_libm) return hypot(x, y);
+    x = fabs(x); y = fabs(y);
+    if (x < y) { double t = x; x = y; y = t; }
+    if (y == 0.0) return x;
+    double h = sqrt(fma(x, x, y * y));
+    double h_sq = h * h, x_sq = x * x;
+    double e = (fma(-y, y, h_sq - x_sq) + fma(h, h, -h_sq)) - fma(x, x, -x_sq);
+    return h - e / (2.0 * h);
+}
+
+static void pose_sincos(double th, double* s, double* c)
+{
+    if (g_pose_libm) { *s = sin(th); *c = cos(th); }
+    else tfo_sincos(th, s, c);
+}
+
+/* cv::LU (lapack.cpp LUImpl, float): partial pivoting; the diagonal keeps the reciprocal pivots */
+static int cv_lu_f(float* A, int m, float eps)
+{
+    int p = 1;
+    for (int i = 0; i < m; i++) {
+        int k = i;
+        for (int j = i + 1; j < m; j++)
+            if (fabsf(A[j * m + i]) > fabsf(A[k * m + i])) k = j;
+        if (fabsf(A[k * m + i]) < eps) return 0;
+        if (k != i) {
+            for (int j = i; j < m; j++) { float t = A[i * m + j]; A[i * m + j] = A[k * m + j]; A[k * m + j] = t; }
+            p = -p;
+        }
+        float d = -1 / A[i * m + i];
+        for (int j = i + 1; j < m; j++) {
+            float alpha = A[j * m + i] * d;
+            for (int c = i + 1; c < m; c++) A[j * m + c] += alpha * A[i * m + c];
+        }
+        A[i * m + i] = -d;
+    }
+    return p;
+}
+
+/* cv::determinant(Matx66f) = Matx_DetOp<float, 6> */
+double tfo_cv_det6(const float Ain[36], int mode)
+{
+    float T[36];
+    memcpy(T, Ain, sizeof(T));
+    double p = cv_lu_f(T, 6, mode == TFO_POSE_OPENCV2 ? FLT_EPSILON : FLT_EPSILON * 10);
+    if (p == 0) return p;
+    for (int i = 0; i < 6; i++) p *= T[i * 6 + i];
+    return 1. / p;
+}
+
+/* cv::RNG::next (core.hpp: multiply-with-carry, CV_RNG_COEFF 4164903690) */
+static unsigned cv_rng_next(uint64_t* st)
+{
+    *st = (uint64_t)(unsigned)*st * 4164903690u + (unsigned)(*st >> 32);
+    return (unsigned)*st;
+}
+
+/* JacobiSVDImpl_<float>(At, ..., m, n, n1 = n, FLT_MIN, 2 FLT_EPSILON), lapack.cpp: one-sided
+   cyclic Jacobi on the rows of At (n rows of m), W in double while iterating, rows sorted by
+   singular value, left vectors normalised (random completion of a zero singular value). */
+/* statistics of the Jacobi sweeps (test-only diagnostics): calls, sweeps, rotations, max sweeps,
+   and a histogram of sweeps per call (index = sweeps, capped at 31) */
+static long long g_svd_stats[4 + 32];
+void tfo_cv_svd_stats(long long out[36], int reset)
+{
+    memcpy(out, g_svd_stats, sizeof(g_svd_stats));
+    if (reset) memset(g_svd_stats, 0, sizeof(g_svd_stats));
+}
+
+void tfo_cv_jacobi_svd(float* At, float* Wout, float* Vt, int m, int n)
+{
+    const double minval = FLT_MIN;
+    const float eps = FLT_EPSILON * 2;
+    double W[8], sd;
+    int i, j, k, iter, max_iter = m > 30 ? m : 30;
+    for (i = 0; i < n; i++) {
+        for (k = 0, sd = 0; k < m; k++) { float t = At[i * m + k]; sd += (double)t * t; }
+        W[i] = sd;
+        for (k = 0; k < n; k++) Vt[i * n + k] = 0;
+        Vt[i * n + i] = 1;
+    }
+    for (iter = 0; iter < max_iter; iter++) {
+        int changed = 0;
+        for (i = 0; i < n - 1; i++)
+            for (j = i + 1; j < n; j++) {
+                float *Ai = At + i * m, *Aj = At + j * m;
+                double a = W[i], p = 0, b = W[j];
+                for (k = 0; k < m; k++) p += (double)Ai[k] * Aj[k];
+                if (fabs(p) <= eps * sqrt((double)a * b)) continue;
+                p *= 2;
+                double beta = a - b, gamma = tfo_cv_hypot(p, beta);
+                float c, s;
+                if (beta < 0) {
+                    double delta = (gamma - beta) * 0.5;
+                    s = (float)sqrt(delta / gamma);
+                    c = (float)(p / (gamma * s * 2));
+                } else {
+                    c = (float)sqrt((gamma + beta) / (gamma * 2));
+                    s = (float)(p / (gamma * c * 2));
+                }
+                a = b = 0;
+                for (k = 0; k < m; k++) {
+                    float t0 = c * Ai[k] + s * Aj[k];
+                    float t1 = -s * Ai[k] + c * Aj[k];
+                    Ai[k] = t0; Aj[k] = t1;
+                    a += (double)t0 * t0; b += (double)t1 * t1;
+                }
+                W[i] = a; W[j] = b;
+                changed = 1;
+                g_svd_stats[2]++;
+                float *Vi = Vt + i * n, *Vj = Vt + j * n;
+                for (k = 0; k < n; k++) {       /* VBLAS<float>::givens: a c + b s, b c - a s */
+                    float t0 = Vi[k] * c + Vj[k] * s;
+                    float t1 = Vj[k] * c - Vi[k] * s;
+                    Vi[k] = t0; Vj[k] = t1;
+                }
+            }
+        if (!changed) break;
+    }
+    g_svd_stats[0]++;
+    g_svd_stats[1] += iter + (iter < max_iter);
+    if (iter + 1 > g_svd_stats[3]) g_svd_stats[3] = iter + 1;
+    g_svd_stats[4 + (iter < 31 ? iter : 31)]++;
+    for (i = 0; i < n; i++) {
+        for (k = 0, sd = 0; k < m; k++) { float t = At[i * m + k]; sd += (double)t * t; }
+        W[i] = sqrt(sd);
+    }
+    for (i = 0; i < n - 1; i++) {
+        j = i;
+        for (k = i + 1; k < n; k++) if (W[j] < W[k]) j = k;
+        if (i != j) {
+            double t = W[i]; W[i] = W[j]; W[j] = t;
+            for (k = 0; k < m; k++) { float u = At[i * m + k]; At[i * m + k] = At[j * m + k]; At[j * m + k] = u; }
+            for (k = 0; k < n; k++) { float u = Vt[i * n + k]; Vt[i * n + k] = Vt[j * n + k]; Vt[j * n + k] = u; }
+        }
+    }
+    for (i = 0; i < n; i++) Wout[i] = (float)W[i];
+    uint64_t rng = 0x12345678;
+    for (i = 0; i < n; i++) {
+        sd = W[i];
+        while (sd <= minval) {
+            const float val0 = (float)(1. / m);
+            for (k = 0; k < m; k++) At[i * m + k] = (cv_rng_next(&rng) & 256) != 0 ? val0 : -val0;
+            for (iter = 0; iter < 2; iter++)
+                for (j = 0; j < i; j++) {
+                    sd = 0;
+                    for (k = 0; k < m; k++) sd += At[i * m + k] * At[j * m + k];
+                    float asum = 0;
+                    for (k = 0; k < m; k++) {
+                        float t = (float)(At[i * m + k] - sd * At[j * m + k]);
+                        At[i * m + k] = t;
+                        asum += fabsf(t);
+                    }
+                    asum = asum > eps * 100 ? 1 / asum : 0;
+                    for (k = 0; k < m; k++) At[i * m + k] *= asum;
+                }
+            sd = 0;
+            for (k = 0; k < m; k++) { float t = At[i * m + k]; sd += (double)t * t; }
+            sd = sqrt(sd);
+        }
+        float s = (float)(1 / sd);
+        for (k = 0; k < m; k++) At[i * m + k] *= s;
+    }
+}
+
+/* cv::solve(A, b, x, DECOMP_SVD) for a float 6x6 and one right-hand side (lapack.cpp): the work
+   matrix is transpose(A); JacobiSVD; SVBkSbImpl_<float>(m, n, w, u = work rows (uT), v = Vt (vT),
+   b, nb = 1) with threshold = (sum w) * (float)(2 DBL_EPSILON) */
+void tfo_cv_solve_svd6(const float A[36], const float b[6], float x[6])
+{
+    float At[36], w[6], Vt[36];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) At[i * 6 + j] = A[j * 6 + i];
+    tfo_cv_jacobi_svd(At, w, Vt, 6, 6);
+    const float eps = (float)(DBL_EPSILON * 2);
+    double threshold = 0;
+    for (int i = 0; i < 6; i++) threshold += w[i];
+    threshold *= eps;
+    for (int j = 0; j < 6; j++) x[j] = 0;
+    for (int i = 0; i < 6; i++) {
+        double wi = w[i];
+        if ((double)fabs(wi) <= threshold) continue;
+        wi = 1 / wi;
+        double s = 0;
+        for (int j = 0; j < 6; j++) s += At[i * 6 + j] * b[j];      /* float product, double sum */
+        s *= wi;
+        for (int j = 0; j < 6; j++) x[j] = (float)(x[j] + s * Vt[i * 6 + j]);
+    }
+}
+
+/* cv::Affine3f(rvec, t)'s rotation: Affine3<float>::rotation(const Vec3f&) (affine.hpp) */
+void tfo_cv_rodrigues(const float rv[3], float R[9], int mode)
+{
+    double theta;
+    if (mode == TFO_POSE_OPENCV2) {        /* norm(Matx): normL2Sqr<float, double> */
+        double s2 = 0;
+        for (int i = 0; i < 3; ++i) { double v = rv[i]; s2 += v * v; }
+        theta = sqrt(s2);
+    } else {                               /* normL2Sqr<float, DataType<float>::work_type = float> */
+        float s2 = 0;
+        for (int i = 0; i < 3; ++i) { float v = rv[i]; s2 += v * v; }
+        theta = sqrtf(s2);
+    }
+    if (theta < DBL_EPSILON) {
+        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+        return;
+    }
+    double s, c;
+    pose_sincos(theta, &s, &c);
+    double c1 = 1. - c;
+    double itheta = (theta != 0) ? 1. / theta : 0.;
+    const float rx = (float)(rv[0] * itheta), ry = (float)(rv[1] * itheta), rz = (float)(rv[2] * itheta);
+    const float rrt[9] = { rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz };
+    const float rxm[9] = { 0, -rz, ry, rz, 0, -rx, -ry, rx, 0 };
+    for (int k = 0; k < 9; ++k) {
+        const float I = (k % 4 == 0) ? 1.0f : 0.0f;
+        const float cI = (float)(I * c), crr = (float)(rrt[k] * c1), sx = (float)(rxm[k] * s);
+        const float t = cI + crr;
+        R[k] = t + sx;
+    }
+}
+
 /* one iteration of estimateTransform after the reductions, projective_icp.cpp:187-210
    (StreamHelper::get unpacking :43-62) */
 int tfo_icp_step(const float s[27], float affine[12], double* det_out)
@@ -538,13 +787,16 @@ int tfo_icp_step(const float s[27], float affine[12], double* det_out)
             if (j == 6) b[i] = value;
             else A[j * 6 + i] = A[i * 6 + j] = value;
         }
-    double det = cv_det6(A);
+    const int cv = g_pose_algebra != TFO_POSE_CANONICAL;
+    double det = cv ? tfo_cv_det6(A, g_pose_algebra) : cv_det6(A);
     if (det_out) *det_out = det;
     if (fabs(det) < 1e-15 || isnan(det)) return 0;
     float r[6];
-    solve6(A, b, r);
+    if (cv) tfo_cv_solve_svd6(A, b, r);
+    else solve6(A, b, r);
     float tinc[12], R[9];
-    tfo_rodrigues(r, R);
+    if (cv) tfo_cv_rodrigues(r, R, g_pose_algebra);
+    else tfo_rodrigues(r, R);
     for (int j = 0; j < 3; ++j) {
         tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1]; tinc[j * 4 + 2] = R[j * 3 + 2];
         tinc[j * 4 + 3] = r[3 + j];

@@ -113,6 +113,18 @@ void tfo_icp_reduce(const float* vcurr, const float* ncurr, const float* vprev, 
                     float min_cosine, float dist2_thres, const float aff[12], float out27[27]);
 /* det check + solve + Rodrigues + compose (projective_icp.cpp:190-210); returns 1 ok, 0 fail */
 int tfo_icp_step(const float sums27[27], float affine_rt[12], double* det_out);
+/* test-only: the pose algebra tfo_icp_step uses (canonical = the GPU's default; OpenCV 2.4.9 or
+   3.x/4.x as published), with glibc's or the portable transcendental functions */
+enum { TFO_POSE_CANONICAL = 0, TFO_POSE_OPENCV2 = 2, TFO_POSE_OPENCV4 = 4 };
+void tfo_set_pose_algebra(int mode, int use_libm);
+int tfo_get_pose_algebra(void);
+double tfo_cv_det6(const float A[36], int mode);
+void tfo_cv_jacobi_svd(float* At, float* W, float* Vt, int m, int n);
+void tfo_cv_solve_svd6(const float A[36], const float b[6], float x[6]);
+void tfo_cv_rodrigues(const float rvec[3], float R[9], int mode);
+double tfo_cv_hypot(double x, double y);
+/* diagnostics: Jacobi calls, sweeps, rotations, max sweeps, histogram of the converged sweep index */
+void tfo_cv_svd_stats(long long out[36], int reset);
 void tfo_rigid_mul(const float a[12], const float b[12], float out[12]);
 void tfo_rigid_inv(const float a[12], float out[12]);
 int  tfo_matrix4_inv(const float m[16], float out[16]);
@@ -120,6 +132,9 @@ void tfo_sincos(double th, double* s, double* c);
 void tfo_m4v(const float m[16], const float v[4], float r[4]);
 void tfo_tsdf_update(int16_t* sdf, uint8_t* w, float eta, float mu, int maxW);
 void tfo_rodrigues(const float r[3], float R[9]);
+/* the direct form (unit axis, sin / cos of the angle, 1 - cos): an independent check of the
+   sinc form tfo_rodrigues uses */
+void tfo_rodrigues_direct(const float r[3], float R[9]);
 void tfo_point_conv(const float p[3], float out[13]);     /* floor/round/length conversions */
 void tfo_interp_bilinear_u8x4(const uint8_t* rgb, size_t pitch, float ix, float iy, float out[4]); /* interpolateBilinear<uchar> */
 uint32_t tfo_colour_average(uint32_t clr, const float sample[4], int maxW);  /* colour running average */

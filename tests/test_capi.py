@@ -131,7 +131,7 @@ def test_entry_points_flush_deferred_frame():
     per-call frame itself (it flushes with its own frame's lookahead) and the host-only ones."""
     import re
     src = open(os.path.join(ROOT, "topfusion_amd", "csrc", "tf_capi.hip")).read()
-    host_only = {"tf_destroy", "tf_get_params", "tf_get_stream", "tf_get_schedule", "tf_profile_enable",
+    host_only = {"tf_destroy", "tf_get_params", "tf_get_stream", "tf_get_schedule", "tf_get_pose_algebra", "tf_profile_enable",
                  "tf_profile_stages", "tf_profile_sample", "tf_profile_reset", "tf_profile_read"}
     per_call = {"tf_process_frame", "tf_process_frame_host"}
     checked = 0

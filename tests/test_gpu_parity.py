@@ -400,7 +400,9 @@ def test_bench_timed_window(oracle_mod):
             tag = f"bench frames {step * F}..{(step + 1) * F - 1}"
             _compare_frame_state(g, o, tag, grey=bool(oko[-1]))
             compare_scene(g, o, tag)
-    assert 0 < n_reset < 200, n_reset          # the reference's resets, not a lost camera
+    # the reference's frame-mixing resets: the oracle's own count over frames 0..799 of
+    # this stream (profiles/r05/pose_algebra_gap_C2.json, canonical mode), pinned
+    assert n_reset == 80, n_reset
     g.close()
     dev.free()
 

@@ -437,6 +437,13 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = tfk_check_div3(c, pin->mu, &c->mu_exact3);   // integrate: eta / mu
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
+    {   // the ICP iterations' pose algebra (tf_set_pose_algebra): TFUSION_ICP_SOLVE=svd / opencv4 (the
+        // reference's cv::solve DECOMP_SVD, OpenCV 3.x-4.x), opencv2 (OpenCV 2.4.9); default canonical
+        const char* env = getenv("TFUSION_ICP_SOLVE");
+        c->pose_alg = !env ? TF_POSE_ALGEBRA_CANONICAL
+                    : (!strcmp(env, "svd") || !strcmp(env, "opencv4")) ? TF_POSE_ALGEBRA_OPENCV4
+                    : !strcmp(env, "opencv2") ? TF_POSE_ALGEBRA_OPENCV2 : TF_POSE_ALGEBRA_CANONICAL;
+    }
     {   // ICP: one persistent launch per frame when all its workgroups fit at once; otherwise (or
         // with TFUSION_ICP_PERSISTENT=0) one k_icp_iter launch per iteration
         const char* env = getenv("TFUSION_ICP_PERSISTENT");
@@ -1007,6 +1014,28 @@ extern "C" tf_status tf_get_schedule(tf_ctx* c, int* icp_persistent)
 {
     if (!c) return TF_INVALID_ARG;
     if (icp_persistent) *icp_persistent = c->icp_persistent;
+    return TF_OK;
+}
+
+extern "C" tf_status tf_set_pose_algebra(tf_ctx* c, int algebra)
+{
+    if (!c) return TF_INVALID_ARG;
+    if (algebra != TF_POSE_ALGEBRA_CANONICAL && algebra != TF_POSE_ALGEBRA_OPENCV2 && algebra != TF_POSE_ALGEBRA_OPENCV4)
+        return TF_INVALID_ARG;
+    TF_FLUSH(c);
+    const int old = c->pose_alg;
+    c->pose_alg = algebra;
+    if (c->icp_persistent && !tfk_icp_persistent_ok(c)) {     // the schedule stays what tf_create chose
+        c->pose_alg = old;
+        return TF_INVALID_ARG;
+    }
+    return TF_OK;
+}
+
+extern "C" tf_status tf_get_pose_algebra(tf_ctx* c, int* algebra)
+{
+    if (!c || !algebra) return TF_INVALID_ARG;
+    *algebra = c->pose_alg;
     return TF_OK;
 }
 

@@ -130,6 +130,7 @@ __device__ __forceinline__ void ip_rows4(const IcpLevel& L, const float* aff, co
                                          const int (&xy)[4], ip_f2 (&r01)[7], ip_f2 (&r23)[7]);
 __device__ __forceinline__ float ip_cta_reduce(const ip_f2 (&r01)[7], const ip_f2 (&r23)[7], int lane);
 
+template <int ALG>
 __global__ void __launch_bounds__(64 * ICP_WAVES)
 k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsigned* __restrict__ ticket,
            int nwg, int slots, int last_iter)
@@ -249,17 +250,16 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
             }
     }
     ICP_TS(3);
-    double det = icp_det6_reg(Am);
+    double det = icp_det6<ALG>(Am);
     ICP_TS(4);
     if (fabs(det) < 1e-15 || isnan(det)) {                     // projective_icp.cpp:197-203
         if (lane == 0) { st->icp_ok = 0; st->abort = 1; }
         return;
     }
     float rv[6];
-    icp_solve6_ldl(Am, bv, rv);
-    ICP_TS(5);
     float R[9], tinc[12], A[12];
-    icp_rodrigues(rv, R);
+    icp_solve_rodrigues<ALG>(Am, bv, rv, R);
+    ICP_TS(5);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1]; tinc[j * 4 + 2] = R[j * 3 + 2];
@@ -560,6 +560,7 @@ __device__ __forceinline__ float ip_residue_tree(const float* c)
 // iteration k+1 computes its rows and is settled before anything of k+1 is published: on
 // failure the affine of k-1 is restored and the loop ends exactly where the serial order ends
 // it.  The solve (wave 0) is the only serial work between two iterations.
+template <int ALG>
 __global__ void __launch_bounds__(64 * IP_WAVES)
 k_icp_frame(IcpFrameArgs a)
 {
@@ -660,7 +661,7 @@ k_icp_frame(IcpFrameArgs a)
             if (det_pending && wave == IP_DETW) {
                 float Am[6][6], bv[6];
                 ip_unpack(det_sm, Am, bv);
-                const double det = icp_det6_reg(Am);
+                const double det = icp_det6<ALG>(Am);
                 if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
                 IPT_REC_T(done - 1, 2 * ICP_NWG + 5, 64 * IP_DETW);
             }
@@ -802,9 +803,7 @@ k_icp_frame(IcpFrameArgs a)
                         for (int q = 0; q < 27; ++q) det_sm[q] = sm[q];
                     } else {                                           // solve -> Rodrigues -> compose
                         float rv[6], R[9], tinc[12];
-                        icp_solve6_ldl(Am, bv, rv);                     // projective_icp.cpp:206-209
-                        IPT_REC(done, 2 * ICP_NWG + 3);
-                        icp_rodrigues(rv, R);
+                        icp_solve_rodrigues<ALG>(Am, bv, rv, R);        // projective_icp.cpp:206-209
                         IPT_REC(done, 2 * ICP_NWG + 7);
 #pragma unroll
                         for (int j = 0; j < 3; ++j) {
@@ -840,7 +839,7 @@ k_icp_frame(IcpFrameArgs a)
         if (wave == IP_DETW) {
             float Am[6][6], bv[6];
             ip_unpack(det_sm, Am, bv);
-            const double det = icp_det6_reg(Am);
+            const double det = icp_det6<ALG>(Am);
             if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
         }
         __syncthreads();
@@ -947,7 +946,11 @@ static int icp_used_levels(const tf_params& p)
 int tfk_icp_persistent_ok(tf_ctx* c)
 {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame, 64 * IP_WAVES, IP_LDS_PAD) != hipSuccess) return 0;
+    const hipError_t oe = c->pose_alg == 0
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame<0>, 64 * IP_WAVES, IP_LDS_PAD)
+        : c->pose_alg == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame<2>, 64 * IP_WAVES, IP_LDS_PAD)
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_icp_frame<4>, 64 * IP_WAVES, IP_LDS_PAD);
+    if (oe != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) return 0;
     if (per_cu * cus < ICP_NWG) return 0;
     for (int l = 0; l < TF_LEVELS; ++l) {
@@ -996,7 +999,9 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
         // workgroup per CU, so the 256 workgroups spread over all CUs instead of doubling up
         hipError_t e = tf_icp_order_before(c);
         if (e == hipSuccess) {
-            tf_launch(c, k_icp_frame, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, a);
+            if (c->pose_alg == 0) tf_launch(c, k_icp_frame<0>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, a);
+            else if (c->pose_alg == 2) tf_launch(c, k_icp_frame<2>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, a);
+            else tf_launch(c, k_icp_frame<4>, dim3(ICP_NWG), dim3(64 * IP_WAVES), IP_LDS_PAD, a);
             e = hipGetLastError();
         }
         const hipError_t e2 = tf_icp_order_after(c);     // (always: releases the ordering lock)
@@ -1013,7 +1018,8 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
         if (slots > ICP_MAX_SLOTS) return hipErrorInvalidValue;
         for (int it = 0; it < p.icp_iter_num[l]; ++it) {
             int last = (pose_update && l == last_l && it == p.icp_iter_num[l] - 1) ? 1 : 0;
-            hipLaunchKernelGGL(k_icp_iter, dim3(nwg), dim3(64 * ICP_WAVES), 0, c->stream, L, c->st, c->icp_partial,
+            auto kern = c->pose_alg == 0 ? k_icp_iter<0> : (c->pose_alg == 2 ? k_icp_iter<2> : k_icp_iter<4>);
+            hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * ICP_WAVES), 0, c->stream, L, c->st, c->icp_partial,
                                c->icp_ticket, nwg, slots, last);
         }
     }

@@ -203,3 +203,283 @@ __device__ __forceinline__ void icp_solve6_ldl(const float (&Af)[6][6], const fl
     for (int i = 0; i < 6; ++i) x[i] = (float)xs[i];
 }
 
+
+// =============================================================================================
+// The reference's own pose algebra: OpenCV's cv::determinant(Matx66f), cv::solve(A, b, r,
+// DECOMP_SVD) and cv::Affine3f(rvec, t) (projective_icp.cpp:197-209; OpenCV >= 2.4.9,
+// CMakeLists.txt:18), selected per context (tf_set_pose_algebra / TFUSION_ICP_SOLVE).  The
+// operations of the oracle's OpenCV 2.4.9 / 3.x-4.x pose-algebra mode (oracle/tf_oracle.c) with its portable
+// transcendental functions (icp_sincos, icp_cv_hypot), in the same order: bit for bit the
+// oracle's.  ALG 2: OpenCV 2.4.9 (LU pivot floor FLT_EPSILON, norm(Vec3f) in double); ALG 4:
+// OpenCV 3.x / 4.x (10 FLT_EPSILON, norm in float).  One wave evaluates it on uniform data, like
+// the LDL^T solve; every register array is indexed statically (rotations are template-unrolled).
+// =============================================================================================
+constexpr float TF_FLT_EPS = 1.19209290e-07f;
+constexpr double TF_FLT_MIN = 1.17549435e-38;
+
+// hypot (the oracle's portable hypot): fma-corrected sum of squares
+__device__ __forceinline__ double icp_cv_hypot(double x, double y)
+{
+    x = fabs(x); y = fabs(y);
+    if (x < y) { const double t = x; x = y; y = t; }
+    if (y == 0.0) return x;
+    const double h = sqrt(fma(x, x, y * y));
+    const double h_sq = h * h, x_sq = x * x;
+    const double e = (fma(-y, y, h_sq - x_sq) + fma(h, h, -h_sq)) - fma(x, x, -x_sq);
+    return h - e / (2.0 * h);
+}
+
+// cv::determinant(Matx66f) = Matx_DetOp<float, 6>: LU (reciprocal pivots left on the diagonal),
+// det = 1 / (p * prod); ALG 0: the canonical form (icp_det6_reg)
+template <int ALG>
+__device__ __forceinline__ double icp_det6(const float (&A0)[6][6])
+{
+    if constexpr (ALG == 0) {
+        return icp_det6_reg(A0);
+    } else {
+        float A[6][6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) A[i][j] = A0[i][j];
+        const float eps = ALG == 2 ? TF_FLT_EPS : TF_FLT_EPS * 10;
+        int p = 1;
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            float best = fabsf(A[i][i]);
+            int k = i;
+#pragma unroll
+            for (int j = i + 1; j < 6; j++) { float v = fabsf(A[j][i]); if (v > best) { best = v; k = j; } }
+            k = __builtin_amdgcn_readfirstlane(k);
+            if (best < eps) return 0.0;
+            if (k != i) {
+#pragma unroll
+                for (int r = i + 1; r < 6; ++r)
+                    if (r == k) {
+#pragma unroll
+                        for (int c = i; c < 6; ++c) { float t = A[i][c]; A[i][c] = A[r][c]; A[r][c] = t; }
+                    }
+                p = -p;
+            }
+            const float d = -1 / A[i][i];
+#pragma unroll
+            for (int j = i + 1; j < 6; j++) {
+                const float alpha = A[j][i] * d;
+#pragma unroll
+                for (int c = i + 1; c < 6; c++) A[j][c] += alpha * A[i][c];
+            }
+            A[i][i] = -d;
+        }
+        double det = p;
+#pragma unroll
+        for (int i = 0; i < 6; i++) det *= A[i][i];
+        return 1. / det;
+    }
+}
+
+// one rotation (I, J) of JacobiSVDImpl_<float> (lapack.cpp): true if it rotated
+template <int I, int J>
+__device__ __forceinline__ bool icp_cv_rot(float (&At)[6][6], float (&Vt)[6][6], double (&W)[6])
+{
+    constexpr float eps = TF_FLT_EPS * 2;
+    double a = W[I], p = 0, b = W[J];
+#pragma unroll
+    for (int k = 0; k < 6; k++) p += (double)At[I][k] * At[J][k];
+    if (fabs(p) <= (double)eps * sqrt(a * b)) return false;
+    p *= 2;
+    const double beta = a - b, gamma = icp_cv_hypot(p, beta);
+    float c, s;
+    if (beta < 0) {
+        const double delta = (gamma - beta) * 0.5;
+        s = (float)sqrt(delta / gamma);
+        c = (float)(p / (gamma * s * 2));
+    } else {
+        c = (float)sqrt((gamma + beta) / (gamma * 2));
+        s = (float)(p / (gamma * c * 2));
+    }
+    a = b = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        const float t0 = c * At[I][k] + s * At[J][k];
+        const float t1 = -s * At[I][k] + c * At[J][k];
+        At[I][k] = t0; At[J][k] = t1;
+        a += (double)t0 * t0; b += (double)t1 * t1;
+    }
+    W[I] = a; W[J] = b;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {                 // VBLAS<float>::givens
+        const float t0 = Vt[I][k] * c + Vt[J][k] * s;
+        const float t1 = Vt[J][k] * c - Vt[I][k] * s;
+        Vt[I][k] = t0; Vt[J][k] = t1;
+    }
+    return true;
+}
+
+// cv::RNG::next (multiply-with-carry, CV_RNG_COEFF 4164903690)
+__device__ __forceinline__ unsigned icp_cv_rng(unsigned long long& st)
+{
+    st = (unsigned long long)(unsigned)st * 4164903690ull + (unsigned)(st >> 32);
+    return (unsigned)st;
+}
+
+// cv::solve(A, b, x, DECOMP_SVD) for a float 6x6 and one right-hand side (lapack.cpp): the work
+// matrix transpose(A), JacobiSVDImpl_<float>(m = n = 6, eps 2 FLT_EPSILON, minval FLT_MIN), then
+// SVBkSbImpl_<float> with threshold (sum w) * (float)(2 DBL_EPSILON)
+__device__ __forceinline__ void icp_cv_solve_svd6(const float (&A)[6][6], const float (&bv)[6], float (&x)[6])
+{
+    float At[6][6], Vt[6][6];
+    double W[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) { At[i][k] = A[k][i]; sd += (double)At[i][k] * At[i][k]; }
+        W[i] = sd;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) Vt[i][k] = i == k ? 1.f : 0.f;
+    }
+#pragma unroll 1
+    for (int iter = 0; iter < 30; iter++) {        // max_iter = max(m, 30)
+        bool ch = false;
+        ch |= icp_cv_rot<0, 1>(At, Vt, W); ch |= icp_cv_rot<0, 2>(At, Vt, W); ch |= icp_cv_rot<0, 3>(At, Vt, W);
+        ch |= icp_cv_rot<0, 4>(At, Vt, W); ch |= icp_cv_rot<0, 5>(At, Vt, W); ch |= icp_cv_rot<1, 2>(At, Vt, W);
+        ch |= icp_cv_rot<1, 3>(At, Vt, W); ch |= icp_cv_rot<1, 4>(At, Vt, W); ch |= icp_cv_rot<1, 5>(At, Vt, W);
+        ch |= icp_cv_rot<2, 3>(At, Vt, W); ch |= icp_cv_rot<2, 4>(At, Vt, W); ch |= icp_cv_rot<2, 5>(At, Vt, W);
+        ch |= icp_cv_rot<3, 4>(At, Vt, W); ch |= icp_cv_rot<3, 5>(At, Vt, W); ch |= icp_cv_rot<4, 5>(At, Vt, W);
+        if (!ch) break;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) sd += (double)At[i][k] * At[i][k];
+        W[i] = sqrt(sd);
+    }
+#pragma unroll
+    for (int i = 0; i < 5; i++) {                  // selection sort, descending (strict <: first maximum)
+        int j = i;
+        double wj = W[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; k++) if (wj < W[k]) { j = k; wj = W[k]; }
+        j = __builtin_amdgcn_readfirstlane(j);
+        if (j != i) {
+#pragma unroll
+            for (int r = i + 1; r < 6; ++r)
+                if (r == j) {
+                    const double t = W[i]; W[i] = W[r]; W[r] = t;
+#pragma unroll
+                    for (int k = 0; k < 6; k++) { float u = At[i][k]; At[i][k] = At[r][k]; At[r][k] = u; }
+#pragma unroll
+                    for (int k = 0; k < 6; k++) { float u = Vt[i][k]; Vt[i][k] = Vt[r][k]; Vt[r][k] = u; }
+                }
+        }
+    }
+    float w[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) w[i] = (float)W[i];
+    unsigned long long rng = 0x12345678ull;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        double sd = W[i];
+        while (sd <= TF_FLT_MIN) {                 // a zero singular value: random completion
+            const float val0 = (float)(1. / 6);
+#pragma unroll
+            for (int k = 0; k < 6; k++) At[i][k] = (icp_cv_rng(rng) & 256) != 0 ? val0 : -val0;
+#pragma unroll
+            for (int it2 = 0; it2 < 2; it2++)
+#pragma unroll
+                for (int j = 0; j < i; j++) {
+                    sd = 0;
+#pragma unroll
+                    for (int k = 0; k < 6; k++) sd += At[i][k] * At[j][k];
+                    float asum = 0;
+#pragma unroll
+                    for (int k = 0; k < 6; k++) {
+                        const float t = (float)(At[i][k] - sd * At[j][k]);
+                        At[i][k] = t;
+                        asum += fabsf(t);
+                    }
+                    asum = asum > TF_FLT_EPS * 2 * 100 ? 1 / asum : 0;
+#pragma unroll
+                    for (int k = 0; k < 6; k++) At[i][k] *= asum;
+                }
+            sd = 0;
+#pragma unroll
+            for (int k = 0; k < 6; k++) sd += (double)At[i][k] * At[i][k];
+            sd = sqrt(sd);
+        }
+        const float s = (float)(1 / sd);
+#pragma unroll
+        for (int k = 0; k < 6; k++) At[i][k] *= s;
+    }
+    // SVBkSbImpl_<float>(6, 6, w, u = At (uT), v = Vt (vT), b, nb = 1)
+    double threshold = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) threshold += w[i];
+    threshold *= (double)(float)(2.220446049250313e-16 * 2);
+#pragma unroll
+    for (int j = 0; j < 6; j++) x[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        double wi = w[i];
+        if ((double)fabs(wi) <= threshold) continue;
+        wi = 1 / wi;
+        double s = 0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) s += At[i][j] * bv[j];         // float product, double sum
+        s *= wi;
+#pragma unroll
+        for (int j = 0; j < 6; j++) x[j] = (float)(x[j] + s * Vt[i][j]);
+    }
+}
+
+// cv::Affine3f(rvec, t)'s rotation: Affine3<float>::rotation(const Vec3f&) (affine.hpp), every
+// Matx operation rounded to float
+template <int ALG>
+__device__ __forceinline__ void icp_cv_rodrigues(const float* rv, float* R)
+{
+    double theta;
+    if constexpr (ALG == 2) {
+        double s2 = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { const double v = rv[i]; s2 += v * v; }
+        theta = sqrt(s2);
+    } else {
+        float s2 = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { const float v = rv[i]; s2 += v * v; }
+        theta = sqrtf(s2);
+    }
+    if (theta < 2.220446049250313e-16) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+        return;
+    }
+    double s, c;
+    icp_sincos(theta, &s, &c);
+    const double c1 = 1. - c;
+    const double itheta = (theta != 0) ? 1. / theta : 0.;
+    const float rx = (float)(rv[0] * itheta), ry = (float)(rv[1] * itheta), rz = (float)(rv[2] * itheta);
+    const float rrt[9] = { rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz };
+    const float rxm[9] = { 0, -rz, ry, rz, 0, -rx, -ry, rx, 0 };
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const float I = (k % 4 == 0) ? 1.0f : 0.0f;
+        const float cI = (float)(I * c), crr = (float)(rrt[k] * c1), sx = (float)(rxm[k] * s);
+        const float t = cI + crr;
+        R[k] = t + sx;
+    }
+}
+
+// the iteration's solve + Rodrigues under pose algebra ALG
+template <int ALG>
+__device__ __forceinline__ void icp_solve_rodrigues(const float (&Am)[6][6], const float (&bv)[6], float (&rv)[6], float* R)
+{
+    if constexpr (ALG == 0) {
+        icp_solve6_ldl(Am, bv, rv);
+        icp_rodrigues(rv, R);
+    } else {
+        icp_cv_solve_svd6(Am, bv, rv);
+        icp_cv_rodrigues<ALG>(rv, R);
+    }
+}

@@ -335,6 +335,7 @@ struct tf_ctx {
     unsigned* icp_ticket;    // last-workgroup ticket (zero between launches)
     unsigned long long* icp_tagged;   // persistent ICP: [256][28] tagged column sums + [16] broadcast
     int icp_persistent;      // 1: one launch per frame (k_icp_frame), 0: one launch per iteration
+    int pose_alg;            // TF_POSE_ALGEBRA_*: the ICP iterations' det / solve / Rodrigues (tf_icp_tail.h)
     int icp_max_cta;
     int count_lanes;         // frame path: count integration's voxel lanes (profiling)
     long long* integ_cnt;    // [TF_INTEG_WG][2] per-workgroup running counts of voxel lanes read / written

@@ -154,6 +154,19 @@ class TopFu:
     def stream(self):
         return L.load().tf_get_stream(self._h)
 
+    POSE_ALGEBRAS = {"canonical": 0, "opencv2": 2, "opencv4": 4, "svd": 4}
+
+    def set_pose_algebra(self, algebra):
+        """The ICP iterations' det / solve / Rodrigues (tf_set_pose_algebra): "canonical" (default,
+        LDL^T + sinc Rodrigues) or the reference's OpenCV algebra, "opencv4" (= "svd") / "opencv2"."""
+        a = self.POSE_ALGEBRAS[algebra] if isinstance(algebra, str) else int(algebra)
+        L.check(L.load().tf_set_pose_algebra(self._h, a), "tf_set_pose_algebra")
+
+    def pose_algebra(self):
+        v = ctypes.c_int()
+        L.check(L.load().tf_get_pose_algebra(self._h, ctypes.byref(v)), "tf_get_pose_algebra")
+        return v.value
+
     def icp_persistent(self):
         """True when ICP runs as one persistent launch per frame."""
         v = ctypes.c_int()
