@@ -52,7 +52,7 @@ int main(int argc, char** argv)
             for (int c = 0; c < 3; ++c) rt[4 * r + c] = (float)DR[3 * r + c];
             rt[4 * r + 3] = (float)Dt[r];
         }
-        p.depth_to_rgb = Affine3f::fromRt(rt);
+        p.depth_to_rgb = affine_from_rt(rt);
     }
 
     TopFu topfu(p);                                                  // A

@@ -91,7 +91,7 @@ namespace tfusion
                 int ok = 0, iters = 0;
                 const tf_status s = tf_icp_estimate(c, in, cl, pl, levels, rt, &ok, &iters);
                 if (s != TF_OK) throw std::runtime_error(std::string("tf_icp_estimate: ") + tf_status_string(s));
-                affine = Affine3f::fromRt(rt);
+                affine = affine_from_rt(rt);
                 last_iterations_ = iters;
                 return ok != 0;
             }

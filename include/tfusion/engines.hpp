@@ -188,7 +188,7 @@ namespace tfusion
     namespace detail
     {
         inline void intr4(const Intr& i, float out[4]) { out[0] = i.fx; out[1] = i.fy; out[2] = i.cx; out[3] = i.cy; }
-        inline void rt_of(const Affine3f& a, float rt[12]) { a.toRt(rt); }
+        inline void rt_of(const Affine3f& a, float rt[12]) { affine_to_rt(a, rt); }
         inline void rt_of(const Matrix4f& m, float rt[12]) { m.toRt(rt); }
     }
 

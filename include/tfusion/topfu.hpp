@@ -138,7 +138,7 @@ namespace tfusion
             c.vis_capacity = vis_capacity; c.max_render_blocks = max_render_blocks;
             c.voxel_rgb = integrate_colour ? 1 : 0;
             c.rgb_intr[0] = rgb_intr.fx; c.rgb_intr[1] = rgb_intr.fy; c.rgb_intr[2] = rgb_intr.cx; c.rgb_intr[3] = rgb_intr.cy;
-            depth_to_rgb.toRt(c.depth_to_rgb);
+            affine_to_rt(depth_to_rgb, c.depth_to_rgb);
             return c;
         }
     };
@@ -146,7 +146,7 @@ namespace tfusion
     class TopFu
     {
     public:
-        typedef std::shared_ptr<TopFu> Ptr;   // cv::Ptr<TopFu> in the reference
+        typedef SharedPtr<TopFu> Ptr;   // cv::Ptr<TopFu> (topfu.hpp:65); std::shared_ptr without OpenCV
 
         explicit TopFu(const TopFuParams& params) : params_(params)
         {
@@ -209,7 +209,7 @@ namespace tfusion
                 return false;
             }
             check(s, "tf_process_frame");
-            if (frame_counter_ > 0) poses_.push_back(Affine3f::fromRt(rt));   // poses_.back() * affine
+            if (frame_counter_ > 0) poses_.push_back(affine_from_rt(rt));   // poses_.back() * affine
             ++frame_counter_;
             return true;
         }

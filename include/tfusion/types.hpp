@@ -3,9 +3,17 @@
 //
 // Mirrors tfusion/include/tfusion/types.hpp (Intr :19-26, Point/Normal :30-40, cuda typedefs
 // :56-82, ScopeTime/SampledScopeTime :86-108) and tfusion/include/tfusion/cuda/device_array.hpp
-// (DeviceArray2D create/upload/download/ptr/step/rows/cols/release, :19-222).  OpenCV is not
-// required: Affine3f / Vec3f / Matx33f are small own types with the cv:: member names the
-// reference's callers use (matrix, rotation(), translation(), inv(), operator*, Identity()).
+// (DeviceArray2D create/upload/download/ptr/step/rows/cols/release, :19-222).
+//
+// The value types.  The reference typedefs them to OpenCV's (types.hpp:15-18: Mat3f = cv::Matx33f,
+// Vec3f / Vec3i = cv::Vec3f / cv::Vec3i, Affine3f = cv::Affine3f; TopFu::Ptr = cv::Ptr<TopFu>,
+// topfu.hpp:65), and apps/demo.cpp hands them to cv::viz (demo.cpp:35 volume_pose / volume_size,
+// :115 getCameraPose()).  Where OpenCV's headers exist (TFUSION_OPENCV_TYPES, detected with
+// __has_include(<opencv2/core/affine.hpp>); -DTFUSION_OPENCV_TYPES=0/1 overrides) they are the same
+// cv:: types, so demo.cpp compiles unchanged.  Without OpenCV they are small own types with the
+// cv:: member names the callers use (matrix, rotation(), translation(), inv(), operator*,
+// Identity(), translate(), all()).  Code here touches them only through that common subset and
+// the free functions affine_from_rt / affine_to_rt.
 #pragma once
 #include <hip/hip_runtime_api.h>
 
@@ -14,13 +22,41 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <utility>
 #include <vector>
 
+#ifndef TFUSION_OPENCV_TYPES
+#  if defined(__has_include)
+#    if __has_include(<opencv2/core/affine.hpp>)
+#      define TFUSION_OPENCV_TYPES 1
+#    endif
+#  endif
+#endif
+#ifndef TFUSION_OPENCV_TYPES
+#  define TFUSION_OPENCV_TYPES 0
+#endif
+
+#if TFUSION_OPENCV_TYPES
+#include <opencv2/core/core.hpp>
+#include <opencv2/core/affine.hpp>
+
 namespace tfusion
 {
+    typedef cv::Matx33f Mat3f;                 // types.hpp:15-18
+    typedef cv::Vec3f Vec3f;
+    typedef cv::Vec3i Vec3i;
+    typedef cv::Affine3f Affine3f;
+    typedef cv::Matx44f Matx44f;
+    template <class T> using SharedPtr = cv::Ptr<T>;     // TopFu::Ptr (topfu.hpp:65)
+}
+#else
+namespace tfusion
+{
+    template <class T> using SharedPtr = std::shared_ptr<T>;
+
     struct Vec3f {
         float val[3];
         Vec3f() : val{ 0.f, 0.f, 0.f } {}
@@ -43,9 +79,10 @@ namespace tfusion
         float& operator()(int r, int c) { return val[r * 3 + c]; }
     };
 
-    // cv::Matx44f subset: row-major 4x4, element (r, c) = val[4r + c]
+    // cv::Matx44f subset: row-major 4x4, element (r, c) = val[4r + c], zero-initialised like cv::Matx
     struct Matx44f {
         float val[16];
+        Matx44f() : val{} {}
         float operator()(int r, int c) const { return val[r * 4 + c]; }
         float& operator()(int r, int c) { return val[r * 4 + c]; }
     };
@@ -56,25 +93,12 @@ namespace tfusion
     struct Affine3f {
         Matx44f matrix;
         Affine3f() { *this = Identity(); }
+        explicit Affine3f(const Matx44f& m) : matrix(m) {}
         static Affine3f Identity()
         {
             Affine3f a(0);
             for (int i = 0; i < 4; ++i) a.matrix.val[i * 5] = 1.f;
             return a;
-        }
-        // from the C-ABI's row-major 3x4 [R|t]
-        static Affine3f fromRt(const float rt[12])
-        {
-            Affine3f a(0);
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 4; ++c) a.matrix(r, c) = rt[r * 4 + c];
-            a.matrix(3, 3) = 1.f;
-            return a;
-        }
-        void toRt(float rt[12]) const
-        {
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 4; ++c) rt[r * 4 + c] = matrix(r, c);
         }
         Mat3f rotation() const
         {
@@ -113,8 +137,27 @@ namespace tfusion
             return o;
         }
     private:
-        explicit Affine3f(int) : matrix{} {}
+        explicit Affine3f(int) : matrix() {}
     };
+}
+#endif
+
+namespace tfusion
+{
+    // the C-ABI's row-major 3x4 [R|t] <-> Affine3f (own or cv::)
+    inline Affine3f affine_from_rt(const float rt[12])
+    {
+        Matx44f m;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) m(r, c) = rt[r * 4 + c];
+        m(3, 3) = 1.f;
+        return Affine3f(m);
+    }
+    inline void affine_to_rt(const Affine3f& a, float rt[12])
+    {
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) rt[r * 4 + c] = a.matrix(r, c);
+    }
 
     // Matrix4f (tfusion/include/Matrix.hpp:22-66, 126-133): column-major, m[4c + r]; the 16-value
     // constructor fills m in argument order, so Matrix4f(P(0,0), P(1,0), P(2,0), P(3,0), P(0,1), ...)
@@ -237,6 +280,61 @@ namespace tfusion
             void* data_ = nullptr;
             size_t step_ = 0;
             int rows_ = 0, cols_ = 0;
+            int* ref_ = nullptr;
+        };
+
+        // DeviceArray<T> (device_array.hpp:19-96): a linear device buffer, reference-counted like
+        // DeviceArray2D (apps/demo.cpp:146 declares a DeviceArray<Point> cloud buffer)
+        template <typename T>
+        class DeviceArray
+        {
+        public:
+            typedef T type;
+            enum { elem_size = sizeof(T) };
+            DeviceArray() = default;
+            explicit DeviceArray(size_t size) { create(size); }
+            DeviceArray(const DeviceArray& o) : data_(o.data_), size_(o.size_), ref_(o.ref_) { if (ref_) ++*ref_; }
+            DeviceArray& operator=(const DeviceArray& o)
+            {
+                if (this != &o) { release(); data_ = o.data_; size_ = o.size_; ref_ = o.ref_; if (ref_) ++*ref_; }
+                return *this;
+            }
+            ~DeviceArray() { release(); }
+            void create(size_t size)
+            {
+                if (data_ && size == size_) return;
+                release();
+                if (size == 0) return;
+                hip_check(hipMalloc(&data_, sizeof(T) * size), "DeviceArray::create");
+                size_ = size;
+                ref_ = new int(1);
+            }
+            void release()
+            {
+                if (ref_ && --*ref_ == 0) { (void)hipFree(data_); delete ref_; }
+                data_ = nullptr; ref_ = nullptr; size_ = 0;
+            }
+            void upload(const T* host, size_t size)
+            {
+                create(size);
+                hip_check(hipMemcpy(data_, host, sizeof(T) * size, hipMemcpyHostToDevice), "DeviceArray::upload");
+            }
+            void download(T* host) const
+            {
+                hip_check(hipMemcpy(host, data_, sizeof(T) * size_, hipMemcpyDeviceToHost), "DeviceArray::download");
+            }
+            void upload(const std::vector<T>& v) { upload(v.data(), v.size()); }
+            void download(std::vector<T>& v) const { v.resize(size_); if (size_) download(v.data()); }
+            void swap(DeviceArray& o) { std::swap(data_, o.data_); std::swap(size_, o.size_); std::swap(ref_, o.ref_); }
+            bool empty() const { return data_ == nullptr; }
+            size_t size() const { return size_; }
+            size_t sizeBytes() const { return size_ * sizeof(T); }
+            T* ptr() { return static_cast<T*>(data_); }
+            const T* ptr() const { return static_cast<const T*>(data_); }
+
+        private:
+            void* data_ = nullptr;
+            size_t size_ = 0;
             int* ref_ = nullptr;
         };
 

@@ -115,3 +115,26 @@ def test_demo_headless_pgm_sequence(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     m = re.search(r"frames (\d+) ok (\d+) resets (\d+)", r.stdout)
     assert m and int(m.group(1)) == 12 and int(m.group(2)) >= 8, r.stdout
+
+
+def test_cv_types_alias_compiles():
+    """where OpenCV exists the tfusion value types are OpenCV's own
+    (include/tfusion/types.hpp, TFUSION_OPENCV_TYPES), so apps/demo.cpp's uses -- TopFu::Ptr as
+    cv::Ptr (demo.cpp:30), params.volume_size / volume_pose and getCameraPose() handed to cv::viz
+    (:34-35, :115), cuda::DeviceArray<Point> (:146), OpenNISource (io/capture.hpp) -- compile with
+    no conversion.  Compile-only, against the stand-in cv headers of tests/cvstub (OpenCV is absent
+    from this image)."""
+    src = os.path.join(ROOT, "tests", "cvstub", "demo_api_check.cpp")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-DTFUSION_OPENCV_TYPES=1",
+                        "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROOT, "tests", "cvstub"),
+                        "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include", src],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    # and without OpenCV (this image) the same headers pick their own types
+    probe = ('#include <tfusion/types.hpp>\n#include <type_traits>\n'
+             'static_assert(TFUSION_OPENCV_TYPES == 0, "no OpenCV here");\n'
+             'static_assert(std::is_same<tfusion::SharedPtr<int>, std::shared_ptr<int>>::value, "");\nint main(){}\n')
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++", "-D__HIP_PLATFORM_AMD__",
+                        "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include", "-"],
+                       input=probe, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
