@@ -392,8 +392,11 @@ static int icp_row(const float* vcurr, const float* ncurr, const float* vprev, c
     if (isnan(s.x)) return 40;
     f3 R0 = mk3(aff[0], aff[1], aff[2]), R1 = mk3(aff[4], aff[5], aff[6]), R2 = mk3(aff[8], aff[9], aff[10]);
     s = mk3(kdot(R0, s) + aff[3], kdot(R1, s) + aff[7], kdot(R2, s) + aff[11]);   /* aff * s, device.hpp:70-72 */
-    float coox = fmaf(fx, s.x / s.z, cx);                                        /* proj, proj_icp.cu:31-37 */
-    float cooy = fmaf(fy, s.y / s.z, cy);
+    /* proj, proj_icp.cu:31-37: __fmaf_rn(f, __fdividef(p.x, p.z), c) -- __fdividef is x times an
+       approximate reciprocal of y; canonical: x * RN(1 / y), one reciprocal for both coordinates */
+    const float rz = 1.0f / s.z;
+    float coox = fmaf(fx, s.x * rz, cx);
+    float cooy = fmaf(fy, s.y * rz, cy);
     if (s.z <= 0 || coox < 0 || cooy < 0 || coox >= (float)W || cooy >= (float)H) return 80;
     int tx = (int)floorf(coox), ty = (int)floorf(cooy);                         /* point-sampled tex2D */
     const float* dp = vprev + 4 * (ty * W + tx);

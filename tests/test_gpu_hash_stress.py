@@ -101,9 +101,13 @@ def test_hall_renderer_gpu_equals_numpy():
         assert ((want > 0) & (want < 2047)).mean() > 0.2, k        # surface in computeDists' range
 
 
-def test_fuse_frames_equals_per_call_engine(oracle_mod):
+@pytest.mark.parametrize("fuse_tail", ["1", "0"])
+def test_fuse_frames_equals_per_call_engine(oracle_mod, monkeypatch, fuse_tail):
     """tf_scene_fuse_frames == tf_imgproc_compute_dists + tf_scene_alloc + tf_scene_integrate per
-    frame (GPU vs GPU, whole state), and both == the oracle, over 24 hall frames."""
+    frame (GPU vs GPU, whole state), and both == the oracle, over 24 hall frames.  fuse_tail 1
+    (default): four launches per frame, frame k+1's head (dists, matrices, setToType3) in frame k's
+    integration grid; 0: the seven-launch form."""
+    monkeypatch.setenv("TFUSION_FUSE_TAIL", fuse_tail)
     from topfusion_amd import TopFu, _lib as L
     n = 24
     R, t, w2c = _walk(n)

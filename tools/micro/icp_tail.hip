@@ -47,6 +47,32 @@ __global__ void k_tail(const float* in, float* out, long long* cyc, int n, int w
             float f = (float)dx;
             for (int k = 0; k < 10; ++k) f = 1.0f / (f + 1.0f);
             dx = f;
+        } else if (which == 8) {                // the reference's cv::solve(DECOMP_SVD) (ALG 4)
+            float rv[6];
+            icp_cv_solve_svd6(Am, bv, rv);
+            bv[0] += rv[0] * 1e-30f;
+        } else if (which == 9) {                // cv solve + Affine3f rotation + compose
+            float rv[6], R[9], tinc[12];
+            icp_solve_rodrigues<4>(Am, bv, rv, R);
+            for (int j = 0; j < 3; ++j) {
+                tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1];
+                tinc[j * 4 + 2] = R[j * 3 + 2]; tinc[j * 4 + 3] = rv[3 + j];
+            }
+            tf_rigid_mul(tinc, aff, aff);
+            bv[0] += aff[3] * 1e-30f;
+        } else if (which == 10) {               // 10 dependent f64 adds
+            for (int k = 0; k < 10; ++k) dx = dx + 1e-3;
+        } else if (which == 11) {               // 10 dependent f64 muls
+            for (int k = 0; k < 10; ++k) dx = dx * 0.999;
+        } else if (which == 12) {               // 10 dependent (readlane -> f32 add) round trips
+            float f = (float)dx + (float)threadIdx.x;
+            for (int k = 0; k < 10; ++k)
+                f = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), k)) + 1.0f + (float)threadIdx.x;
+            dx = f;
+        } else if (which == 13) {               // 10 dependent f32 adds
+            float f = (float)dx;
+            for (int k = 0; k < 10; ++k) f = f + 1e-3f;
+            dx = f;
         }
     }
     const long long t1 = clock64();
@@ -61,12 +87,13 @@ int main()
     for (int i = 0; i < 6; ++i) for (int j = 0; j < 6; ++j) hA[i * 6 + j] = (i == j) ? 1000.f + 10 * i : 3.f / (1 + i + j);
     for (int i = 0; i < 6; ++i) hA[36 + i] = 0.01f * (i + 1);
     float *dA, *dO; long long* dC;
-    hipMalloc(&dA, sizeof(hA)); hipMalloc(&dO, 64); hipMalloc(&dC, 8 * sizeof(long long));
+    hipMalloc(&dA, sizeof(hA)); hipMalloc(&dO, 64 * 4); hipMalloc(&dC, 16 * sizeof(long long));
     hipMemcpy(dA, hA, sizeof(hA), hipMemcpyHostToDevice);
     const int N = 1000;
     const char* names[] = { "solve+rodrigues+compose", "solve (LDL^T)", "rodrigues", "10x f64 div", "10x f64 sqrt",
-                            "10x f64 fma", "10x f32 fma", "10x f32 div" };
-    for (int w = 0; w < 8; ++w) {
+                            "10x f64 fma", "10x f32 fma", "10x f32 div", "cv solve (SVD)", "cv solve+rot+compose",
+                            "10x f64 add", "10x f64 mul", "10x readlane+add", "10x f32 add" };
+    for (int w = 0; w < 14; ++w) {
         hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, 0, dA, dO, dC, 10, w);   // warm
         hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, 0, dA, dO, dC, N, w);
         long long c = 0;

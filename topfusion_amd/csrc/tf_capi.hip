@@ -154,7 +154,7 @@ static void ctx_free(tf_ctx* c)
                      c->visCounts, c->visAgg, c->visibleIds, c->visType, c->range, c->range_render, c->raycast, c->grey,
                      c->blockRec, c->blockTiles, c->blockOff, c->edChunk, c->edSpill, c->edBins, c->edBinCnt, c->edDone, c->depth_in, c->dists, c->icp_partial, c->icp_ticket, c->icp_tagged, c->st,
                      c->swapState, c->swapFlags, c->swapStore, c->swapCounts,
-                     c->vba_rgb_guard, c->rgb_in, c->integ_cnt, c->fuse_pose, c->fuse_rec, c->tile_cost, c->tile_order };
+                     c->vba_rgb_guard, c->rgb_in, c->integ_cnt, c->fuse_pose, c->fuse_rec, c->fuse_dists, c->tile_cost, c->tile_order };
     for (void* b : bufs) if (b) (void)hipFree(b);
     // pyramid maps: one allocation per map (level 0 is the base; swaps keep levels together)
     float4* maps[4] = { c->curr_pts[0], c->curr_nrm[0], c->prev_pts[0], c->prev_nrm[0] };
@@ -377,6 +377,9 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         // (past the ICP: the sticky-error path)
         env = getenv("TFUSION_FILL_FAULT");
         c->fill_fault_launch = env ? atoll(env) : 0;
+        // TFUSION_FUSE_TAIL=0: engine batches in the 7-launch form (A/B)
+        env = getenv("TFUSION_FUSE_TAIL");
+        c->fuse_tail = !(env && env[0] == '0');
         // TFUSION_VIS_FAULT=launch: that k_vis_build launch's wait for the lower chunks' counts fails
         env = getenv("TFUSION_VIS_FAULT");
         c->vis_fault_launch = env ? atoll(env) : 0;

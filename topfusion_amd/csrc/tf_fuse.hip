@@ -10,6 +10,8 @@
 // counters into the batch's record list.  This is the C5 hash-stress driver (capacity
 // saturation, silent allocation failure, eviction churn), so the frames carry no ICP and no
 // frame-mixing resets.
+#include <utility>
+
 #include "tf_internal.h"
 #include "tf_preproc.h"
 
@@ -52,6 +54,27 @@ hipError_t tfk_fuse_frames(tf_ctx* c, const uint16_t* frames, size_t stride, siz
     static_assert(sizeof(tf_fuse_record) == 10 * sizeof(int), "tf_fuse_record layout");
     const dim3 dg((c->W + 15) / 16, (c->H + 15) / 16);
     const int swapping = c->p.use_swapping ? 1 : 0;
+    if (!swapping && c->fuse_tail && n > 0) {
+        // four launches per frame: requests, apply, visible list, then k_fuse_tail -- frame k's
+        // integration and record beside frame k+1's head (dists into the other buffer, matrices,
+        // setToType3); the batch's first head alone before them.  c->dists alternates between the
+        // two buffers and ends on the last frame's.
+        if (!c->fuse_dists) {
+            const hipError_t e = hipMalloc((void**)&c->fuse_dists, sizeof(float) * (size_t)c->W * c->H);
+            if (e != hipSuccess) { c->fuse_dists = nullptr; return e; }
+        }
+        hipError_t e = tfk_fuse_head(c, frames, pitch, c->dists, c->fuse_pose);
+        for (int k = 0; k < n && e == hipSuccess; ++k) {
+            e = tfk_alloc(c, 2);                         // (setToType3 ran in the head)
+            if (e != hipSuccess) break;
+            const bool more = k + 1 < n;
+            const uint16_t* nf = more ? (const uint16_t*)((const char*)frames + (size_t)(k + 1) * stride) : nullptr;
+            e = tfk_fuse_tail(c, c->fuse_pose + 12 * (size_t)k, c->fuse_rec + 10 * (size_t)k, nf, pitch, c->fuse_dists,
+                              more ? c->fuse_pose + 12 * (size_t)(k + 1) : nullptr);
+            if (more) std::swap(c->dists, c->fuse_dists);
+        }
+        return e != hipSuccess ? e : hipGetLastError();
+    }
     for (int k = 0; k < n; ++k) {
         const uint16_t* f = (const uint16_t*)((const char*)frames + (size_t)k * stride);
         hipLaunchKernelGGL(k_fuse_begin, dg, dim3(256), 0, c->stream, f, pitch, c->W, c->H, c->dists,

@@ -445,7 +445,10 @@ __device__ __forceinline__ void ip_project2(const IcpLevel& L, const float* aff,
     sx = kdot2(ip_bc(aff[0]), ip_bc(aff[1]), ip_bc(aff[2]), vx, vy, vz) + ip_bc(aff[3]);
     sy = kdot2(ip_bc(aff[4]), ip_bc(aff[5]), ip_bc(aff[6]), vx, vy, vz) + ip_bc(aff[7]);
     sz = kdot2(ip_bc(aff[8]), ip_bc(aff[9]), ip_bc(aff[10]), vx, vy, vz) + ip_bc(aff[11]);
-    const ip_f2 qx = { sx.x / sz.x, sx.y / sz.y }, qy = { sy.x / sz.x, sy.y / sz.y };
+    // __fdividef(p.x, p.z) = p.x times an approximate reciprocal (proj_icp.cu:34-35): canonical
+    // p.x * RN(1 / p.z), one IEEE reciprocal per pixel for both coordinates, the products packed
+    const ip_f2 rz = { 1.0f / sz.x, 1.0f / sz.y };
+    const ip_f2 qx = sx * rz, qy = sy * rz;
     const ip_f2 coox = __builtin_elementwise_fma(ip_bc(L.fx), qx, ip_bc(L.cx));
     const ip_f2 cooy = __builtin_elementwise_fma(ip_bc(L.fy), qy, ip_bc(L.cy));
     ok0 = xy0 >= 0 && !isnan(vx.x) &&

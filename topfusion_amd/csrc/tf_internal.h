@@ -399,6 +399,8 @@ struct tf_ctx {
     long long vis_launches;
     long long vis_fault_launch;
     // engine-level batches (tf_scene_fuse_frames, tf_fuse.hip): the batch's poses and per-frame records
+    float* fuse_dists;                   // the second dists buffer of a batch (frame k+1's head runs beside frame k)
+    int fuse_tail;                       // TFUSION_FUSE_TAIL (default 1): 4 launches per frame (k_fuse_tail)
     float* fuse_pose;                    // [fuse_cap][12] world -> camera, row-major [R|t]
     int* fuse_rec;                       // [fuse_cap] tf_fuse_record
     int fuse_cap;
@@ -451,6 +453,9 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot = 0,       // snapshot: + the frame
 // frame_path: + frame-0 map copy; with_ed: CreateExpectedDepths' projection pass in the
 // grid's first TF_ED_BLOCKS workgroups (then tfk_expected_depths(c, 1) runs only the fill)
 hipError_t tfk_integrate(tf_ctx* c, int frame_path = 0, int with_ed = 0);
+hipError_t tfk_fuse_head(tf_ctx* c, const uint16_t* frame, size_t pitch, float* dists, const float* pose);
+hipError_t tfk_fuse_tail(tf_ctx* c, const float* pose, int* rec, const uint16_t* next_frame, size_t pitch,
+                         float* next_dists, const float* next_pose);
 hipError_t tfk_raycast(tf_ctx* c, int update_visible);
 hipError_t tfk_render_type(tf_ctx* c, int type);   // RenderImage pixel stage (tf_render_type) on raycast
 // CreateICPMaps raycast + renderImage, one launch (frame path); next: + that frame's dists/pyramid/normals

@@ -795,6 +795,11 @@ struct IntegArgs {
     unsigned* vba_rgb;
     float rfx, rfy, rcx, rcy;           // projParams_rgb
     float D[16];                        // calib_inv (depth -> rgb) as a column-major Matrix4f
+    // engine batches (k_fuse_tail): the frame's world -> camera pose [R|t] as given (so the pass
+    // does not read st->M_alloc, which the next frame's begin rewrites in the same grid) and the
+    // integration workgroups of the grid
+    const float* pose_rt;
+    int fuse_nwg;
 };
 
 // computeUpdatedVoxelDepthInfo (SceneReconstructionEngine.hpp:23-71) in two halves, so that
@@ -999,7 +1004,7 @@ __device__ __forceinline__ void integ_apply_pair(uint4 v, uint4 v2, const float 
     }
 }
 
-template <bool WITH_ED, bool RGB>
+template <bool WITH_ED, bool RGB, bool FUSED = false>
 __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
                                            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed,
                                            long long* __restrict__ cnt);
@@ -1052,7 +1057,7 @@ k_integrate_pass(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __
 {
     integ_body<false, false>(a, st, hash, visibleIds, vba, ed, cnt);
 }
-template <bool WITH_ED, bool RGB>
+template <bool WITH_ED, bool RGB, bool FUSED>
 __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
                                            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, EdArgs ed,
                                            long long* __restrict__ cnt)
@@ -1061,7 +1066,7 @@ __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__
     // reads only the visible list and the pose; integration writes only voxels): one launch
     // and its dispatch gap fewer per frame.  The stand-alone instance (stage entry points, C3I)
     // has no such branch: its grid-stride loop is the plain one.
-    int bid = blockIdx.x, nblk = gridDim.x;
+    int bid = blockIdx.x, nblk = FUSED ? a.fuse_nwg : (int)gridDim.x;
     if (WITH_ED) {
         if (bid < TF_ED_BLOCKS) { ed_project_block(ed, st, bid, TF_ED_BLOCKS); return; }
         bid -= TF_ED_BLOCKS; nblk -= TF_ED_BLOCKS;
@@ -1083,8 +1088,12 @@ __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__
     // cached for the raycasts that read them next
     const bool stream = n > TF_INTEG_STREAM_BLOCKS;
     float M[16];
+    if (FUSED) {
+        tf_rt_to_m4(a.pose_rt, M);               // M_alloc of a given world -> camera pose (alloc_mode 2)
+    } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) M[i] = st->M_alloc[i];
+        for (int i = 0; i < 16; ++i) M[i] = st->M_alloc[i];
+    }
     // M_rgb = calib_inv * M_d (SceneReconstructionEngine_host.cu:217), Matrix4 operator*
     // (Matrix.hpp:113-119): r(x, y) += lhs(k, y) * rhs(x, k) from zero
     float Mr[16];
@@ -1182,7 +1191,129 @@ __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__
     }
 }
 
-hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
+// ---------------------------------------------------------------------------------------
+// Engine-level batches (tf_scene_fuse_frames, tf_fuse.hip), four launches per frame.  Frame
+// k+1's head -- computeDists of its raw depth into the other dists buffer, its pose matrices, and
+// setToType3 over frame k's visible list with frame k+1's visibility test (k_set_type3) --
+// shares no data with frame k's IntegrateIntoScene (voxels, read-only list and hash, frame k's
+// dists and pose passed as arguments) nor with frame k's record (counters no head writes), so all
+// three run in one grid: k_fuse_tail.  The allocation launches then need no head of their own.
+// ---------------------------------------------------------------------------------------
+struct FuseNext {
+    const uint16_t* frame;              // frame k+1's raw depth (nullptr: no next frame)
+    size_t pitch;
+    float* dists;                       // -> its dists buffer
+    const float* pose;                  // its world -> camera pose [R|t]
+    int dg_x, n_dists;                  // 16x16 dists tiles
+};
+
+// setToType3 with the frame's own visibility test, computeDists, and (workgroup 0) the frame's
+// matrices and flags (k_fuse_begin, tf_fuse.hip); b in [0, 256 + n_dists)
+__device__ __forceinline__ void fuse_head_part(int b, const FuseNext& f, const VisArgs& v, TfDevState* __restrict__ st,
+                                               const TfHashEntry* __restrict__ hash, const int* __restrict__ visibleIds,
+                                               unsigned char* __restrict__ visType)
+{
+    if (b < 256) {
+        float pose[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) pose[i] = f.pose[i];
+        const int halted = st->halt;                       // (only a frame end writes it)
+        if (b == 0 && threadIdx.x == 0) {
+            tf_set_pose_matrices(st, pose, 2);
+            st->abort = halted ? 1 : 0;
+            st->mode = 1;
+        }
+        if (halted) return;
+        float M[16];
+        tf_rt_to_m4(pose, M);
+        set_type3_pass(v, st->noVisibleEntries, M, hash, visibleIds, visType, b * 256 + threadIdx.x, 256 * 256);
+        return;
+    }
+    b -= 256;
+    const int x = (b % f.dg_x) * 16 + (threadIdx.x & 15), y = (b / f.dg_x) * 16 + (threadIdx.x >> 4);
+    if (x >= v.W || y >= v.H) return;
+    f.dists[y * v.W + x] = tf_dist_of(*(const uint16_t*)((const char*)f.frame + (size_t)y * f.pitch + (size_t)x * 2));
+}
+
+// the batch's first frame: its head alone
+__global__ void __launch_bounds__(256)
+k_fuse_head(FuseNext f, VisArgs v, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+            const int* __restrict__ visibleIds, unsigned char* __restrict__ visType)
+{
+    fuse_head_part((int)blockIdx.x, f, v, st, hash, visibleIds, visType);
+}
+
+// frame k: IntegrateIntoScene (workgroups [0, a.fuse_nwg)), its record (tf_fuse_record, the next
+// workgroup), then frame k+1's head
+__global__ void __launch_bounds__(256)
+k_fuse_tail(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restrict__ hash,
+            const int* __restrict__ visibleIds, TfVoxel* __restrict__ vba, long long* __restrict__ cnt,
+            int* __restrict__ rec, FuseNext f, VisArgs v, unsigned char* __restrict__ visType)
+{
+    const int b = (int)blockIdx.x;
+    if (b < a.fuse_nwg) {
+        integ_body<false, false, true>(a, st, hash, visibleIds, vba, EdArgs{}, cnt);
+        return;
+    }
+    if (b == a.fuse_nwg) {
+        if (threadIdx.x == 0) {
+            rec[0] = st->lastFreeBlockId;
+            rec[1] = st->lastFreeExcessListId;
+            rec[2] = st->noVisibleEntries;
+            rec[3] = st->alloc_fail[0];
+            rec[4] = st->alloc_fail[1];
+            rec[5] = rec[6] = rec[7] = rec[8] = rec[9] = 0;           // (no swapping on this path)
+        }
+        return;
+    }
+    fuse_head_part(b - a.fuse_nwg - 1, f, v, st, hash, visibleIds, visType);
+}
+
+static VisArgs make_vis_args(tf_ctx* c)
+{
+    VisArgs v;
+    v.fx = c->p.fx; v.fy = c->p.fy; v.cx = c->p.cx; v.cy = c->p.cy;
+    v.factor = (float)TF_BLK * c->p.voxelSize;
+    v.W = c->W; v.H = c->H; v.n_total = c->n_total; v.cap = c->p.vis_capacity;
+    v.enlarged = 0;
+    return v;
+}
+
+static FuseNext make_fuse_next(tf_ctx* c, const uint16_t* frame, size_t pitch, float* dists, const float* pose)
+{
+    FuseNext f;
+    f.frame = frame; f.pitch = pitch; f.dists = dists; f.pose = pose;
+    f.dg_x = (c->W + 15) / 16;
+    f.n_dists = frame ? f.dg_x * ((c->H + 15) / 16) : 0;
+    return f;
+}
+
+static IntegArgs make_integ_args(tf_ctx* c, int frame_path);
+
+hipError_t tfk_fuse_head(tf_ctx* c, const uint16_t* frame, size_t pitch, float* dists, const float* pose)
+{
+    const FuseNext f = make_fuse_next(c, frame, pitch, dists, pose);
+    hipLaunchKernelGGL(k_fuse_head, dim3(256 + f.n_dists), dim3(256), 0, c->stream, f, make_vis_args(c), c->st, c->hash,
+                       c->visibleIds, c->visType);
+    return hipGetLastError();
+}
+
+// frame k (its dists in c->dists, its pose `pose`, record `rec`) + frame k+1's head (next_frame
+// nullptr: none)
+hipError_t tfk_fuse_tail(tf_ctx* c, const float* pose, int* rec, const uint16_t* next_frame, size_t pitch,
+                         float* next_dists, const float* next_pose)
+{
+    IntegArgs a = make_integ_args(c, 0);
+    a.pose_rt = pose;
+    a.fuse_nwg = c->integ_wg_frame;
+    const FuseNext f = make_fuse_next(c, next_frame, pitch, next_dists, next_pose);
+    const int nwg = a.fuse_nwg + 1 + (next_frame ? 256 + f.n_dists : 0);
+    hipLaunchKernelGGL(k_fuse_tail, dim3(nwg), dim3(256), 0, c->stream, a, c->st, c->hash, c->visibleIds, c->vba,
+                       c->integ_cnt, rec, f, make_vis_args(c), c->visType);
+    return hipGetLastError();
+}
+
+static IntegArgs make_integ_args(tf_ctx* c, int frame_path)
 {
     IntegArgs a;
     a.curr_pts = c->curr_pts[0]; a.curr_nrm = c->curr_nrm[0]; a.prev_pts = c->prev_pts[0]; a.prev_nrm = c->prev_nrm[0];
@@ -1193,7 +1324,6 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
     a.fx = c->p.fx; a.fy = c->p.fy; a.cx = c->p.cx; a.cy = c->p.cy;
     a.voxelSize = c->p.voxelSize; a.mu = c->p.mu; a.maxW = c->p.maxW;
     a.inv_mu = 1.0f / c->p.mu; a.mu_exact3 = c->mu_exact3;
-    const bool rgb = c->p.voxel_rgb && c->rgb_cur;
     a.rgb = c->rgb_cur; a.rgb_pitch = c->rgb_pitch; a.vba_rgb = c->vba_rgb;
     const float* q = c->p.rgb_intr;
     const bool depth_intr = q[0] == 0 && q[1] == 0 && q[2] == 0 && q[3] == 0;   // rgb_intr all 0
@@ -1203,6 +1333,15 @@ hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
     for (int col = 0; col < 4; ++col)
         for (int row = 0; row < 4; ++row)
             a.D[4 * col + row] = row < 3 ? d[4 * row + col] : (col == 3 ? 1.0f : 0.0f);
+    a.pose_rt = nullptr;
+    a.fuse_nwg = 0;
+    return a;
+}
+
+hipError_t tfk_integrate(tf_ctx* c, int frame_path, int with_ed)
+{
+    IntegArgs a = make_integ_args(c, frame_path);
+    const bool rgb = c->p.voxel_rgb && c->rgb_cur;
     EdArgs ed = {};
     // stand-alone: 2560 workgroups, two rounds of the 5 per CU that k_integrate_pass's register
     // budget keeps resident (C3I 2.354 -> 2.317 ms against 2048 at 4 per CU; one round of exactly
