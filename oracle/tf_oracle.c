@@ -210,7 +210,9 @@ void tfo_rodrigues(const float r[3], float R[9])
     }
     if (t2 > 9.869604401089358) { rodrigues_sqrt(r, R); return; }
     double pc = 1.0, pa = 1.0, pb = 1.0;
-    const int nt = t2 < 0.015625 ? 6 : 13;
+    /* terms: 4 below t^2 = 2^-12 (an ICP increment past its first iteration; the first omitted term
+       is below 2^-60 relative), 6 below 1/64 (below 2^-80), else 13 */
+    const int nt = t2 < 0.000244140625 ? 4 : (t2 < 0.015625 ? 6 : 13);
     for (int n = nt; n >= 1; --n) {
         pc = fma(-(t2 * k_inv_cos[n]), pc, 1.0);
         pa = fma(-(t2 * k_inv_sin[n]), pa, 1.0);
@@ -498,37 +500,60 @@ static double cv_det6(const float Ain[36])
     return det;
 }
 
-/* cv::solve(A, b, DECOMP_SVD) replacement.  A is the symmetric normal matrix J^T J, already
-   past the determinant check: LDL^T in double (lower triangle of A, one reciprocal per pivot),
-   then forward, diagonal and backward substitution.  Few dependent operations -- the GPU runs
-   this on one wave between two iterations (tf_icp.hip: icp_solve6_ldl, same operation order) */
+/* cv::solve(A, b, DECOMP_SVD) replacement (the canonical algebra; the reference's own is
+   tfo_cv_solve_svd6 below).  A is the symmetric normal matrix J^T J, already past the determinant
+   check.  2 x 2 block elimination in double with closed-form 3 x 3 inverses (adjugate / det):
+   A = [P Q; Q^T R] (P the rotation block, R the translation block), b = [b1; b2],
+     T = Q adj(R) / det(R),  S = P - T Q^T,  c = b1 - T b2,
+     x1 = adj(S) c / det(S),  x2 = adj(R) (b2 - Q^T x1) / det(R).
+   Its critical path is two 3 x 3 determinants and two divisions deep (~35 dependent operations
+   against ~110 for a column-by-column LDL^T), and the rotation part x1 -- what Rodrigues needs --
+   comes first.  The GPU's serial ICP tail runs exactly this (tf_icp_tail.h icp_solve6_schur). */
+static void sym3_adj(const double M[3][3], double C[3][3], double* det)
+{
+    C[0][0] = M[1][1] * M[2][2] - M[1][2] * M[2][1];
+    C[0][1] = M[0][2] * M[2][1] - M[0][1] * M[2][2];
+    C[0][2] = M[0][1] * M[1][2] - M[0][2] * M[1][1];
+    C[1][0] = M[1][2] * M[2][0] - M[1][0] * M[2][2];
+    C[1][1] = M[0][0] * M[2][2] - M[0][2] * M[2][0];
+    C[1][2] = M[0][2] * M[1][0] - M[0][0] * M[1][2];
+    C[2][0] = M[1][0] * M[2][1] - M[1][1] * M[2][0];
+    C[2][1] = M[0][1] * M[2][0] - M[0][0] * M[2][1];
+    C[2][2] = M[0][0] * M[1][1] - M[0][1] * M[1][0];
+    *det = (M[0][0] * C[0][0] + M[0][1] * C[1][0]) + M[0][2] * C[2][0];
+}
+
 static void solve6(const float Af[36], const float bf[6], float x[6])
 {
-    double L[36], d[6], r[6], y[6], xs[6];
-    for (int j = 0; j < 6; ++j) {
-        double w[6];
-        for (int k = 0; k < j; ++k) w[k] = L[j * 6 + k] * d[k];
-        double dj = Af[j * 6 + j];
-        for (int k = 0; k < j; ++k) dj = dj - L[j * 6 + k] * w[k];
-        d[j] = dj;
-        r[j] = 1.0 / dj;
-        for (int i = j + 1; i < 6; ++i) {
-            double s = Af[i * 6 + j];
-            for (int k = 0; k < j; ++k) s = s - L[i * 6 + k] * w[k];
-            L[i * 6 + j] = s * r[j];
+    double P[3][3], Q[3][3], R[3][3], b1[3], b2[3];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) {
+            P[i][j] = Af[i * 6 + j];
+            Q[i][j] = Af[i * 6 + 3 + j];
+            R[i][j] = Af[(3 + i) * 6 + 3 + j];
         }
+        b1[i] = bf[i];
+        b2[i] = bf[3 + i];
     }
-    for (int i = 0; i < 6; ++i) {
-        double s = bf[i];
-        for (int k = 0; k < i; ++k) s = s - L[i * 6 + k] * y[k];
-        y[i] = s;
+    double aR[3][3], dR, aS[3][3], dS, T[3][3], S[3][3], c[3], x1[3], e[3];
+    sym3_adj(R, aR, &dR);
+    const double rR = 1.0 / dR;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            T[i][j] = ((Q[i][0] * aR[0][j] + Q[i][1] * aR[1][j]) + Q[i][2] * aR[2][j]) * rR;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j)
+            S[i][j] = P[i][j] - ((T[i][0] * Q[j][0] + T[i][1] * Q[j][1]) + T[i][2] * Q[j][2]);
+        c[i] = b1[i] - ((T[i][0] * b2[0] + T[i][1] * b2[1]) + T[i][2] * b2[2]);
     }
-    for (int i = 5; i >= 0; --i) {
-        double s = y[i] * r[i];
-        for (int k = i + 1; k < 6; ++k) s = s - L[k * 6 + i] * xs[k];
-        xs[i] = s;
+    sym3_adj(S, aS, &dS);
+    const double rS = 1.0 / dS;
+    for (int i = 0; i < 3; ++i) x1[i] = ((aS[i][0] * c[0] + aS[i][1] * c[1]) + aS[i][2] * c[2]) * rS;
+    for (int i = 0; i < 3; ++i) e[i] = b2[i] - ((Q[0][i] * x1[0] + Q[1][i] * x1[1]) + Q[2][i] * x1[2]);
+    for (int i = 0; i < 3; ++i) {
+        x[i] = (float)x1[i];
+        x[3 + i] = (float)(((aR[i][0] * e[0] + aR[i][1] * e[1]) + aR[i][2] * e[2]) * rR);
     }
-    for (int i = 0; i < 6; ++i) x[i] = (float)xs[i];
 }
 
 /* ------------------------------------------------------------------------- */

@@ -183,9 +183,18 @@ def test_swapping_batched_and_save_load(oracle_mod):
     okg = g.process_frames(dev.ptr, len(angles))
     oko = np.array([o(seq[k]) for k in range(len(angles))])
     assert np.array_equal(okg, oko), (okg, oko)
+    dev.free()
+    # the reference's frame-mixing resets empty the GlobalCache: where the sequence ended on one,
+    # the orbit continues (one-frame batches) until blocks are stored again, so save / load has data
+    k = len(angles)
+    while o.swap_stored_flags().sum() == 0 and k < len(angles) + 40:
+        d = synth.render_depth(*synth.orbit_pose(1, deg_per_frame=float(k - len(angles))), W, H, noise_mm=1.0, seed=9000 + k)
+        one = DeviceFrames(d[None])
+        assert bool(g.process_frames(one.ptr, 1)[0]) == o(d), k
+        one.free()
+        k += 1
     _compare(g, o, "batched final", stored=True)
     assert o.swap_stored_flags().sum() > 0
-    dev.free()
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "cache.bin")
         g.swap_save(path)

@@ -17,17 +17,20 @@ __global__ void k_tail(const float* in, float* out, long long* cyc, int n, int w
     for (int it = 0; it < n; ++it) {
         if (which == 0) {                       // solve + Rodrigues + compose (the tail)
             float rv[6], R[9], tinc[12];
-            icp_solve6_ldl(Am, bv, rv);
-            icp_rodrigues(rv, R);
+            icp_solve_rodrigues<0>(Am, bv, rv, R);
             for (int j = 0; j < 3; ++j) {
                 tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1];
                 tinc[j * 4 + 2] = R[j * 3 + 2]; tinc[j * 4 + 3] = rv[3 + j];
             }
             tf_rigid_mul(tinc, aff, aff);
             bv[0] += aff[3] * 1e-30f;           // next repetition depends on this one
-        } else if (which == 1) {                // solve only
+        } else if (which == 1) {                // solve only (LDL^T, rounds 2-4)
             float rv[6];
             icp_solve6_ldl(Am, bv, rv);
+            bv[0] += rv[0] * 1e-30f;
+        } else if (which == 14) {               // solve only (2 x 2 block Schur, round 5)
+            float rv[6];
+            icp_solve6_schur(Am, bv, rv);
             bv[0] += rv[0] * 1e-30f;
         } else if (which == 2) {                // Rodrigues only
             float rv[6] = { bv[0] * 1e-3f, bv[1] * 1e-3f, bv[2] * 1e-3f, 0, 0, 0 }, R[9];
@@ -90,10 +93,10 @@ int main()
     hipMalloc(&dA, sizeof(hA)); hipMalloc(&dO, 64 * 4); hipMalloc(&dC, 16 * sizeof(long long));
     hipMemcpy(dA, hA, sizeof(hA), hipMemcpyHostToDevice);
     const int N = 1000;
-    const char* names[] = { "solve+rodrigues+compose", "solve (LDL^T)", "rodrigues", "10x f64 div", "10x f64 sqrt",
+    const char* names[] = { "solve+rodrigues+compose (canonical)", "solve (LDL^T, r2-4)", "rodrigues", "10x f64 div", "10x f64 sqrt",
                             "10x f64 fma", "10x f32 fma", "10x f32 div", "cv solve (SVD)", "cv solve+rot+compose",
-                            "10x f64 add", "10x f64 mul", "10x readlane+add", "10x f32 add" };
-    for (int w = 0; w < 14; ++w) {
+                            "10x f64 add", "10x f64 mul", "10x readlane+add", "10x f32 add", "solve (block Schur)" };
+    for (int w = 0; w < 15; ++w) {
         hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, 0, dA, dO, dC, 10, w);   // warm
         hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, 0, dA, dO, dC, N, w);
         long long c = 0;

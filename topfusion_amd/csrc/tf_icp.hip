@@ -297,6 +297,9 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 // error) so no wave can outlive a missing peer.
 // =========================================================================================
 #define IP_WAVES 8
+#ifndef TF_PROJ_DIV
+#define TF_PROJ_DIV 0
+#endif
 #define IP_SREG 1                       // CTA slots kept in registers per wave (8 per WG; larger images use k_icp_iter)
 #define IP_SPIN_LIMIT (1u << 21)
 #ifndef IP_SLEEP
@@ -446,8 +449,12 @@ __device__ __forceinline__ void ip_project2(const IcpLevel& L, const float* aff,
     sy = kdot2(ip_bc(aff[4]), ip_bc(aff[5]), ip_bc(aff[6]), vx, vy, vz) + ip_bc(aff[7]);
     sz = kdot2(ip_bc(aff[8]), ip_bc(aff[9]), ip_bc(aff[10]), vx, vy, vz) + ip_bc(aff[11]);
     // __fdividef(p.x, p.z) = p.x times an approximate reciprocal (proj_icp.cu:34-35): canonical
-    // p.x * RN(1 / p.z), one IEEE reciprocal per pixel for both coordinates, the products packed
+    // p.x * RN(1 / p.z), one reciprocal per pixel for both coordinates, the products packed
+#if TF_PROJ_DIV                                   // A/B only: the IEEE division sequence for RN(1 / z)
     const ip_f2 rz = { 1.0f / sz.x, 1.0f / sz.y };
+#else
+    const ip_f2 rz = { tf_rcp_rn(sz.x), tf_rcp_rn(sz.y) };
+#endif
     const ip_f2 qx = sx * rz, qy = sy * rz;
     const ip_f2 coox = __builtin_elementwise_fma(ip_bc(L.fx), qx, ip_bc(L.cx));
     const ip_f2 cooy = __builtin_elementwise_fma(ip_bc(L.fy), qy, ip_bc(L.cy));

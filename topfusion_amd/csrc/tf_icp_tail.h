@@ -47,6 +47,9 @@ __device__ __forceinline__ void icp_sincos(double th, double* s, double* c)
 // two-chain form it replaces was ~40 dependent f64 operations, 0.9 us of every ICP iteration;
 // the CPU restatement computes the same).  t > pi (never for an ICP
 // increment) takes that form.  TF_RODRIGUES_SINC=0: the old form throughout (A/B).
+#ifndef TF_SOLVE_LDL
+#define TF_SOLVE_LDL 0
+#endif
 #ifndef TF_RODRIGUES_SINC
 #define TF_RODRIGUES_SINC 1
 #endif
@@ -66,7 +69,14 @@ __device__ __forceinline__ void icp_rodrigues(const float* rv, float* R)
     }
     if (t2 > 9.869604401089358) { icp_rodrigues_sqrt(rv, R); return; }   // t > pi
     double pc = 1.0, pa = 1.0, pb = 1.0;          // cos t, sin t / t, 2 (1 - cos t) / t^2
-    if (t2 < 0.015625) {                          // t < 1/8: 6 terms (first omitted < 2^-80 relative)
+    if (t2 < 0.000244140625) {                    // t < 1/64: 4 terms (first omitted < 2^-60 relative)
+#pragma unroll
+        for (int n = 4; n >= 1; --n) {
+            pc = fma(-(t2 * inv_cos[n]), pc, 1.0);
+            pa = fma(-(t2 * inv_sin[n]), pa, 1.0);
+            pb = fma(-(t2 * inv_cos[n + 1]), pb, 1.0);
+        }
+    } else if (t2 < 0.015625) {                   // t < 1/8: 6 terms (first omitted < 2^-80 relative)
 #pragma unroll
         for (int n = 6; n >= 1; --n) {
             pc = fma(-(t2 * inv_cos[n]), pc, 1.0);
@@ -160,7 +170,69 @@ __device__ __forceinline__ double icp_det6_reg(const float (&A0)[6][6])
     return det;
 }
 
-// cv::solve(A, b, DECOMP_SVD) replacement (oracle/tf_oracle.c:solve6, same operation order):
+// cv::solve(A, b, DECOMP_SVD) replacement, the canonical form (oracle/tf_oracle.c:solve6, same
+// operations in the same order): 2 x 2 block elimination in double with closed-form 3 x 3 inverses,
+// A = [P Q; Q^T R], T = Q adj(R) / det R, S = P - T Q^T, x1 = adj(S) (b1 - T b2) / det S,
+// x2 = adj(R) (b2 - Q^T x1) / det R.  The serial tail waits on this chain: two 3 x 3 determinants
+// and two divisions deep (~35 dependent operations) against ~110 for the column-by-column LDL^T
+// below, and x1, which Rodrigues needs, comes before x2.
+__device__ __forceinline__ void icp_sym3_adj(const double (&M)[3][3], double (&C)[3][3], double& det)
+{
+    C[0][0] = M[1][1] * M[2][2] - M[1][2] * M[2][1];
+    C[0][1] = M[0][2] * M[2][1] - M[0][1] * M[2][2];
+    C[0][2] = M[0][1] * M[1][2] - M[0][2] * M[1][1];
+    C[1][0] = M[1][2] * M[2][0] - M[1][0] * M[2][2];
+    C[1][1] = M[0][0] * M[2][2] - M[0][2] * M[2][0];
+    C[1][2] = M[0][2] * M[1][0] - M[0][0] * M[1][2];
+    C[2][0] = M[1][0] * M[2][1] - M[1][1] * M[2][0];
+    C[2][1] = M[0][1] * M[2][0] - M[0][0] * M[2][1];
+    C[2][2] = M[0][0] * M[1][1] - M[0][1] * M[1][0];
+    det = (M[0][0] * C[0][0] + M[0][1] * C[1][0]) + M[0][2] * C[2][0];
+}
+
+__device__ __forceinline__ void icp_solve6_schur(const float (&Af)[6][6], const float (&bf)[6], float (&x)[6])
+{
+    double P[3][3], Q[3][3], R[3][3], b1[3], b2[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            P[i][j] = Af[i][j];
+            Q[i][j] = Af[i][3 + j];
+            R[i][j] = Af[3 + i][3 + j];
+        }
+        b1[i] = bf[i];
+        b2[i] = bf[3 + i];
+    }
+    double aR[3][3], dR, aS[3][3], dS, T[3][3], S[3][3], c[3], x1[3], e[3];
+    icp_sym3_adj(R, aR, dR);
+    const double rR = 1.0 / dR;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            T[i][j] = ((Q[i][0] * aR[0][j] + Q[i][1] * aR[1][j]) + Q[i][2] * aR[2][j]) * rR;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            S[i][j] = P[i][j] - ((T[i][0] * Q[j][0] + T[i][1] * Q[j][1]) + T[i][2] * Q[j][2]);
+        c[i] = b1[i] - ((T[i][0] * b2[0] + T[i][1] * b2[1]) + T[i][2] * b2[2]);
+    }
+    icp_sym3_adj(S, aS, dS);
+    const double rS = 1.0 / dS;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x1[i] = ((aS[i][0] * c[0] + aS[i][1] * c[1]) + aS[i][2] * c[2]) * rS;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) e[i] = b2[i] - ((Q[0][i] * x1[0] + Q[1][i] * x1[1]) + Q[2][i] * x1[2]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        x[i] = (float)x1[i];
+        x[3 + i] = (float)(((aR[i][0] * e[0] + aR[i][1] * e[1]) + aR[i][2] * e[2]) * rR);
+    }
+}
+
+// the previous canonical form (rounds 2-4), kept for tools/micro/icp_tail.hip:
 // LDL^T of the symmetric normal matrix in double with one reciprocal per pivot, then forward,
 // diagonal and backward substitution -- ~270 uniform operations with short dependency chains
 // (the pivoting elimination it replaces issued ~2.5x as many, 21 of them full divisions)
@@ -476,7 +548,11 @@ template <int ALG>
 __device__ __forceinline__ void icp_solve_rodrigues(const float (&Am)[6][6], const float (&bv)[6], float (&rv)[6], float* R)
 {
     if constexpr (ALG == 0) {
+#if TF_SOLVE_LDL                                  // A/B only: the rounds 2-4 form (not the oracle's)
         icp_solve6_ldl(Am, bv, rv);
+#else
+        icp_solve6_schur(Am, bv, rv);
+#endif
         icp_rodrigues(rv, R);
     } else {
         icp_cv_solve_svd6(Am, bv, rv);

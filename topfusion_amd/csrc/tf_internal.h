@@ -92,6 +92,21 @@ struct TfDevState {
 // ---------------------------------------------------------------------------------------
 // canonical device math
 // ---------------------------------------------------------------------------------------
+// RN(1 / z), the IEEE-correct reciprocal (= 1.0f / z under -fhip-fp32-correctly-rounded-divide-sqrt),
+// in three instructions where that is proven: v_rcp_f32 and one fma Newton step give the correctly
+// rounded value for EVERY float z in [2^-126, 2^126) on gfx950 (exhaustive check over all 2^31
+// positive floats, tools/micro/rcp_exact.hip, profiles/r05/rcp_exact.txt; mismatches only for
+// subnormal z and z >= 2^126).  Those, and z <= 0 or NaN, take the IEEE division (a branch no
+// lane normally takes).  Callers whose result for z <= 0 is discarded may pass it.
+__device__ __forceinline__ float tf_rcp_rn(float z)
+{
+    const float r0 = __builtin_amdgcn_rcpf(z);
+    const float e = __builtin_fmaf(-z, r0, 1.0f);
+    float r = __builtin_fmaf(e, r0, r0);
+    if (!(z >= 0x1p-126f && z < 0x1p126f)) r = 1.0f / z;
+    return r;
+}
+
 // replacement for __expf (imgproc.cu:40): 2^(x log2 e), exact range reduction + Horner
 __device__ __forceinline__ float tf_exp(float x)
 {
