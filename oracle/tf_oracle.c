@@ -1354,8 +1354,10 @@ static inline float update_voxel(tfo_voxel* v, const float pt_model[4], const fl
     float pc[4];
     m4v(M, pt_model, pc);
     if (pc[2] <= 0) return -1;
-    float ix = proj[0] * pc[0] / pc[2] + proj[2];
-    float iy = proj[1] * pc[1] / pc[2] + proj[3];
+    /* fx * x / z under --prec-div=false (CMakeLists.txt:1): canonical (fx x) * RN(1/z) */
+    const float rz = 1.0f / pc[2];
+    float ix = (proj[0] * pc[0]) * rz + proj[2];
+    float iy = (proj[1] * pc[1]) * rz + proj[3];
     if ((ix < 1) || (ix > (float)(W - 2)) || (iy < 1) || (iy > (float)(H - 2))) return -1;
     float depth_measure = depth[(int)(ix + 0.5f) + (int)(iy + 0.5f) * W];
     if (depth_measure <= 0.0f) return -1;
@@ -1382,8 +1384,9 @@ static inline void update_voxel_colour(uint32_t* clr, const float pt_model[4], c
 {
     float pc[4];
     m4v(Mr, pt_model, pc);
-    float ix = proj[0] * pc[0] / pc[2] + proj[2];
-    float iy = proj[1] * pc[1] / pc[2] + proj[3];
+    const float rz = 1.0f / pc[2];                 /* (as update_voxel) */
+    float ix = (proj[0] * pc[0]) * rz + proj[2];
+    float iy = (proj[1] * pc[1]) * rz + proj[3];
     if (isnan(ix) || isnan(iy)) return;
     if ((ix < 1) || (ix > (float)(W - 2)) || (iy < 1) || (iy > (float)(H - 2))) return;
     float m4[4];

@@ -402,7 +402,7 @@ def test_bench_timed_window(oracle_mod):
             compare_scene(g, o, tag)
     # the reference's frame-mixing resets: the oracle's own count over frames 0..799 of
     # this stream (profiles/r05/pose_algebra_gap_C2.json, canonical mode), pinned
-    assert n_reset == 78, n_reset
+    assert n_reset == 80, n_reset
     g.close()
     dev.free()
 

@@ -66,7 +66,7 @@ def test_opencv4_algebra_bench_timed_window(cv_oracle):
             tag = f"opencv4 bench frames {step * F}..{(step + 1) * F - 1}"
             _compare_frame_state(g, o, tag, grey=bool(oko[-1]))
             compare_scene(g, o, tag)
-    assert n_reset == 78, n_reset          # the oracle's count under OpenCV 4 (profiles/r05/pose_algebra_gap_C2.json)
+    assert n_reset == 79, n_reset          # the oracle's count under OpenCV 4 (profiles/r05/pose_algebra_gap_C2.json)
     g.close()
     dev.free()
 

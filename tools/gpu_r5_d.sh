@@ -11,4 +11,5 @@ TFUSION_HIP_LIB=$PWD/tools/_build/xcd0/libtfusion_hip.so timeout -k 10 700 pytho
   -m gpu -x -q -rs -k "icp_stage or sequence or bench_timed_window" --timeout 600 --timeout-method thread > $O/tests_xcd0.log 2>&1 \
   || { tail -30 $O/tests_xcd0.log; exit 1; }
 tail -n 1 $O/tests_xcd0.log
-bash tools/gpu_ab_lib.sh tree ldl pdiv both xcd0 2>&1 | tee $O/ab.txt
+bash tools/gpu_ab_lib.sh tree ldl pdiv both idiv xcd0 2>&1 | tee $O/ab.txt
+bash tools/gpu_ab_c3i.sh tree idiv 2>&1 | tee $O/ab_c3i.txt

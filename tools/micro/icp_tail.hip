@@ -7,7 +7,10 @@
 #include "../../topfusion_amd/csrc/tf_icp_tail.h"
 #include "../../topfusion_amd/csrc/tf_pose.h"
 
-__global__ void k_tail(const float* in, float* out, long long* cyc, int n, int which)
+// one instantiation per variant (its own register allocation: a runtime switch over all of them
+// spilled the large ones), one wave
+template <int which>
+__global__ void __launch_bounds__(64) k_tail(const float* in, float* out, long long* cyc, int n)
 {
     float Am[6][6], bv[6], aff[12];
     for (int i = 0; i < 6; ++i) { bv[i] = in[36 + i]; for (int j = 0; j < 6; ++j) Am[i][j] = in[i * 6 + j]; }
@@ -15,7 +18,7 @@ __global__ void k_tail(const float* in, float* out, long long* cyc, int n, int w
     double dx = in[0], dacc = 0;
     const long long t0 = clock64();
     for (int it = 0; it < n; ++it) {
-        if (which == 0) {                       // solve + Rodrigues + compose (the tail)
+        if constexpr (which == 0) {                       // solve + Rodrigues + compose (the tail)
             float rv[6], R[9], tinc[12];
             icp_solve_rodrigues<0>(Am, bv, rv, R);
             for (int j = 0; j < 3; ++j) {
@@ -24,37 +27,37 @@ __global__ void k_tail(const float* in, float* out, long long* cyc, int n, int w
             }
             tf_rigid_mul(tinc, aff, aff);
             bv[0] += aff[3] * 1e-30f;           // next repetition depends on this one
-        } else if (which == 1) {                // solve only (LDL^T, rounds 2-4)
+        } else if constexpr (which == 1) {                // solve only (LDL^T, rounds 2-4)
             float rv[6];
             icp_solve6_ldl(Am, bv, rv);
             bv[0] += rv[0] * 1e-30f;
-        } else if (which == 14) {               // solve only (2 x 2 block Schur, round 5)
+        } else if constexpr (which == 14) {               // solve only (2 x 2 block Schur, round 5)
             float rv[6];
             icp_solve6_schur(Am, bv, rv);
             bv[0] += rv[0] * 1e-30f;
-        } else if (which == 2) {                // Rodrigues only
+        } else if constexpr (which == 2) {                // Rodrigues only
             float rv[6] = { bv[0] * 1e-3f, bv[1] * 1e-3f, bv[2] * 1e-3f, 0, 0, 0 }, R[9];
             icp_rodrigues(rv, R);
             bv[0] += R[1] * 1e-30f;
-        } else if (which == 3) {                // 10 dependent f64 divides
+        } else if constexpr (which == 3) {                // 10 dependent f64 divides
             for (int k = 0; k < 10; ++k) dx = 1.0 / (dx + 1.0);
-        } else if (which == 4) {                // 10 dependent f64 sqrt
+        } else if constexpr (which == 4) {                // 10 dependent f64 sqrt
             for (int k = 0; k < 10; ++k) dx = sqrt(dx + 1.0);
-        } else if (which == 5) {                // 10 dependent f64 fma
+        } else if constexpr (which == 5) {                // 10 dependent f64 fma
             for (int k = 0; k < 10; ++k) dx = fma(dx, 0.999, 1e-3);
-        } else if (which == 6) {                // 10 dependent f32 fma
+        } else if constexpr (which == 6) {                // 10 dependent f32 fma
             float f = (float)dx;
             for (int k = 0; k < 10; ++k) f = fmaf(f, 0.999f, 1e-3f);
             dx = f;
-        } else if (which == 7) {                // 10 dependent f32 IEEE divides
+        } else if constexpr (which == 7) {                // 10 dependent f32 IEEE divides
             float f = (float)dx;
             for (int k = 0; k < 10; ++k) f = 1.0f / (f + 1.0f);
             dx = f;
-        } else if (which == 8) {                // the reference's cv::solve(DECOMP_SVD) (ALG 4)
+        } else if constexpr (which == 8) {                // the reference's cv::solve(DECOMP_SVD) (ALG 4)
             float rv[6];
             icp_cv_solve_svd6(Am, bv, rv);
             bv[0] += rv[0] * 1e-30f;
-        } else if (which == 9) {                // cv solve + Affine3f rotation + compose
+        } else if constexpr (which == 9) {                // cv solve + Affine3f rotation + compose
             float rv[6], R[9], tinc[12];
             icp_solve_rodrigues<4>(Am, bv, rv, R);
             for (int j = 0; j < 3; ++j) {
@@ -63,16 +66,16 @@ __global__ void k_tail(const float* in, float* out, long long* cyc, int n, int w
             }
             tf_rigid_mul(tinc, aff, aff);
             bv[0] += aff[3] * 1e-30f;
-        } else if (which == 10) {               // 10 dependent f64 adds
+        } else if constexpr (which == 10) {               // 10 dependent f64 adds
             for (int k = 0; k < 10; ++k) dx = dx + 1e-3;
-        } else if (which == 11) {               // 10 dependent f64 muls
+        } else if constexpr (which == 11) {               // 10 dependent f64 muls
             for (int k = 0; k < 10; ++k) dx = dx * 0.999;
-        } else if (which == 12) {               // 10 dependent (readlane -> f32 add) round trips
+        } else if constexpr (which == 12) {               // 10 dependent (readlane -> f32 add) round trips
             float f = (float)dx + (float)threadIdx.x;
             for (int k = 0; k < 10; ++k)
                 f = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), k)) + 1.0f + (float)threadIdx.x;
             dx = f;
-        } else if (which == 13) {               // 10 dependent f32 adds
+        } else if constexpr (which == 13) {               // 10 dependent f32 adds
             float f = (float)dx;
             for (int k = 0; k < 10; ++k) f = f + 1e-3f;
             dx = f;
@@ -82,6 +85,14 @@ __global__ void k_tail(const float* in, float* out, long long* cyc, int n, int w
     dacc += dx;
     if (threadIdx.x == 0) { cyc[which] = t1 - t0; out[which] = aff[3] + bv[0] + (float)dacc; }
 }
+
+template <int W>
+static void launch_t(int w, const float* a, float* o, long long* c, int n)
+{
+    if (w == W) hipLaunchKernelGGL(k_tail<W>, dim3(1), dim3(64), 0, 0, a, o, c, n);
+    if constexpr (W > 0) launch_t<W - 1>(w, a, o, c, n);
+}
+static void launch(int w, const float* a, float* o, long long* c, int n) { launch_t<14>(w, a, o, c, n); }
 
 int main()
 {
@@ -97,8 +108,8 @@ int main()
                             "10x f64 fma", "10x f32 fma", "10x f32 div", "cv solve (SVD)", "cv solve+rot+compose",
                             "10x f64 add", "10x f64 mul", "10x readlane+add", "10x f32 add", "solve (block Schur)" };
     for (int w = 0; w < 15; ++w) {
-        hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, 0, dA, dO, dC, 10, w);   // warm
-        hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, 0, dA, dO, dC, N, w);
+        launch(w, dA, dO, dC, 10);   // warm
+        launch(w, dA, dO, dC, N);
         long long c = 0;
         hipMemcpy(&c, dC + w, sizeof(c), hipMemcpyDeviceToHost);
         printf("%-26s %8.1f cycles per repetition (s_memtime)\n", names[w], (double)c / N);

@@ -38,6 +38,15 @@ extern "C" int tf_debug_icp_ts(unsigned long long* out)
 #define IPT_STRIDE (2 * ICP_NWG + 8)
 __device__ unsigned long long g_icp_tl[64 * IPT_STRIDE];
 #define IPT_REC(it, slot) IPT_REC_T(it, slot, 0)
+// a stamp after a value: the value is an operand of a volatile asm placed before the stamp, so
+// the compiler cannot sink the work it depends on past the stamp (VALU issue is in order; what is
+// left in flight is a pipeline depth); workgroup 0 alone records (the slots are shared)
+#define IPT_REC_DEP(it, slot, val_) do { \
+    const float d_ = (float)(val_); \
+    asm volatile("; ipt dependency %0" :: "v"(d_)); \
+    __builtin_amdgcn_sched_barrier(0); \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (it) < 64) g_icp_tl[(it) * IPT_STRIDE + (slot)] = IPT_NOW(); \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
 // the stamp is fenced against the scheduler (no instruction moves across it) and issued after the
 // VALU work before it has been issued; the data it measures lives in registers, so the segment
 // between two stamps is that segment's issue time
@@ -64,6 +73,7 @@ extern "C" int tf_debug_icp_clock(unsigned long long* out)
 #define IPT_ADD(k, v) do { } while (0)
 #define IPT_REC(it, slot) do { } while (0)
 #define IPT_REC_T(it, slot, t) do { } while (0)
+#define IPT_REC_DEP(it, slot, val_) do { } while (0)
 #define IPT_CLK(it) do { } while (0)
 #endif
 
@@ -805,7 +815,7 @@ k_icp_frame(IcpFrameArgs a)
 #pragma unroll
                     for (int q = 0; q < 27; ++q)
                         sm[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tot), q));
-                    IPT_REC(done, 2 * ICP_NWG + 6);
+                    IPT_REC_DEP(done, 2 * ICP_NWG + 6, sm[26] + sm[0]);
                     ip_unpack(sm, Am, bv);
                     IPT_REC(done, 2 * ICP_NWG + 2);
                     if (wave == IP_DETW) {                             // det after the barrier
@@ -813,8 +823,15 @@ k_icp_frame(IcpFrameArgs a)
                         for (int q = 0; q < 27; ++q) det_sm[q] = sm[q];
                     } else {                                           // solve -> Rodrigues -> compose
                         float rv[6], R[9], tinc[12];
+#ifdef TF_ICP_TIMING
+                        if constexpr (ALG == 0) {                       // the two halves stamped apart
+                            icp_solve6_schur(Am, bv, rv);
+                            IPT_REC_DEP(done, 2 * ICP_NWG + 3, rv[0] + rv[5]);
+                            icp_rodrigues(rv, R);
+                        } else
+#endif
                         icp_solve_rodrigues<ALG>(Am, bv, rv, R);        // projective_icp.cpp:206-209
-                        IPT_REC(done, 2 * ICP_NWG + 7);
+                        IPT_REC_DEP(done, 2 * ICP_NWG + 7, R[0] + R[8]);
 #pragma unroll
                         for (int j = 0; j < 3; ++j) {
                             tinc[j * 4 + 0] = R[j * 3 + 0]; tinc[j * 4 + 1] = R[j * 3 + 1];
@@ -825,7 +842,7 @@ k_icp_frame(IcpFrameArgs a)
                         for (int i = 0; i < 12; ++i) A[i] = aff[i];
                         tf_rigid_mul(tinc, A, A);
                         if (lane < 12) aff_s[lane] = A[lane];
-                        IPT_REC(done, 2 * ICP_NWG + 4);
+                        IPT_REC_DEP(done, 2 * ICP_NWG + 4, A[0] + A[11]);
                         last_sums = tot;
                     }
                 }

@@ -778,6 +778,9 @@ hipError_t tfk_alloc(tf_ctx* c, int snapshot, TfAhead bil, size_t pitch, int onl
 // computeUpdatedVoxelDepthInfo (SceneReconstructionEngine.hpp:23-71).
 // 128 lanes per 8^3 block, 4 consecutive voxels (16 B) per lane; blocks grid-strided.
 // ---------------------------------------------------------------------------------------
+#ifndef TF_INTEG_DIV
+#define TF_INTEG_DIV 0
+#endif
 struct IntegArgs {
     const float* dists;
     int W, H;
@@ -814,8 +817,17 @@ __device__ __forceinline__ bool integ_project(float px, float py, float pz, cons
     tf_m4v3(M, px, py, pz, 1.0f, pc);
     *z = pc[2];
     if (pc[2] <= 0) return false;
+    // projParams_d.x * pt_camera.x / pt_camera.z (SceneReconstructionEngine.hpp:35-36), built with
+    // --prec-div=false (CMakeLists.txt:1): the quotient as a product with the reciprocal -- canonical
+    // (fx x) RN(1/z), one reciprocal per voxel for both coordinates (round 5; it was (fx x) / z)
+#if TF_INTEG_DIV                                   // A/B only: the IEEE quotients (not the oracle's)
     float ix = a.fx * pc[0] / pc[2] + a.cx;
     float iy = a.fy * pc[1] / pc[2] + a.cy;
+#else
+    const float rz = tf_rcp_rn(pc[2]);
+    float ix = (a.fx * pc[0]) * rz + a.cx;
+    float iy = (a.fy * pc[1]) * rz + a.cy;
+#endif
     if ((ix < 1) || (ix > (float)(a.W - 2)) || (iy < 1) || (iy > (float)(a.H - 2))) return false;
     *idx = (int)(ix + 0.5f) + (int)(iy + 0.5f) * a.W;
     return true;
@@ -876,8 +888,9 @@ __device__ __forceinline__ void integ_colour_fetch(float px, float py, float pz,
 {
     float pc[3];
     tf_m4v3(Mr, px, py, pz, 1.0f, pc);
-    const float ix = a.rfx * pc[0] / pc[2] + a.rcx;
-    const float iy = a.rfy * pc[1] / pc[2] + a.rcy;
+    const float rz = tf_rcp_rn(pc[2]);                 // (SceneReconstructionEngine.hpp:132-133, as integ_project)
+    const float ix = (a.rfx * pc[0]) * rz + a.rcx;
+    const float iy = (a.rfy * pc[1]) * rz + a.rcy;
     t.ok = ix >= 1 && ix <= (float)(a.W - 2) && iy >= 1 && iy <= (float)(a.H - 2);
     const int x0 = t.ok ? (int)floorf(ix) : 1, y0 = t.ok ? (int)floorf(iy) : 1;
     t.dx = ix - (float)x0; t.dy = iy - (float)y0;
