@@ -328,6 +328,23 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 #define IP_XCD_STORE 1
 #endif
 #define IP_XCC_AT (IP_PART + 2 * IP_NPART * ICP_T_STRIDE)   // the leaders' XCD ids (TF_ICP_TAG_WORDS)
+// Hop 2's readers are all 256 workgroups, polling 8 x 27 granules.  Each leader publishes its
+// partials IP_PCOPY = 8 times, 4 KiB apart, and the workgroups of residue class x (one XCD
+// under round-robin dispatch) poll copy x: 32 pollers per line instead of 256 (ICP -1.5 us per
+// launch, A/B profiles/r05/ab_icp_hop2_copies.txt).
+#ifndef IP_OK_BITWISE
+#define IP_OK_BITWISE 1                          // A/B: 0 = short-circuit correspondence flags
+#endif
+#ifndef IP_PCOPY
+#define IP_PCOPY 8                               // A/B: 1 = one copy polled by every workgroup
+#endif
+#define IP_PCOPY_AT (IP_XCC_AT + 16)
+#define IP_PCOPY_STRIDE 512
+static_assert(IP_PCOPY_AT + 8 * IP_PCOPY_STRIDE <= TF_ICP_TAG_WORDS, "TF_ICP_TAG_WORDS");
+__device__ __forceinline__ int ip_part_at(int copy)
+{
+    return IP_PCOPY == 1 ? IP_PART : IP_PCOPY_AT + copy * IP_PCOPY_STRIDE;
+}
 
 struct IcpFrameArgs {
     IcpLevel lv[TF_LEVELS];             // in processing order (coarse -> fine)
@@ -463,15 +480,33 @@ __device__ __forceinline__ void ip_project2(const IcpLevel& L, const float* aff,
 #if TF_PROJ_DIV                                   // A/B only: the IEEE division sequence for RN(1 / z)
     const ip_f2 rz = { 1.0f / sz.x, 1.0f / sz.y };
 #else
-    const ip_f2 rz = { tf_rcp_rn(sz.x), tf_rcp_rn(sz.y) };
+    // (one wave-uniform branch for the pair's rare IEEE fallback, tf_internal.h)
+    ip_f2 rz = { tf_rcp_fast(sz.x), tf_rcp_fast(sz.y) };
+    const bool slow0 = tf_rcp_slow(sz.x), slow1 = tf_rcp_slow(sz.y);
+#if TF_RCP_BRANCH
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(slow0 | slow1) != 0, 0)) {
+        if (slow0) rz.x = 1.0f / sz.x;
+        if (slow1) rz.y = 1.0f / sz.y;
+    }
+#else
+    if (slow0) rz.x = 1.0f / sz.x;
+    if (slow1) rz.y = 1.0f / sz.y;
+#endif
 #endif
     const ip_f2 qx = sx * rz, qy = sy * rz;
     const ip_f2 coox = __builtin_elementwise_fma(ip_bc(L.fx), qx, ip_bc(L.cx));
     const ip_f2 cooy = __builtin_elementwise_fma(ip_bc(L.fy), qy, ip_bc(L.cy));
+#if IP_OK_BITWISE            // (bitwise, not short-circuit: no exec-mask branches)
+    ok0 = (xy0 >= 0) & !isnan(vx.x) &
+          !((sz.x <= 0) | (coox.x < 0) | (cooy.x < 0) | (coox.x >= (float)L.W) | (cooy.x >= (float)L.H));
+    ok1 = (xy1 >= 0) & !isnan(vx.y) &
+          !((sz.y <= 0) | (coox.y < 0) | (cooy.y < 0) | (coox.y >= (float)L.W) | (cooy.y >= (float)L.H));
+#else
     ok0 = xy0 >= 0 && !isnan(vx.x) &&
           !(sz.x <= 0 || coox.x < 0 || cooy.x < 0 || coox.x >= (float)L.W || cooy.x >= (float)L.H);
     ok1 = xy1 >= 0 && !isnan(vx.y) &&
           !(sz.y <= 0 || coox.y < 0 || cooy.y < 0 || coox.y >= (float)L.W || cooy.y >= (float)L.H);
+#endif
     idx0 = ok0 ? (int)floorf(cooy.x) * L.W + (int)floorf(coox.x) : 0;
     idx1 = ok1 ? (int)floorf(cooy.y) * L.W + (int)floorf(coox.y) : 0;
 }
@@ -589,6 +624,9 @@ k_icp_frame(IcpFrameArgs a)
     __shared__ float tv[27][IP_NPART + 1];      // the 8 residue-class partials per sum
     __shared__ float aff_s[12];
     __shared__ int det_ok_s;
+    // the det check's sums and the affine it may restore live in LDS, not in registers across the
+    // iteration: the serial tail runs in the registers they would hold
+    __shared__ float det_sm_s[27], aff_prev_s[12];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, wg = blockIdx.x;
     TfDevState* st = a.st;
     unsigned long long* tag = a.tag;
@@ -641,7 +679,7 @@ k_icp_frame(IcpFrameArgs a)
     for (int i = 0; i < 12; ++i) aff[i] = (i % 5 == 0) ? 1.0f : 0.0f;     // affine = Identity
     int status = 1, done = 0;
     float last_sums = 0.f;
-    float aff_prev[12], det_sm[27];
+
     bool det_pending = false;
 
 #pragma unroll 1
@@ -679,7 +717,9 @@ k_icp_frame(IcpFrameArgs a)
             IPT_REC(done, wg);
             IPT_CLK(done);
             if (det_pending && wave == IP_DETW) {
-                float Am[6][6], bv[6];
+                float Am[6][6], bv[6], det_sm[27];
+#pragma unroll
+                for (int q = 0; q < 27; ++q) det_sm[q] = det_sm_s[q];
                 ip_unpack(det_sm, Am, bv);
                 const double det = icp_det6<ALG>(Am);
                 if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
@@ -726,7 +766,7 @@ k_icp_frame(IcpFrameArgs a)
                 if (!det_ok_s) {
                     status = 0;
 #pragma unroll
-                    for (int i = 0; i < 12; ++i) aff[i] = aff_prev[i];
+                    for (int i = 0; i < 12; ++i) aff[i] = aff_prev_s[i];
                     break;
                 }
             }
@@ -782,14 +822,17 @@ k_icp_frame(IcpFrameArgs a)
                     if (e < 32 * 27) tl[q][kk] = __uint_as_float((unsigned)v[k]);
                 }
                 const int lead_timeout = __syncthreads_or(timeout);
-                if (!lead_timeout && tid < 27)          // a missing column: publish nothing, WG0 times out
-                    ip_store(&tag[IP_PART + (gen & 1) * IP_NPART * ICP_T_STRIDE + wg * ICP_T_STRIDE + tid],
-                             ip_pack(gen, ip_residue_tree(tl[tid])));
+                if (!lead_timeout && tid < 27) {        // a missing column: publish nothing, WG0 times out
+                    const unsigned long long pv = ip_pack(gen, ip_residue_tree(tl[tid]));
+#pragma unroll
+                    for (int c = 0; c < IP_PCOPY; ++c)
+                        ip_store(&tag[ip_part_at(c) + (gen & 1) * IP_NPART * ICP_T_STRIDE + wg * ICP_T_STRIDE + tid], pv);
+                }
             }
             {
                 // ---- gather the 8 x 27 partials, last three tree steps, det / solve / compose
                 // (every workgroup, redundantly and bit-identically -- no broadcast hop)
-                const unsigned long long* parts = &tag[IP_PART + (gen & 1) * IP_NPART * ICP_T_STRIDE];
+                const unsigned long long* parts = &tag[ip_part_at(wg & (IP_PCOPY - 1)) + (gen & 1) * IP_NPART * ICP_T_STRIDE];
                 bool timeout = false;
                 if (tid < IP_NPART * 27) {
                     const int x = tid / 27, q = tid - x * 27;
@@ -819,8 +862,7 @@ k_icp_frame(IcpFrameArgs a)
                     ip_unpack(sm, Am, bv);
                     IPT_REC(done, 2 * ICP_NWG + 2);
                     if (wave == IP_DETW) {                             // det after the barrier
-#pragma unroll
-                        for (int q = 0; q < 27; ++q) det_sm[q] = sm[q];
+                        if (lane < 27) det_sm_s[lane] = tot;
                     } else {                                           // solve -> Rodrigues -> compose
                         float rv[6], R[9], tinc[12];
 #ifdef TF_ICP_TIMING
@@ -850,8 +892,10 @@ k_icp_frame(IcpFrameArgs a)
                 IPT_REC(done, 2 * ICP_NWG + 1);
                 status = any_timeout ? 2 : 1;
                 det_pending = !any_timeout;
+                if (wave == 0 && lane == 0) {
 #pragma unroll
-                for (int i = 0; i < 12; ++i) aff_prev[i] = aff[i];
+                    for (int i = 0; i < 12; ++i) aff_prev_s[i] = aff[i];
+                }
                 if (status == 1) {
 #pragma unroll
                     for (int i = 0; i < 12; ++i) aff[i] = aff_s[i];
@@ -864,7 +908,9 @@ k_icp_frame(IcpFrameArgs a)
     }
     if (det_pending) {                                            // the last iteration's det check
         if (wave == IP_DETW) {
-            float Am[6][6], bv[6];
+            float Am[6][6], bv[6], det_sm[27];
+#pragma unroll
+            for (int q = 0; q < 27; ++q) det_sm[q] = det_sm_s[q];
             ip_unpack(det_sm, Am, bv);
             const double det = icp_det6<ALG>(Am);
             if (lane == 0) det_ok_s = !(fabs(det) < 1e-15 || isnan(det));
@@ -873,7 +919,7 @@ k_icp_frame(IcpFrameArgs a)
         if (!det_ok_s) {
             status = 0;
 #pragma unroll
-            for (int i = 0; i < 12; ++i) aff[i] = aff_prev[i];
+            for (int i = 0; i < 12; ++i) aff[i] = aff_prev_s[i];
         }
     }
     // ---- workgroup 0 records the frame's ICP result

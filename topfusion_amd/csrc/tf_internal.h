@@ -22,7 +22,7 @@
 #define TF_NUM_STAGES 9     // tf_stage_id in include/tfusion_hip.h
 #define TF_PROF_RING 32     // frames enqueued between host syncs (and timing-event ring slots)
 #define TF_ST_BYTES (sizeof(TfDevState) + 2 * sizeof(int) * TF_PROF_RING)   // c->st + frame_ok / frame_mode rings
-#define TF_ICP_TAG_WORDS (2 * 256 * 28 + 16 + 2 * 8 * 28 + 16)   // persistent ICP tagged granules (tf_icp.hip)
+#define TF_ICP_TAG_WORDS (2 * 256 * 28 + 16 + 2 * 8 * 28 + 16 + 8 * 512)   // persistent ICP tagged granules (tf_icp.hip)
 
 // HashEntry, VoxelBlockHash.hpp:32-44 (16 B; one dwordx4 probe)
 struct __attribute__((aligned(16))) TfHashEntry {
@@ -96,14 +96,36 @@ struct TfDevState {
 // in three instructions where that is proven: v_rcp_f32 and one fma Newton step give the correctly
 // rounded value for EVERY float z in [2^-126, 2^126) on gfx950 (exhaustive check over all 2^31
 // positive floats, tools/micro/rcp_exact.hip, profiles/r05/rcp_exact.txt; mismatches only for
-// subnormal z and z >= 2^126).  Those, and z <= 0 or NaN, take the IEEE division (a branch no
-// lane normally takes).  Callers whose result for z <= 0 is discarded may pass it.
-__device__ __forceinline__ float tf_rcp_rn(float z)
+// subnormal z and z >= 2^126).  v_rcp_f32 works on the magnitude and both fma round to nearest,
+// so the same holds for z in (-2^126, -2^-126]; NaN gives NaN either way.  The rest (zero,
+// subnormal, |z| >= 2^126) takes the IEEE division behind a wave-uniform branch that no wave
+// takes on real depth data -- as a select, the division sequence cost ~12 instructions per
+// reciprocal on the ICP rows' critical SIMD.
+#ifndef TF_RCP_BRANCH
+#define TF_RCP_BRANCH 1          // A/B only: 0 = the division computed for every lane and selected
+#endif
+__device__ __forceinline__ float tf_rcp_fast(float z)
 {
     const float r0 = __builtin_amdgcn_rcpf(z);
     const float e = __builtin_fmaf(-z, r0, 1.0f);
-    float r = __builtin_fmaf(e, r0, r0);
-    if (!(z >= 0x1p-126f && z < 0x1p126f)) r = 1.0f / z;
+    return __builtin_fmaf(e, r0, r0);
+}
+__device__ __forceinline__ bool tf_rcp_slow(float z)
+{
+    const float a = __builtin_fabsf(z);
+    return a < 0x1p-126f || a >= 0x1p126f;
+}
+__device__ __forceinline__ float tf_rcp_rn(float z)
+{
+    float r = tf_rcp_fast(z);
+    const bool slow = tf_rcp_slow(z);
+#if TF_RCP_BRANCH
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(slow) != 0, 0)) {
+        if (slow) r = 1.0f / z;
+    }
+#else
+    if (slow) r = 1.0f / z;
+#endif
     return r;
 }
 

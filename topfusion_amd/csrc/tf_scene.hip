@@ -958,6 +958,23 @@ __device__ __forceinline__ void integ_proj_pair(const TfHashEntry& e, const TfHa
     }
 }
 
+// TF_C3X (diagnostic builds only, tools/build_variant.sh; never the product, results wrong):
+// bit 0 -- every depth sample reads pixel 0 (no depth-image traffic); bit 1 -- no voxel loads
+// (each lane starts from an empty voxel).  C3I's reads split by source with PMC FETCH_SIZE.
+#ifndef TF_C3X
+#define TF_C3X 0
+#endif
+__device__ __forceinline__ float integ_sample(const float* dists, int di)
+{
+    return dists[(TF_C3X & 1) ? 0 : di];
+}
+__device__ __forceinline__ void integ_vload(uint4* p, uint4* p2, bool stream, uint4& v, uint4& v2)
+{
+    if (TF_C3X & 2) { v = make_uint4(0, 0, 0, 0); v2 = v; return; }
+    if (stream) { v = nt_load16(p); v2 = nt_load16(p2); }
+    else { v = *p; v2 = *p2; }
+}
+
 // update half: the eight voxels against their depth samples dm, stores of the changed lanes,
 // then (RGB) the colour of the voxels inside the colour gate
 template <bool RGB>
@@ -1154,11 +1171,10 @@ __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__
         uint4* p2 = (uint4*)(vba + (size_t)(e2.ptr < 0 ? 0 : e2.ptr) * TF_BLK3 + lin);
         {
             int di[8];
-            if (stream) { v = nt_load16(p); v2 = nt_load16(p2); }
-            else { v = *p; v2 = *p2; }
+            integ_vload(p, p2, stream, v, v2);
             integ_proj_pair(e, e2, vx, vy, vz, M, a, z, di, ok);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) dm[k] = a.dists[di[k]];
+            for (int k = 0; k < 8; ++k) dm[k] = integ_sample(a.dists, di[k]);
         }
         for (; i < n; i += step) {
             // pass k+1: project, issue its voxel loads and depth samples
@@ -1172,11 +1188,10 @@ __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__
             uint4* pn2 = (uint4*)(vba + (size_t)(ne2.ptr < 0 ? 0 : ne2.ptr) * TF_BLK3 + lin);
             {
                 int di[8];
-                if (stream) { vn = nt_load16(pn); vn2 = nt_load16(pn2); }
-                else { vn = *pn; vn2 = *pn2; }
+                integ_vload(pn, pn2, stream, vn, vn2);
                 integ_proj_pair(ne, ne2, vx, vy, vz, M, a, zn, di, okn);
 #pragma unroll
-                for (int k = 0; k < 8; ++k) dmn[k] = a.dists[di[k]];
+                for (int k = 0; k < 8; ++k) dmn[k] = integ_sample(a.dists, di[k]);
             }
             // pass k+2's entries, pass k+3's ids
             const TfHashEntry nne = hash[nid1], nne2 = hash[nid2];
