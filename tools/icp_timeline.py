@@ -38,6 +38,18 @@ for i in range(its):
     if nxt is not None:
         line += f" next-start {nxt.min():5.2f}/{np.median(nxt):5.2f}/{nxt.max():5.2f}"
     print(line)
+# the tail's halves on the shader clock, each run twice back to back (the second run's code is
+# in the instruction cache): workgroup 0, per iteration
+try:
+    tb = (ctypes.c_longlong * 256)()
+    _lib.load().tf_debug_icp_tail_cycles(tb)
+    tc = np.frombuffer(tb, dtype=np.int64).reshape(64, 4)[:its]
+    print("tail cycles (shader clock) per iteration: solve, solve again, rodrigues, rodrigues again")
+    for i in range(its):
+        print(f"  it {i:2d}: {tc[i, 0]:6d} {tc[i, 1]:6d} {tc[i, 2]:6d} {tc[i, 3]:6d}")
+    print(f"  median: {int(np.median(tc[:, 0]))} {int(np.median(tc[:, 1]))} {int(np.median(tc[:, 2]))} {int(np.median(tc[:, 3]))}")
+except Exception as ex:
+    print("tail cycles:", ex)
 # the shader clock workgroup 0 ran at (s_memtime against the 100 MHz s_memrealtime)
 try:
     cb = (ctypes.c_ulonglong * 128)()

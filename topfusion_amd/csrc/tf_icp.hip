@@ -62,6 +62,16 @@ extern "C" int tf_debug_icp_timeline(unsigned long long* out)
 __device__ unsigned long long g_icp_clk[64 * 2];
 #define IPT_CLK(it) do { if (blockIdx.x == 0 && threadIdx.x == 0 && (it) < 64) { \
     g_icp_clk[2 * (it)] = __builtin_amdgcn_s_memtime(); g_icp_clk[2 * (it) + 1] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+// the tail's halves on the shader clock, each run twice in a row (solve, solve again, Rodrigues,
+// Rodrigues again) per iteration of workgroup 0
+__device__ long long g_icp_tail_cyc[64 * 4];
+#define IPT_CYC(val_) ({ const float d_ = (float)(val_); asm volatile("; ipt dependency %0" :: "v"(d_)); \
+    __builtin_amdgcn_sched_barrier(0); const long long t_ = (long long)__builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0); t_; })
+extern "C" int tf_debug_icp_tail_cycles(long long* out)
+{
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_tail_cyc), sizeof(g_icp_tail_cyc), 0, hipMemcpyDeviceToHost);
+}
 extern "C" int tf_debug_icp_clock(unsigned long long* out)
 {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_clk), sizeof(g_icp_clk), 0, hipMemcpyDeviceToHost);
@@ -867,9 +877,30 @@ k_icp_frame(IcpFrameArgs a)
                         float rv[6], R[9], tinc[12];
 #ifdef TF_ICP_TIMING
                         if constexpr (ALG == 0) {                       // the two halves stamped apart
+                            // each half run twice back to back on the shader clock: the second
+                            // run finds its code in the instruction cache (g_icp_tail_cyc)
+                            const long long c0 = IPT_CYC(0.f);
                             icp_solve6_schur(Am, bv, rv);
-                            IPT_REC_DEP(done, 2 * ICP_NWG + 3, rv[0] + rv[5]);
+                            const long long c1 = IPT_CYC(rv[0] + rv[5]);
+                            float bv2[6], rv2[6], R2[9];
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) bv2[i] = bv[i] + rv[i] * 0.0f;
+                            icp_solve6_schur(Am, bv2, rv2);
+                            const long long c2 = IPT_CYC(rv2[0] + rv2[5]);
+                            IPT_REC_DEP(done, 2 * ICP_NWG + 3, rv[0] + rv[5] + rv2[1] * 0.0f);
+                            const long long c3 = IPT_CYC(0.f);
                             icp_rodrigues(rv, R);
+                            const long long c4 = IPT_CYC(R[0] + R[8]);
+                            float rvb[6];
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) rvb[i] = rv[i] + R[i] * 0.0f;
+                            icp_rodrigues(rvb, R2);
+                            const long long c5 = IPT_CYC(R2[0] + R2[8]);
+                            if (blockIdx.x == 0 && lane == 0 && done < 64) {
+                                g_icp_tail_cyc[4 * done + 0] = c1 - c0; g_icp_tail_cyc[4 * done + 1] = c2 - c1;
+                                g_icp_tail_cyc[4 * done + 2] = c4 - c3; g_icp_tail_cyc[4 * done + 3] = c5 - c4;
+                            }
+                            R[0] = R[0] + R2[0] * 0.0f;
                         } else
 #endif
                         icp_solve_rodrigues<ALG>(Am, bv, rv, R);        // projective_icp.cpp:206-209
