@@ -960,12 +960,17 @@ __device__ __forceinline__ void integ_proj_pair(const TfHashEntry& e, const TfHa
 
 // TF_C3X (diagnostic builds only, tools/build_variant.sh; never the product, results wrong):
 // bit 0 -- every depth sample reads pixel 0 (no depth-image traffic); bit 1 -- no voxel loads
-// (each lane starts from an empty voxel).  C3I's reads split by source with PMC FETCH_SIZE.
+// (each lane starts from an empty voxel); bits 2 / 3 -- samples rounded down to 16 B / 128 B.  C3I's reads split by source with PMC FETCH_SIZE.
 #ifndef TF_C3X
 #define TF_C3X 0
 #endif
+#ifndef TF_INTEG_LANEMAP
+#define TF_INTEG_LANEMAP 1
+#endif
 __device__ __forceinline__ float integ_sample(const float* dists, int di)
 {
+    if (TF_C3X & 4) di &= ~3;           // (diagnostic: 16-byte aligned: lanes of a segment share an address)
+    if (TF_C3X & 8) di &= ~31;          // (diagnostic: 128-byte line starts: the same lines, fewer addresses)
     return dists[(TF_C3X & 1) ? 0 : di];
 }
 __device__ __forceinline__ void integ_vload(uint4* p, uint4* p2, bool stream, uint4& v, uint4& v2)
@@ -1139,8 +1144,17 @@ __device__ __forceinline__ void integ_body(IntegArgs a, TfDevState* __restrict__
             }
     }
     const int half = threadIdx.x >> 7, t = threadIdx.x & 127;
+    // a lane's four voxels: x in {0..3} or {4..7} of one (y, z) row of the block.  Each wave takes
+    // four y rows of all eight z layers (TF_INTEG_LANEMAP 1) -- not eight y rows of four layers: a
+    // depth-sample instruction then spans half the image rows, and the samples' L1 -> L2 line
+    // fetches, not the voxel stream, are what the pass waits on (profiles/r05/c3i_read_attribution.json)
+#if TF_INTEG_LANEMAP
+    const int vx = (t & 1) * 4, vy = ((t >> 1) & 3) | ((t >> 6) << 2), vz = (t >> 3) & 7;
+    const int lin = vx + 8 * vy + 64 * vz;
+#else
     const int lin = t * 4;                       // first voxel of this lane: x in {0,4}
     const int vx = lin & 7, vy = (lin >> 3) & 7, vz = lin >> 6;
+#endif
     // two blocks per half-workgroup per pass, their id / entry / voxel loads issued before
     // either is computed: twice the bytes in flight per wave (at C3 scale, 2^21 blocks, the
     // pass is a stream over 8.6 GB)
