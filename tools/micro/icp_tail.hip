@@ -86,6 +86,99 @@ __global__ void __launch_bounds__(64) k_tail(const float* in, float* out, long l
     if (threadIdx.x == 0) { cyc[which] = t1 - t0; out[which] = aff[3] + bv[0] + (float)dacc; }
 }
 
+// icp_tail_rows (row layout) against the scalar tail on random ICP-like systems: sums of 7-vector
+// outer products (the rows), small random increments, a random affine; every output bit compared.
+// Also each form's latency with the whole system changing every repetition (nothing hoisted).
+__device__ __forceinline__ float rnd(unsigned& st)
+{
+    st = st * 1664525u + 1013904223u;
+    return (float)(st >> 8) * (1.0f / 16777216.0f) - 0.5f;
+}
+__device__ void make_system(unsigned seed, float (&sm)[27], float (&aff)[12])
+{
+    unsigned st = seed * 2654435761u + 12345u;
+    for (int q = 0; q < 27; ++q) sm[q] = 0.f;
+    const int nrow = 8 + (seed % 57);
+    for (int n = 0; n < nrow; ++n) {
+        float r[7];
+        for (int k = 0; k < 6; ++k) r[k] = rnd(st) * (k < 3 ? 2.0f : 1.0f);
+        r[6] = rnd(st) * 1e-2f;
+        int q = 0;
+        for (int a = 0; a < 6; ++a)
+            for (int b = a; b < 7; ++b, ++q) sm[q] += r[a] * r[b];
+    }
+    float rv[3] = { rnd(st) * 0.2f, rnd(st) * 0.2f, rnd(st) * 0.2f }, R[9];
+    float rv6[6] = { rv[0], rv[1], rv[2], 0, 0, 0 };
+    icp_rodrigues(rv6, R);
+    for (int j = 0; j < 3; ++j) {
+        for (int c = 0; c < 3; ++c) aff[4 * j + c] = R[3 * j + c];
+        aff[4 * j + 3] = rnd(st);
+    }
+}
+__device__ void tail_scalar(const float (&sm)[27], const float (&aff)[12], float (&out)[12], float (&rv)[6])
+{
+    float Am[6][6], bv[6];
+    int shift = 0;
+    for (int i = 0; i < 6; ++i)
+        for (int j = i; j < 7; ++j) {
+            const float v = sm[shift++];
+            if (j == 6) bv[i] = v; else { Am[j][i] = v; Am[i][j] = v; }
+        }
+    float R[9], tinc[12];
+    icp_solve6_schur(Am, bv, rv);
+    icp_rodrigues(rv, R);
+    for (int j = 0; j < 3; ++j) {
+        tinc[4 * j + 0] = R[3 * j + 0]; tinc[4 * j + 1] = R[3 * j + 1];
+        tinc[4 * j + 2] = R[3 * j + 2]; tinc[4 * j + 3] = rv[3 + j];
+    }
+    tf_rigid_mul(tinc, aff, out);
+}
+__global__ void __launch_bounds__(64) k_rows_check(int nsys, int* bad, int* first_bad)
+{
+    __shared__ double xs[9];
+    const int lane = threadIdx.x;
+    for (int sys = 0; sys < nsys; ++sys) {
+        float sm[27], aff[12], o_s[12], rv_s[6], orow[4], rv_r[6];
+        make_system((unsigned)sys, sm, aff);
+        tail_scalar(sm, aff, o_s, rv_s);
+        icp_tail_rows(sm, aff, lane, xs, orow, rv_r);
+        bool ok = true;
+        for (int k = 0; k < 6; ++k) ok = ok && __float_as_uint(rv_s[k]) == __float_as_uint(rv_r[k]);
+        if (lane < 3)
+            for (int c = 0; c < 4; ++c) ok = ok && __float_as_uint(orow[c]) == __float_as_uint(o_s[4 * lane + c]);
+        if (__builtin_amdgcn_ballot_w64(!ok && lane < 3) != 0 && lane == 0) {
+            if (*bad == 0) *first_bad = sys;
+            *bad += 1;
+        }
+    }
+}
+template <int ROWS>
+__global__ void __launch_bounds__(64) k_rows_time(int n, long long* cyc, float* out)
+{
+    __shared__ double xs[9];
+    const int lane = threadIdx.x;
+    float sm[27], aff[12];
+    make_system(7u, sm, aff);
+    float acc = 0.f;
+    const long long t0 = clock64();
+    for (int it = 0; it < n; ++it) {
+        float rv[6];
+        if constexpr (ROWS) {
+            float orow[4];
+            icp_tail_rows(sm, aff, lane, xs, orow, rv);
+            acc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, orow[3]), 0));
+        } else {
+            float o[12];
+            tail_scalar(sm, aff, o, rv);
+            acc = o[3];
+        }
+        sm[0] += acc * 1e-30f;          // the next repetition's whole system depends on this one
+        sm[22] += rv[4] * 1e-30f;
+    }
+    const long long t1 = clock64();
+    if (lane == 0) { cyc[ROWS] = t1 - t0; out[ROWS] = acc; }
+}
+
 template <int W>
 static void launch_t(int w, const float* a, float* o, long long* c, int n)
 {
@@ -107,6 +200,23 @@ int main()
     const char* names[] = { "solve+rodrigues+compose (canonical)", "solve (LDL^T, r2-4)", "rodrigues", "10x f64 div", "10x f64 sqrt",
                             "10x f64 fma", "10x f32 fma", "10x f32 div", "cv solve (SVD)", "cv solve+rot+compose",
                             "10x f64 add", "10x f64 mul", "10x readlane+add", "10x f32 add", "solve (block Schur)" };
+    {   // the row-layout tail: bit-exact against the scalar one, and each one's latency
+        int* dBad; int hb[2] = { 0, -1 };
+        hipMalloc(&dBad, 2 * sizeof(int));
+        hipMemcpy(dBad, hb, sizeof(hb), hipMemcpyHostToDevice);
+        const int nsys = 20000;
+        hipLaunchKernelGGL(k_rows_check, dim3(1), dim3(64), 0, 0, nsys, dBad, dBad + 1);
+        hipMemcpy(hb, dBad, sizeof(hb), hipMemcpyDeviceToHost);
+        printf("row-layout tail vs scalar tail: %d of %d random systems differ in any output bit (first %d)\n", hb[0], nsys, hb[1]);
+        long long hc[2];
+        for (int w = 0; w < 2; ++w) {
+            if (w) { hipLaunchKernelGGL(k_rows_time<1>, dim3(1), dim3(64), 0, 0, 10, dC, dO); hipLaunchKernelGGL(k_rows_time<1>, dim3(1), dim3(64), 0, 0, N, dC, dO); }
+            else { hipLaunchKernelGGL(k_rows_time<0>, dim3(1), dim3(64), 0, 0, 10, dC, dO); hipLaunchKernelGGL(k_rows_time<0>, dim3(1), dim3(64), 0, 0, N, dC, dO); }
+        }
+        hipMemcpy(hc, dC, sizeof(hc), hipMemcpyDeviceToHost);
+        printf("%-26s %8.1f cycles per repetition (s_memtime, system changing every repetition)\n", "tail scalar", (double)hc[0] / N);
+        printf("%-26s %8.1f cycles per repetition (s_memtime, system changing every repetition)\n", "tail row layout", (double)hc[1] / N);
+    }
     for (int w = 0; w < 15; ++w) {
         launch(w, dA, dO, dC, 10);   // warm
         launch(w, dA, dO, dC, N);

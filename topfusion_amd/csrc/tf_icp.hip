@@ -342,6 +342,9 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 // partials IP_PCOPY = 8 times, 4 KiB apart, and the workgroups of residue class x (one XCD
 // under round-robin dispatch) poll copy x: 32 pollers per line instead of 256 (ICP -1.5 us per
 // launch, A/B profiles/r05/ab_icp_hop2_copies.txt).
+#ifndef IP_TAIL_ROWS
+#define IP_TAIL_ROWS 0                           // A/B: 1 = the row-layout tail (bit-exact, slower: DESIGN 8)
+#endif
 #ifndef IP_OK_BITWISE
 #define IP_OK_BITWISE 1                          // A/B: 0 = short-circuit correspondence flags
 #endif
@@ -637,6 +640,7 @@ k_icp_frame(IcpFrameArgs a)
     // the det check's sums and the affine it may restore live in LDS, not in registers across the
     // iteration: the serial tail runs in the registers they would hold
     __shared__ float det_sm_s[27], aff_prev_s[12];
+    __shared__ double xs_s[9];                  // icp_tail_rows' exchange of S (wave 0)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, wg = blockIdx.x;
     TfDevState* st = a.st;
     unsigned long long* tag = a.tag;
@@ -874,6 +878,20 @@ k_icp_frame(IcpFrameArgs a)
                     if (wave == IP_DETW) {                             // det after the barrier
                         if (lane < 27) det_sm_s[lane] = tot;
                     } else {                                           // solve -> Rodrigues -> compose
+#if IP_TAIL_ROWS
+                      if constexpr (ALG == 0) {                          // row layout (tf_icp_tail.h)
+                        float orow[4], rvr[6];
+                        icp_tail_rows(sm, aff, lane, xs_s, orow, rvr);
+                        IPT_REC_DEP(done, 2 * ICP_NWG + 7, orow[0] + orow[3]);
+                        if (lane < 3) {
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) aff_s[4 * lane + c] = orow[c];
+                        }
+                        IPT_REC_DEP(done, 2 * ICP_NWG + 4, orow[1]);
+                        last_sums = tot;
+                      } else
+#endif
+                      {
                         float rv[6], R[9], tinc[12];
 #ifdef TF_ICP_TIMING
                         if constexpr (ALG == 0) {                       // the two halves stamped apart
@@ -917,6 +935,7 @@ k_icp_frame(IcpFrameArgs a)
                         if (lane < 12) aff_s[lane] = A[lane];
                         IPT_REC_DEP(done, 2 * ICP_NWG + 4, A[0] + A[11]);
                         last_sums = tot;
+                      }
                     }
                 }
                 __syncthreads();

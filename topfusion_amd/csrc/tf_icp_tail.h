@@ -543,6 +543,170 @@ __device__ __forceinline__ void icp_cv_rodrigues(const float* rv, float* R)
     }
 }
 
+// =============================================================================================
+// The canonical tail in row layout (round 5).  icp_solve6_schur + icp_rodrigues + tf_rigid_mul on
+// one wave issue ~500 instructions, every lane computing every element (the segment is issue-
+// bound: ~300 f64 instructions at 4 cycles each).  Here lane i < 3 computes row i of each 3 x 3
+// intermediate (T, S, adj S, the rotation) and of the new affine, values every row needs are read
+// across with readlane or through LDS, and the uniform parts (adj R, the determinants' sums) run
+// once on every lane.  Each element sees exactly the operations, in the same order, of the scalar
+// functions above -- the results are theirs bit for bit (tools/micro/icp_tail.hip: 0 of 20 000
+// random systems differ; 37 GPU parity tests).  ~280 instructions, and no faster: the tail is a
+// dependency chain, not issue-bound (1545 vs 1585 cycles alone; ICP 124.7 -> 128.3 us in the
+// kernel, profiles/r05/ab_icp_tail_rows.txt), so it stays an A/B build (IP_TAIL_ROWS=1).
+// =============================================================================================
+// sums are indexed as StreamHelper lays them out (projective_icp.cpp:51-61): Am[r][c] (r <= c) is
+// sum {0, 7, 13, 18, 22, 25}[r] + c - r, bv[r] is Am[r][6]
+template <typename T>
+__device__ __forceinline__ T icp_sel3(int i, T a, T b, T c) { return i == 0 ? a : (i == 1 ? b : c); }
+__device__ __forceinline__ double icp_rl_d(double v, int src)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), src);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ float icp_rl_f(float v, int src)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+// sm: the 27 sums (uniform); aff: the current affine (uniform); i: the lane (rows 0-2 used);
+// xs: 9 doubles of wave-private LDS.  Out: orow = row i of Tinc * aff, rv = the increment (uniform)
+__device__ __forceinline__ void icp_tail_rows(const float (&sm)[27], const float (&aff)[12], int i, double* xs,
+                                              float (&orow)[4], float (&rv)[6])
+{
+    // (indices written out: icp_smi folded by hand, so every sum is a register, never an indexed one)
+    double R[3][3], Q[3][3], b2[3];
+    R[0][0] = sm[18]; R[0][1] = sm[19]; R[0][2] = sm[20];
+    R[1][0] = sm[19]; R[1][1] = sm[22]; R[1][2] = sm[23];
+    R[2][0] = sm[20]; R[2][1] = sm[23]; R[2][2] = sm[25];
+    Q[0][0] = sm[3]; Q[0][1] = sm[4]; Q[0][2] = sm[5];
+    Q[1][0] = sm[9]; Q[1][1] = sm[10]; Q[1][2] = sm[11];
+    Q[2][0] = sm[14]; Q[2][1] = sm[15]; Q[2][2] = sm[16];
+    b2[0] = sm[21]; b2[1] = sm[24]; b2[2] = sm[26];
+    // adj R (uniform): R is symmetric bit for bit, and so is its adjugate (the mirrored formulas
+    // are the same products, commuted): six cofactors of icp_sym3_adj, det R as there
+    double aR[3][3];
+    aR[0][0] = R[1][1] * R[2][2] - R[1][2] * R[2][1];
+    aR[0][1] = R[0][2] * R[2][1] - R[0][1] * R[2][2];
+    aR[0][2] = R[0][1] * R[1][2] - R[0][2] * R[1][1];
+    aR[1][1] = R[0][0] * R[2][2] - R[0][2] * R[2][0];
+    aR[1][2] = R[0][2] * R[1][0] - R[0][0] * R[1][2];
+    aR[2][2] = R[0][0] * R[1][1] - R[0][1] * R[1][0];
+    aR[1][0] = aR[0][1]; aR[2][0] = aR[0][2]; aR[2][1] = aR[1][2];
+    const double dR = (R[0][0] * aR[0][0] + R[0][1] * aR[1][0]) + R[0][2] * aR[2][0];
+    const double rR = 1.0 / dR;
+    // row i's inputs
+    double Qi[3], Pi[3], Qc[3], aRi[3];
+    Qi[0] = icp_sel3(i, sm[3], sm[9], sm[14]);
+    Pi[0] = icp_sel3(i, sm[0], sm[1], sm[2]);
+    Qc[0] = icp_sel3(i, sm[3], sm[4], sm[5]);
+    aRi[0] = icp_sel3(i, aR[0][0], aR[1][0], aR[2][0]);
+    Qi[1] = icp_sel3(i, sm[4], sm[10], sm[15]);
+    Pi[1] = icp_sel3(i, sm[1], sm[7], sm[8]);
+    Qc[1] = icp_sel3(i, sm[9], sm[10], sm[11]);
+    aRi[1] = icp_sel3(i, aR[0][1], aR[1][1], aR[2][1]);
+    Qi[2] = icp_sel3(i, sm[5], sm[11], sm[16]);
+    Pi[2] = icp_sel3(i, sm[2], sm[8], sm[13]);
+    Qc[2] = icp_sel3(i, sm[14], sm[15], sm[16]);
+    aRi[2] = icp_sel3(i, aR[0][2], aR[1][2], aR[2][2]);
+    const double b1i = icp_sel3(i, sm[6], sm[12], sm[17]);
+    const double b2i = icp_sel3(i, sm[21], sm[24], sm[26]);
+    // T, S, c: row i
+    double Ti[3], Si[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Ti[j] = ((Qi[0] * aR[0][j] + Qi[1] * aR[1][j]) + Qi[2] * aR[2][j]) * rR;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Si[j] = Pi[j] - ((Ti[0] * Q[j][0] + Ti[1] * Q[j][1]) + Ti[2] * Q[j][2]);
+    const double ci = b1i - ((Ti[0] * b2[0] + Ti[1] * b2[1]) + Ti[2] * b2[2]);
+    // S through LDS: row i of adj S = C[i][j] = S[j+1][i+1] S[j+2][i+2] - S[j+1][i+2] S[j+2][i+1]
+    if (i < 3) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) xs[3 * i + j] = Si[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int i1 = i == 0 ? 1 : (i == 1 ? 2 : 0), i2 = i == 0 ? 2 : (i == 1 ? 0 : 1);
+    double SA[3], SB[3];                                    // column i+1, column i+2 of S
+#pragma unroll
+    for (int r = 0; r < 3; ++r) { SA[r] = xs[3 * r + i1]; SB[r] = xs[3 * r + i2]; }
+    const double s0i = xs[i < 3 ? i : 0];                   // S[0][i]
+    double aSi[3];
+    aSi[0] = SA[1] * SB[2] - SB[1] * SA[2];
+    aSi[1] = SA[2] * SB[0] - SB[2] * SA[0];
+    aSi[2] = SA[0] * SB[1] - SB[0] * SA[1];
+    // det S = (S00 aS00 + S01 aS10) + S02 aS20: term k on lane k
+    const double tk = s0i * aSi[0];
+    const double dS = (icp_rl_d(tk, 0) + icp_rl_d(tk, 1)) + icp_rl_d(tk, 2);
+    const double rS = 1.0 / dS;
+    const double c0 = icp_rl_d(ci, 0), c1 = icp_rl_d(ci, 1), c2 = icp_rl_d(ci, 2);
+    const double x1i = ((aSi[0] * c0 + aSi[1] * c1) + aSi[2] * c2) * rS;
+    const double x10 = icp_rl_d(x1i, 0), x11 = icp_rl_d(x1i, 1), x12 = icp_rl_d(x1i, 2);
+    const double ei = b2i - ((Qc[0] * x10 + Qc[1] * x11) + Qc[2] * x12);
+    const double e0 = icp_rl_d(ei, 0), e1 = icp_rl_d(ei, 1), e2 = icp_rl_d(ei, 2);
+    const float x2f = (float)(((aRi[0] * e0 + aRi[1] * e1) + aRi[2] * e2) * rR);
+    rv[0] = (float)x10; rv[1] = (float)x11; rv[2] = (float)x12;
+    rv[3] = icp_rl_f(x2f, 0); rv[4] = icp_rl_f(x2f, 1); rv[5] = icp_rl_f(x2f, 2);
+    // Rodrigues, row i (icp_rodrigues' operations per element)
+    float Ri[3];
+    {
+        constexpr double inv_sin[14] = { 0.0, 1.0/6.0, 1.0/20.0, 1.0/42.0, 1.0/72.0, 1.0/110.0, 1.0/156.0,
+            1.0/210.0, 1.0/272.0, 1.0/342.0, 1.0/420.0, 1.0/506.0, 1.0/600.0, 1.0/702.0 };
+        constexpr double inv_cos[15] = { 0.0, 1.0/2.0, 1.0/12.0, 1.0/30.0, 1.0/56.0, 1.0/90.0, 1.0/132.0,
+            1.0/182.0, 1.0/240.0, 1.0/306.0, 1.0/380.0, 1.0/462.0, 1.0/552.0, 1.0/650.0, 1.0/756.0 };
+        const double rx = rv[0], ry = rv[1], rz = rv[2];
+        const double t2 = (rx * rx + ry * ry) + rz * rz;
+        if (t2 < 4.930380657631324e-32) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) Ri[j] = (i == j) ? 1.0f : 0.0f;
+        } else if (t2 > 9.869604401089358) {
+            float Rf[9];
+            icp_rodrigues_sqrt(rv, Rf);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) Ri[j] = icp_sel3(i, Rf[j], Rf[3 + j], Rf[6 + j]);
+        } else {
+            double pc = 1.0, pa = 1.0, pb = 1.0;
+            if (t2 < 0.000244140625) {
+#pragma unroll
+                for (int n = 4; n >= 1; --n) {
+                    pc = fma(-(t2 * inv_cos[n]), pc, 1.0);
+                    pa = fma(-(t2 * inv_sin[n]), pa, 1.0);
+                    pb = fma(-(t2 * inv_cos[n + 1]), pb, 1.0);
+                }
+            } else if (t2 < 0.015625) {
+#pragma unroll
+                for (int n = 6; n >= 1; --n) {
+                    pc = fma(-(t2 * inv_cos[n]), pc, 1.0);
+                    pa = fma(-(t2 * inv_sin[n]), pa, 1.0);
+                    pb = fma(-(t2 * inv_cos[n + 1]), pb, 1.0);
+                }
+            } else {
+#pragma unroll
+                for (int n = 13; n >= 1; --n) {
+                    pc = fma(-(t2 * inv_cos[n]), pc, 1.0);
+                    pa = fma(-(t2 * inv_sin[n]), pa, 1.0);
+                    pb = fma(-(t2 * inv_cos[n + 1]), pb, 1.0);
+                }
+            }
+            const double b = 0.5 * pb;
+            const double ri = icp_sel3(i, rx, ry, rz);
+            const double rj[3] = { rx, ry, rz };
+            // [r]x row i: (0, -rz, ry), (rz, 0, -rx), (-ry, rx, 0)
+            const double m[3] = { icp_sel3(i, 0.0, rz, -ry), icp_sel3(i, -rz, 0.0, rx), icp_sel3(i, ry, -rx, 0.0) };
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const double I = (i == j) ? 1.0 : 0.0;
+                Ri[j] = (float)((pc * I + b * (ri * rj[j])) + pa * m[j]);
+            }
+        }
+    }
+    // row i of Tinc * aff (tf_rigid_mul)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) orow[c] = (Ri[0] * aff[0 * 4 + c] + Ri[1] * aff[1 * 4 + c]) + Ri[2] * aff[2 * 4 + c];
+    orow[3] = ((Ri[0] * aff[3] + Ri[1] * aff[7]) + Ri[2] * aff[11]) + x2f;
+}
+
 // the iteration's solve + Rodrigues under pose algebra ALG
 template <int ALG>
 __device__ __forceinline__ void icp_solve_rodrigues(const float (&Am)[6][6], const float (&bv)[6], float (&rv)[6], float* R)
