@@ -640,7 +640,9 @@ k_icp_frame(IcpFrameArgs a)
     // the det check's sums and the affine it may restore live in LDS, not in registers across the
     // iteration: the serial tail runs in the registers they would hold
     __shared__ float det_sm_s[27], aff_prev_s[12];
+#if IP_TAIL_ROWS
     __shared__ double xs_s[9];                  // icp_tail_rows' exchange of S (wave 0)
+#endif
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, wg = blockIdx.x;
     TfDevState* st = a.st;
     unsigned long long* tag = a.tag;
