@@ -10,6 +10,8 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
   python3 $R/bench.py --no-cpu-baseline > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
 cd $R
+TFUSION_HIP_LIB=tools/_build/libtfusion_hip_timing.so timeout -k 10 120 python tools/icp_timeline.py > $O/icp_timeline.txt 2>&1 \
+  || { tail -20 $O/icp_timeline.txt; exit 1; }
 python3 tools/trace_summary.py $O/prof/run_kernel_trace.csv > $O/kernel_trace_summary.txt 2>&1 || true
 head -8 $O/kernel_trace_summary.txt | cut -c1-160
 timeout -k 10 300 bash tools/gpu_pmc.sh ${TAG}_c2 C2 > $O/pmc_c2.log 2>&1 || { tail -20 $O/pmc_c2.log; exit 1; }
