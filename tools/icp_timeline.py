@@ -17,7 +17,7 @@ tf = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy), device=0)
 tf.process_frames(dev.ptr, 3)
 bench.device_sync()
 NW = 256
-S = 2 * NW + 8
+S = 2 * NW + 10
 buf = (ctypes.c_ulonglong * (64 * S))()
 _lib.load().tf_debug_icp_timeline(buf)
 tl = np.frombuffer(buf, dtype=np.uint64).reshape(64, S).astype(np.int64)
@@ -37,6 +37,9 @@ for i in range(its):
             f"rodrigues {ph[3]:5.2f} compose {ph[4]:5.2f} det {ph[5]:5.2f}] tail {tail:5.2f}")
     if nxt is not None:
         line += f" next-start {nxt.min():5.2f}/{np.median(nxt):5.2f}/{nxt.max():5.2f}"
+        if tl[i + 1, 2 * NW + 8] > 0:               # the next iteration starts a level: its set-up
+            line += (f" [level set-up {(tl[i + 1, 2 * NW + 8] - t0) / 100.0:5.2f}"
+                     f" maps in {(tl[i + 1, 2 * NW + 9] - t0) / 100.0:5.2f}]")
     print(line)
 # the tail's halves on the shader clock, each run twice back to back (the second run's code is
 # in the instruction cache): workgroup 0, per iteration

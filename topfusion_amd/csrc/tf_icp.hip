@@ -35,7 +35,7 @@ extern "C" int tf_debug_icp_ts(unsigned long long* out)
 #define IPT_NOW() __builtin_amdgcn_s_memrealtime()
 #define IPT_ADD(k, v) do { } while (0)
 // timeline of the last persistent launch: per iteration [256 starts][256 publishes][8 WG0 events]
-#define IPT_STRIDE (2 * ICP_NWG + 8)
+#define IPT_STRIDE (2 * ICP_NWG + 10)
 __device__ unsigned long long g_icp_tl[64 * IPT_STRIDE];
 #define IPT_REC(it, slot) IPT_REC_T(it, slot, 0)
 // a stamp after a value: the value is an operand of a volatile asm placed before the stamp, so
@@ -703,6 +703,7 @@ k_icp_frame(IcpFrameArgs a)
         // uniform selects instead of a dynamic index into the kernel arguments (no scratch copy)
         const IcpLevel L = li == 0 ? a.lv[0] : (li == 1 ? a.lv[1] : a.lv[2]);
         const int slots = li == 0 ? a.slots[0] : (li == 1 ? a.slots[1] : a.slots[2]);
+        IPT_REC(done, 2 * ICP_NWG + 8);                 // (timing build: the level's set-up begins)
         // current-frame maps of my CTA slots -> registers (constant over the level)
         IpPix px[IP_SREG][2];
         int xy[IP_SREG][4];
@@ -726,6 +727,7 @@ k_icp_frame(IcpFrameArgs a)
                 ip_set(px[rr], j, v, n);
             }
         }
+        IPT_REC_DEP(done, 2 * ICP_NWG + 9, px[0][0].vx.x + px[0][1].nz.y);   // (its maps arrived)
         const int iters = li == 0 ? a.iters[0] : (li == 1 ? a.iters[1] : a.iters[2]);
 #pragma unroll 1
         for (int it = 0; it < iters; ++it) {
