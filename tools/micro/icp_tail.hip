@@ -179,6 +179,78 @@ __global__ void __launch_bounds__(64) k_rows_time(int n, long long* cyc, float* 
     if (lane == 0) { cyc[ROWS] = t1 - t0; out[ROWS] = acc; }
 }
 
+
+// candidate: S' = det R * P - Q adj(R) Q^T (one division on the chain; 1/det R off it)
+__device__ __forceinline__ void icp_solve6_schur2(const float (&Af)[6][6], const float (&bf)[6], float (&x)[6])
+{
+    double P[3][3], Q[3][3], R[3][3], b1[3], b2[3];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) { P[i][j] = Af[i][j]; Q[i][j] = Af[i][3 + j]; R[i][j] = Af[3 + i][3 + j]; }
+        b1[i] = bf[i]; b2[i] = bf[3 + i];
+    }
+    double aR[3][3], dR, aS[3][3], dS, U[3][3], S[3][3], c[3], x1[3], e[3];
+    icp_sym3_adj(R, aR, dR);
+    const double rR = 1.0 / dR;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) U[i][j] = (Q[i][0] * aR[0][j] + Q[i][1] * aR[1][j]) + Q[i][2] * aR[2][j];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) S[i][j] = dR * P[i][j] - ((U[i][0] * Q[j][0] + U[i][1] * Q[j][1]) + U[i][2] * Q[j][2]);
+        c[i] = dR * b1[i] - ((U[i][0] * b2[0] + U[i][1] * b2[1]) + U[i][2] * b2[2]);
+    }
+    icp_sym3_adj(S, aS, dS);
+    const double rS = 1.0 / dS;
+    for (int i = 0; i < 3; ++i) x1[i] = ((aS[i][0] * c[0] + aS[i][1] * c[1]) + aS[i][2] * c[2]) * rS;
+    for (int i = 0; i < 3; ++i) e[i] = b2[i] - ((Q[0][i] * x1[0] + Q[1][i] * x1[1]) + Q[2][i] * x1[2]);
+    for (int i = 0; i < 3; ++i) {
+        x[i] = (float)x1[i];
+        x[3 + i] = (float)(((aR[i][0] * e[0] + aR[i][1] * e[1]) + aR[i][2] * e[2]) * rR);
+    }
+}
+__device__ void unpack27(const float (&sm)[27], float (&Am)[6][6], float (&bv)[6])
+{
+    int shift = 0;
+    for (int i = 0; i < 6; ++i)
+        for (int j = i; j < 7; ++j) {
+            const float v = sm[shift++];
+            if (j == 6) bv[i] = v; else { Am[j][i] = v; Am[i][j] = v; }
+        }
+}
+template <int V>
+__global__ void __launch_bounds__(64) k_solve_time(int n, long long* cyc, float* out, int* ndiff, float* maxrel)
+{
+    float sm[27], aff[12];
+    make_system(11u, sm, aff);
+    float acc = 0.f;
+    const long long t0 = clock64();
+    for (int it = 0; it < n; ++it) {
+        float Am[6][6], bv[6], rv[6];
+        unpack27(sm, Am, bv);
+        if constexpr (V == 0) icp_solve6_schur(Am, bv, rv); else icp_solve6_schur2(Am, bv, rv);
+        acc = rv[0] + rv[4];
+        sm[0] += acc * 1e-30f;          // the next repetition's whole system depends on this one
+        sm[22] += rv[4] * 1e-30f;
+    }
+    const long long t1 = clock64();
+    if (threadIdx.x == 0) { cyc[V] = t1 - t0; out[V] = acc; }
+    if (V == 1 && threadIdx.x == 0) {   // bits: S' against the canonical solve over random systems
+        int d = 0; float mr = 0.f;
+        for (int sys = 0; sys < 20000; ++sys) {
+            float s2[27], a2[12], Am[6][6], bv[6], r0[6], r1[6];
+            make_system((unsigned)sys, s2, a2);
+            unpack27(s2, Am, bv);
+            icp_solve6_schur(Am, bv, r0); icp_solve6_schur2(Am, bv, r1);
+            bool same = true;
+            for (int k = 0; k < 6; ++k) {
+                same = same && __float_as_uint(r0[k]) == __float_as_uint(r1[k]);
+                const float rel = fabsf(r0[k] - r1[k]) / fmaxf(fabsf(r0[k]), 1e-30f);
+                mr = fmaxf(mr, rel);
+            }
+            d += !same;
+        }
+        *ndiff = d; *maxrel = mr;
+    }
+}
+
 template <int W>
 static void launch_t(int w, const float* a, float* o, long long* c, int n)
 {
@@ -216,6 +288,20 @@ int main()
         hipMemcpy(hc, dC, sizeof(hc), hipMemcpyDeviceToHost);
         printf("%-26s %8.1f cycles per repetition (s_memtime, system changing every repetition)\n", "tail scalar", (double)hc[0] / N);
         printf("%-26s %8.1f cycles per repetition (s_memtime, system changing every repetition)\n", "tail row layout", (double)hc[1] / N);
+    }
+    {   // the S' solve (one division on the chain) against the canonical Schur solve
+        int* dD; float* dM; hipMalloc(&dD, sizeof(int)); hipMalloc(&dM, sizeof(float));
+        long long hc[2];
+        hipLaunchKernelGGL(k_solve_time<0>, dim3(1), dim3(64), 0, 0, 10, dC, dO, dD, dM);
+        hipLaunchKernelGGL(k_solve_time<0>, dim3(1), dim3(64), 0, 0, N, dC, dO, dD, dM);
+        hipLaunchKernelGGL(k_solve_time<1>, dim3(1), dim3(64), 0, 0, 10, dC, dO, dD, dM);
+        hipLaunchKernelGGL(k_solve_time<1>, dim3(1), dim3(64), 0, 0, N, dC, dO, dD, dM);
+        hipMemcpy(hc, dC, sizeof(hc), hipMemcpyDeviceToHost);
+        int nd = 0; float mr = 0;
+        hipMemcpy(&nd, dD, sizeof(int), hipMemcpyDeviceToHost); hipMemcpy(&mr, dM, sizeof(float), hipMemcpyDeviceToHost);
+        printf("%-26s %8.1f cycles per repetition (s_memtime, system changing every repetition)\n", "solve Schur", (double)hc[0] / N);
+        printf("%-26s %8.1f cycles per repetition (s_memtime, system changing every repetition)\n", "solve Schur S'", (double)hc[1] / N);
+        printf("S' vs Schur: %d of 20000 random systems differ in some output bit, max relative difference %g\n", nd, mr);
     }
     for (int w = 0; w < 15; ++w) {
         launch(w, dA, dO, dC, 10);   // warm
