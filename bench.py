@@ -658,6 +658,11 @@ def main():
     prof_timed = tf.profile_read() if not args.no_profile else {}
     tot = tf.totals()
     st = tf.stats()
+    # the timed context closes here: the measurements below each run a context of their own, and
+    # with two contexts on a device every persistent ICP launch is ordered after the other
+    # context's by a stream event (tf_capi.hip icp_order_*), a dispatch gap no single user sees
+    tf_params, tf_alg, tf_persistent = tf.params(), tf.pose_algebra(), tf.icp_persistent()
+    tf.close()
     prof = {}
     lanes_bd = nvis_bd = None
     if n_breakdown:
@@ -736,9 +741,9 @@ def main():
                 if not ms:
                     continue
                 if k == "integrate" and lanes_bd is not None:    # lanes counted in the breakdown pass
-                    b = stage_bytes(k, tf.params(), nvis_bd, W, H, lanes_bd)
+                    b = stage_bytes(k, tf_params, nvis_bd, W, H, lanes_bd)
                 else:
-                    b = stage_bytes(k, tf.params(), nvis_mean, W, H)
+                    b = stage_bytes(k, tf_params, nvis_mean, W, H)
                 ach = b / (ms * 1e-3) / 1e9
                 roof_all[k] = {"bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                "frac": round(ach / PEAK_HBM_GBS, 5),
@@ -767,7 +772,7 @@ def main():
             first = args.warmup * F
             frames = dev.download(0, min(n_frames, first + 128))
             nt = omp_threads()
-            cpu = cpu_baseline_protocol(frames, first, pkw, args.cpu_seconds, nt, tf.pose_algebra())
+            cpu = cpu_baseline_protocol(frames, first, pkw, args.cpu_seconds, nt, tf_alg)
         out = {
             "metric": f"fused frames/sec @{W}x{H}, {args.voxel * 1000:g} mm voxel hash; ICP+integrate ms/frame"
                       + (" (swapping scene)" if args.swapping else "")
@@ -828,7 +833,7 @@ def main():
                 "timed_frames": [args.warmup * F, n_frames]},
             "render_tiles_mean": round(tot["tiles_sum"] / max(1, tot["frames_tracked"]), 1),
             "visible_blocks_last": st["noVisibleEntries"],
-            "allocated_blocks_last": int(tf.params().n_blocks - 1 - st["lastFreeBlockId"]),
+            "allocated_blocks_last": int(tf_params.n_blocks - 1 - st["lastFreeBlockId"]),
             "last_frame_ok": bool(ok[-1]),
             "swapped_out_per_frame": round(tot["swapped_out"] / max(1, tot["frames"]), 2) if args.swapping else None,
             "swapped_in_merged_per_frame": round(tot["swapped_in_merged"] / max(1, tot["frames"]), 2) if args.swapping else None,
@@ -839,13 +844,12 @@ def main():
             "roofline": roof,
             "hbm_stream_copy_GBs": stream_gbs,
             "roofline_stages": roof_all,
-            "icp_schedule": "persistent" if tf.icp_persistent() else "per_iteration",
-            "pose_algebra": {0: "canonical", 2: "opencv2", 4: "opencv4"}[tf.pose_algebra()],
+            "icp_schedule": "persistent" if tf_persistent else "per_iteration",
+            "pose_algebra": {0: "canonical", 2: "opencv2", 4: "opencv4"}[tf_alg],
             "cpu_baseline": cpu,
             "multi_gpu": multi if world > 1 else None,
         }
         print(json.dumps(out))
-    tf.close()
     dev.free()
     if rgb is not None:
         rgb.free()
