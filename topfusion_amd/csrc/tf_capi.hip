@@ -453,7 +453,13 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
         c->icp_persistent = (env && env[0] == '0') ? 0 : tfk_icp_persistent_ok(c);
     }
     if (c->icp_persistent) {
-        e = hipEventCreateWithFlags(&c->icp_ev, hipEventDisableTiming);
+        // ordering only (the contexts share no memory): no system-scope fence at the record --
+        // with it, each record wrote back and invalidated the caches, a ~5 us dispatch gap after
+        // every persistent ICP launch while two contexts exist (TF_ICP_EV_SYSFENCE=1: the old event)
+#ifndef TF_ICP_EV_SYSFENCE
+#define TF_ICP_EV_SYSFENCE 0
+#endif
+        e = hipEventCreateWithFlags(&c->icp_ev, hipEventDisableTiming | (TF_ICP_EV_SYSFENCE ? 0u : hipEventDisableSystemFence));
         if (e != hipSuccess) { c->icp_ev = nullptr; ctx_free(c); return tf_from_hip(e); }
         icp_order_register(c, +1);
     }
