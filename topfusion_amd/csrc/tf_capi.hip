@@ -699,7 +699,10 @@ extern "C" tf_status tf_profile_enable(tf_ctx* c, int enable)
 {
     if (!c) return TF_INVALID_ARG;
     if (enable && !c->prof_ev[0]) {
-        for (int i = 0; i < 2 * TF_NUM_STAGES * TF_PROF_RING; ++i) TF_CHECK(hipEventCreate(&c->prof_ev[i]));
+        // timing only (read after the stream is synchronised): no system-scope fence at the record,
+        // whose cache writeback and invalidate were a dispatch gap after every timed stage
+        for (int i = 0; i < 2 * TF_NUM_STAGES * TF_PROF_RING; ++i)
+            TF_CHECK(hipEventCreateWithFlags(&c->prof_ev[i], hipEventDisableSystemFence));
     }
     c->prof_enabled = enable ? 1 : 0;
     c->count_lanes = enable ? 1 : 0;
