@@ -198,17 +198,25 @@ void*     tf_get_stream(tf_ctx* ctx);
 tf_status tf_get_schedule(tf_ctx* ctx, int* icp_persistent);
 /* The ICP iterations' pose algebra: estimateTransform's cv::determinant(A), cv::solve(A, b, r,
  * cv::DECOMP_SVD) and Affine3f Tinc(r) (tfusion/src/projective_icp.cpp:197-209).
- *   TF_POSE_ALGEBRA_CANONICAL (default): the pivoting LU determinant, an LDL^T solve in double and
- *     Rodrigues in sinc form -- the fast form (a short serial tail per iteration);
- *   TF_POSE_ALGEBRA_OPENCV4 / _OPENCV2: OpenCV's own algorithms as OpenCV 3.x-4.x / 2.4.9 publish
- *     them (Matx_DetOp's LU, JacobiSVD + SVBkSb in float, Affine3::rotation with float rounding of
- *     every Matx operation), the reference's arithmetic (see DESIGN.md §2 for what the two
- *     algebras do to a sequence).
+ *   TF_POSE_ALGEBRA_CANONICAL: the pivoting LU determinant, a 2 x 2 block Schur solve in double
+ *     (closed-form 3 x 3 adjugates) and Rodrigues in sinc form -- a short serial tail per iteration;
+ *   TF_POSE_ALGEBRA_OPENCV4 / _OPENCV2: OpenCV's published algorithms as the oracle restates them
+ *     for OpenCV 3.x-4.x / 2.4.9 (Matx_DetOp's LU, JacobiSVD + SVBkSb in float, Affine3::rotation
+ *     with float rounding of every Matx operation; not checked against an OpenCV build, none is
+ *     available) -- the reference's algebra (see DESIGN.md §2 for what the two algebras do to a
+ *     sequence).
  * The environment variable TFUSION_ICP_SOLVE=svd|opencv4|opencv2 sets it at tf_create.
  * TF_INVALID_ARG if the algebra's persistent ICP kernel would not fit the schedule chosen. */
 enum { TF_POSE_ALGEBRA_CANONICAL = 0, TF_POSE_ALGEBRA_OPENCV2 = 2, TF_POSE_ALGEBRA_OPENCV4 = 4 };
 tf_status tf_set_pose_algebra(tf_ctx* ctx, int algebra);
 tf_status tf_get_pose_algebra(tf_ctx* ctx, int* algebra);
+/* One ICP iteration's algebra on caller systems (no context): for each of n systems given as
+ * the 27 sums of estimateTransform's reduction (StreamHelper layout, projective_icp.cpp:51-61),
+ * det[q] = cv::determinant(A) and x[q] = cv::solve(A, b, DECOMP_SVD) (:197-206) under the
+ * algebra TF_POSE_ALGEBRA_* -- the same device code the persistent ICP runs (OpenCV algebras:
+ * the lane-parallel Jacobi SVD).  Device buffers: sums 27 n floats, x 6 n floats, det n doubles
+ * (may be NULL); asynchronous on `stream` (NULL: the null stream). */
+tf_status tf_icp_solve_systems(int algebra, const float* dev_sums, int n, float* dev_x, double* dev_det, void* stream);
 
 /* ---- stage entry points (operate on context state; parity tests) ------------- */
 /* computeDists + depthBilateralFilter + depthTruncation + depthBuildPyramid +

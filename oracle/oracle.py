@@ -83,8 +83,12 @@ def lib(omp=False):
         L.tfo_cv_det6.argtypes = [P, ctypes.c_int]; L.tfo_cv_det6.restype = ctypes.c_double
         L.tfo_cv_jacobi_svd.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int]
         L.tfo_cv_solve_svd6.argtypes = [P, P, P]
+        L.tfo_solve6.argtypes = [P, P, P]
+        L.tfo_det6.argtypes = [P]; L.tfo_det6.restype = ctypes.c_double
         L.tfo_cv_rodrigues.argtypes = [P, P, ctypes.c_int]
         L.tfo_cv_svd_stats.argtypes = [P, ctypes.c_int]
+        L.tfo_capture_sums.argtypes = [P, ctypes.c_longlong]
+        L.tfo_captured_sums.restype = ctypes.c_longlong
         L.tfo_cv_hypot.argtypes = [ctypes.c_double, ctypes.c_double]; L.tfo_cv_hypot.restype = ctypes.c_double
         L.tfo_point_conv.argtypes = [P, P]
         L.tfo_hash_index.argtypes = [ctypes.c_int] * 4; L.tfo_hash_index.restype = ctypes.c_int

@@ -721,7 +721,9 @@ void tfo_cv_jacobi_svd(float* At, float* Wout, float* Vt, int m, int n)
     uint64_t rng = 0x12345678;
     for (i = 0; i < n; i++) {
         sd = W[i];
-        while (sd <= minval) {
+        /* bounded as OpenCV 3.x / 4.x write it (`ii < 100 && sd <= minval`, then `sd > minval ? 1/sd
+           : 0`); 2.4.9's unbounded loop and 1/sd differ only where it would not terminate */
+        for (int ii = 0; ii < 100 && sd <= minval; ii++) {
             const float val0 = (float)(1. / m);
             for (k = 0; k < m; k++) At[i * m + k] = (cv_rng_next(&rng) & 256) != 0 ? val0 : -val0;
             for (iter = 0; iter < 2; iter++)
@@ -741,7 +743,7 @@ void tfo_cv_jacobi_svd(float* At, float* Wout, float* Vt, int m, int n)
             for (k = 0; k < m; k++) { float t = At[i * m + k]; sd += (double)t * t; }
             sd = sqrt(sd);
         }
-        float s = (float)(1 / sd);
+        float s = (float)(sd > minval ? 1 / sd : 0.);
         for (k = 0; k < m; k++) At[i * m + k] *= s;
     }
 }
@@ -805,8 +807,21 @@ void tfo_cv_rodrigues(const float rv[3], float R[9], int mode)
 
 /* one iteration of estimateTransform after the reductions, projective_icp.cpp:187-210
    (StreamHelper::get unpacking :43-62) */
+/* the canonical algebra's determinant and solve (the forms tfo_icp_step uses), exported for the
+   solve-only parity test (tests/test_gpu_pose_algebra.py) */
+void tfo_solve6(const float A[36], const float b[6], float x[6]) { solve6(A, b, x); }
+double tfo_det6(const float A[36]) { return cv_det6(A); }
+
+/* test-only capture of every ICP step's 27 sums (tools/svd_systems.py: realistic inputs for the
+   Jacobi-SVD micro-benchmarks); off unless a buffer is installed */
+static float* g_cap_buf;
+static long long g_cap_cap, g_cap_n;
+void tfo_capture_sums(float* buf, long long cap) { g_cap_buf = buf; g_cap_cap = cap; g_cap_n = 0; }
+long long tfo_captured_sums(void) { return g_cap_n; }
+
 int tfo_icp_step(const float s[27], float affine[12], double* det_out)
 {
+    if (g_cap_buf && g_cap_n < g_cap_cap) memcpy(g_cap_buf + 27 * g_cap_n++, s, 27 * sizeof(float));
     float A[36], b[6];
     int shift = 0;
     for (int i = 0; i < 6; ++i)

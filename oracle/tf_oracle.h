@@ -119,12 +119,18 @@ enum { TFO_POSE_CANONICAL = 0, TFO_POSE_OPENCV2 = 2, TFO_POSE_OPENCV4 = 4 };
 void tfo_set_pose_algebra(int mode, int use_libm);
 int tfo_get_pose_algebra(void);
 double tfo_cv_det6(const float A[36], int mode);
+/* the canonical algebra's determinant and solve (test-only exports) */
+void tfo_solve6(const float A[36], const float b[6], float x[6]);
+double tfo_det6(const float A[36]);
 void tfo_cv_jacobi_svd(float* At, float* W, float* Vt, int m, int n);
 void tfo_cv_solve_svd6(const float A[36], const float b[6], float x[6]);
 void tfo_cv_rodrigues(const float rvec[3], float R[9], int mode);
 double tfo_cv_hypot(double x, double y);
 /* diagnostics: Jacobi calls, sweeps, rotations, max sweeps, histogram of the converged sweep index */
 void tfo_cv_svd_stats(long long out[36], int reset);
+/* test-only: record every ICP step's 27 sums into buf (27 floats each, at most cap steps) */
+void tfo_capture_sums(float* buf, long long cap);
+long long tfo_captured_sums(void);
 void tfo_rigid_mul(const float a[12], const float b[12], float out[12]);
 void tfo_rigid_inv(const float a[12], float out[12]);
 int  tfo_matrix4_inv(const float m[16], float out[16]);

@@ -92,3 +92,73 @@ def test_opencv2_algebra_per_call(cv_oracle, monkeypatch, schedule):
     compare_scene(g, o, f"opencv2 {schedule}")
     g.close()
     dev.free()
+
+
+def _solve_systems_inputs():
+    """ICP systems (27 sums each): every iteration the oracle ran on the bench's first 120 C2
+    frames under OpenCV 4's algebra (tests/golden/icp_systems_C2_opencv4.f32, made by
+    tools/svd_systems.py), random ICP-like systems at three scales, and degenerate ones -- A = 0
+    and rank 1..5 (zero singular values: the random completion)."""
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    cap = np.fromfile(os.path.join(here, "golden", "icp_systems_C2_opencv4.f32"), np.float32).reshape(-1, 27)
+    rng = np.random.default_rng(20261018)
+    iu = [(a, c) for a in range(6) for c in range(a, 7)]
+    out = [cap]
+    for scale, rows in ((1.0, 40), (1e-6, 12), (1e6, 8), (1.0, 7)):
+        v = (rng.random((3000, rows, 7), np.float32) - 0.5) * np.float32(scale)
+        s = np.stack([np.einsum("nr,nr->n", v[:, :, a], v[:, :, c]) for a, c in iu], axis=1)
+        out.append(s.astype(np.float32))
+    deg = []
+    for rank in range(6):
+        for _ in range(20):
+            v = rng.random((rank, 7), np.float32) - 0.5
+            deg.append(np.array([np.dot(v[:, a], v[:, c]) for a, c in iu], np.float32))
+    out.append(np.stack(deg))
+    return np.ascontiguousarray(np.concatenate(out), np.float32)
+
+
+@pytest.mark.parametrize("algebra", ["opencv4", "opencv2", "canonical"])
+def test_solve_systems_bit_exact(oracle_mod, algebra):
+    """tf_icp_solve_systems (the persistent ICP's det + solve device code; OpenCV: the lane-parallel
+    Jacobi SVD with its fast (c, s) sequence and exact fallback) against the oracle's serial
+    cv::determinant / cv::solve(DECOMP_SVD) (canonical: LU + block Schur), every bit of x and det."""
+    import ctypes
+    from parity_util import DeviceBuffer
+    from topfusion_amd import _lib as L
+    sums = _solve_systems_inputs()
+    n = sums.shape[0]
+    code = {"canonical": 0, "opencv2": 2, "opencv4": 4}[algebra]
+    d_in = DeviceFrames(sums)
+    d_x = DeviceBuffer(n * 6 * 4)
+    d_det = DeviceBuffer(n * 8)
+    L.check(L.load().tf_icp_solve_systems(code, d_in.ptr, n, d_x.ptr, d_det.ptr, None), "tf_icp_solve_systems")
+    d_x.sync()
+    x = np.empty((n, 6), np.float32)
+    det = np.empty(n, np.float64)
+    assert d_x._hip.hipMemcpy(x.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(d_x.ptr), ctypes.c_size_t(x.nbytes), 2) == 0
+    assert d_x._hip.hipMemcpy(det.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(d_det.ptr), ctypes.c_size_t(det.nbytes), 2) == 0
+    Lo = oracle_mod.lib()
+    ox = np.empty((n, 6), np.float32)
+    od = np.empty(n, np.float64)
+    iu = [(a, c) for a in range(6) for c in range(a, 7)]
+    for q in range(n):
+        A = np.zeros((6, 6), np.float32)
+        b = np.zeros(6, np.float32)
+        for (a, c), v in zip(iu, sums[q]):
+            if c == 6:
+                b[a] = v
+            else:
+                A[a, c] = A[c, a] = v
+        xq = np.zeros(6, np.float32)
+        if code == 0:
+            Lo.tfo_solve6(A.ctypes.data, b.ctypes.data, xq.ctypes.data)
+            od[q] = Lo.tfo_det6(A.ctypes.data)
+        else:
+            Lo.tfo_cv_solve_svd6(A.ctypes.data, b.ctypes.data, xq.ctypes.data)
+            od[q] = Lo.tfo_cv_det6(A.ctypes.data, code)
+        ox[q] = xq
+    assert_bit_exact(f"{algebra} solve x", x, ox)
+    assert_bit_exact(f"{algebra} det", det, od)
+    for buf in (d_in, d_x, d_det):
+        buf.free()

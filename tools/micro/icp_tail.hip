@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(64) k_tail(const float* in, float* out, long l
             dx = f;
         } else if constexpr (which == 8) {                // the reference's cv::solve(DECOMP_SVD) (ALG 4)
             float rv[6];
-            icp_cv_solve_svd6(Am, bv, rv);
+            icp_cv_solve_svd6<4>(Am, bv, rv);
             bv[0] += rv[0] * 1e-30f;
         } else if constexpr (which == 9) {                // cv solve + Affine3f rotation + compose
             float rv[6], R[9], tinc[12];

@@ -119,6 +119,7 @@ def load():
         "tf_get_schedule": ([P, ctypes.POINTER(I)], I),
         "tf_set_pose_algebra": ([P, I], I),
         "tf_get_pose_algebra": ([P, ctypes.POINTER(I)], I),
+        "tf_icp_solve_systems": ([I, P, I, P, P, P], I),
         "tf_stage_preprocess": ([P, P, S], I),
         "tf_stage_preprocess_host": ([P, P, S], I),
         "tf_stage_icp": ([P, P, ctypes.POINTER(I), ctypes.POINTER(I)], I),

@@ -130,6 +130,9 @@ __device__ __forceinline__ void tstep(float* v, int lane)
     }
 }
 
+#ifndef IP_SVD_LANES
+#define IP_SVD_LANES 1         // the OpenCV algebra's cv::solve(DECOMP_SVD): 1 = lane-parallel, 0 = serial (A/B)
+#endif
 #include "tf_icp_tail.h"
 #include "tf_pose.h"
 #include "tf_vis.h"
@@ -278,7 +281,12 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
     }
     float rv[6];
     float R[9], tinc[12], A[12];
-    icp_solve_rodrigues<ALG>(Am, bv, rv, R);
+    if constexpr (ALG != 0 && IP_SVD_LANES) {                  // (tot: lane 2q holds sum q)
+        icp_cv_solve_svd6_lanes<ALG>(tot, 2, lane, rv);
+        icp_cv_rodrigues<ALG>(rv, R);
+    } else {
+        icp_solve_rodrigues<ALG>(Am, bv, rv, R);
+    }
     ICP_TS(5);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -925,7 +933,12 @@ k_icp_frame(IcpFrameArgs a)
                             R[0] = R[0] + R2[0] * 0.0f;
                         } else
 #endif
-                        icp_solve_rodrigues<ALG>(Am, bv, rv, R);        // projective_icp.cpp:206-209
+                        if constexpr (ALG != 0 && IP_SVD_LANES) {       // projective_icp.cpp:206-209
+                            icp_cv_solve_svd6_lanes<ALG>(tot, 1, lane, rv);
+                            icp_cv_rodrigues<ALG>(rv, R);
+                        } else {
+                            icp_solve_rodrigues<ALG>(Am, bv, rv, R);
+                        }
                         IPT_REC_DEP(done, 2 * ICP_NWG + 7, R[0] + R[8]);
 #pragma unroll
                         for (int j = 0; j < 3; ++j) {
@@ -1151,4 +1164,46 @@ hipError_t tfk_icp(tf_ctx* c, int pose_update, int frame_begin, int fold_t3)
         }
     }
     return hipGetLastError();
+}
+
+// ---- the iteration's algebra on caller systems (tf_icp_solve_systems): one wave per system,
+// the forms k_icp_frame runs (canonical: LU determinant + block Schur solve; OpenCV: Matx_DetOp +
+// the lane-parallel cv::solve(DECOMP_SVD))
+template <int ALG>
+__global__ void __launch_bounds__(64) k_solve_systems(const float* __restrict__ sums, int n, float* __restrict__ x,
+                                                      double* __restrict__ det)
+{
+    const int lane = threadIdx.x;
+    for (int q = blockIdx.x; q < n; q += gridDim.x) {
+        float sm[27], Am[6][6], bv[6], xs[6];
+#pragma unroll
+        for (int i = 0; i < 27; ++i) sm[i] = sums[27 * (size_t)q + i];
+        ip_unpack(sm, Am, bv);
+        const double d = icp_det6<ALG>(Am);
+        if constexpr (ALG != 0 && IP_SVD_LANES) {
+            const float tot = lane < 27 ? sums[27 * (size_t)q + lane] : 0.f;
+            icp_cv_solve_svd6_lanes<ALG>(tot, 1, lane, xs);
+        } else if constexpr (ALG != 0) {
+            icp_cv_solve_svd6<ALG>(Am, bv, xs);
+        } else {
+            icp_solve6_schur(Am, bv, xs);
+        }
+        if (lane < 6) x[6 * (size_t)q + lane] = xs[lane];
+        if (lane == 0 && det) det[q] = d;
+    }
+}
+
+extern "C" tf_status tf_icp_solve_systems(int algebra, const float* dev_sums, int n, float* dev_x, double* dev_det,
+                                          void* stream)
+{
+    if (n < 0 || (n > 0 && (!dev_sums || !dev_x))) return TF_INVALID_ARG;
+    if (algebra != TF_POSE_ALGEBRA_CANONICAL && algebra != TF_POSE_ALGEBRA_OPENCV2 && algebra != TF_POSE_ALGEBRA_OPENCV4)
+        return TF_INVALID_ARG;
+    if (n == 0) return TF_OK;
+    const hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(n < 4096 ? n : 4096);
+    if (algebra == 0) hipLaunchKernelGGL(k_solve_systems<0>, grid, dim3(64), 0, s, dev_sums, n, dev_x, dev_det);
+    else if (algebra == 2) hipLaunchKernelGGL(k_solve_systems<2>, grid, dim3(64), 0, s, dev_sums, n, dev_x, dev_det);
+    else hipLaunchKernelGGL(k_solve_systems<4>, grid, dim3(64), 0, s, dev_sums, n, dev_x, dev_det);
+    return hipGetLastError() == hipSuccess ? TF_OK : TF_HIP_ERROR;
 }

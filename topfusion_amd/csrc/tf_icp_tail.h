@@ -289,6 +289,19 @@ __device__ __forceinline__ void icp_solve6_ldl(const float (&Af)[6][6], const fl
 constexpr float TF_FLT_EPS = 1.19209290e-07f;
 constexpr double TF_FLT_MIN = 1.17549435e-38;
 
+// readlane of a double / float (uniform result)
+__device__ __forceinline__ double icp_rl_d(double v, int src)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, src);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), src);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ float icp_rl_f(float v, int src)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+
 // hypot (the oracle's portable hypot): fma-corrected sum of squares
 __device__ __forceinline__ double icp_cv_hypot(double x, double y)
 {
@@ -394,9 +407,20 @@ __device__ __forceinline__ unsigned icp_cv_rng(unsigned long long& st)
     return (unsigned)st;
 }
 
+// What follows JacobiSVDImpl_<float>'s sweeps: W = |row| sorted descending (rows of At and Vt
+// with it), a zero singular value completed at random, the rows of At normalised; then
+// SVBkSbImpl_<float>(6, 6, w, u = At (uT), v = Vt (vT), b, nb = 1).  Shared by the serial solve
+// below and the lane-parallel one's zero-singular-value path.  The completion is bounded at 100
+// draws and a row still zero after them is scaled by 0, as OpenCV 3.x / 4.x write it
+// (`ii < 100 && sd <= minval`, `sd > minval ? 1/sd : 0`); 2.4.9 writes an unbounded loop and 1/sd,
+// which differ only where 2.4.9 would not terminate.
+template <int ALG>
+__device__ __forceinline__ void icp_cv_svd_finish(float (&At)[6][6], float (&Vt)[6][6], const float (&bv)[6], float (&x)[6]);
+
 // cv::solve(A, b, x, DECOMP_SVD) for a float 6x6 and one right-hand side (lapack.cpp): the work
 // matrix transpose(A), JacobiSVDImpl_<float>(m = n = 6, eps 2 FLT_EPSILON, minval FLT_MIN), then
 // SVBkSbImpl_<float> with threshold (sum w) * (float)(2 DBL_EPSILON)
+template <int ALG>
 __device__ __forceinline__ void icp_cv_solve_svd6(const float (&A)[6][6], const float (&bv)[6], float (&x)[6])
 {
     float At[6][6], Vt[6][6];
@@ -420,6 +444,13 @@ __device__ __forceinline__ void icp_cv_solve_svd6(const float (&A)[6][6], const 
         ch |= icp_cv_rot<3, 4>(At, Vt, W); ch |= icp_cv_rot<3, 5>(At, Vt, W); ch |= icp_cv_rot<4, 5>(At, Vt, W);
         if (!ch) break;
     }
+    icp_cv_svd_finish<ALG>(At, Vt, bv, x);
+}
+
+template <int ALG>
+__device__ __forceinline__ void icp_cv_svd_finish(float (&At)[6][6], float (&Vt)[6][6], const float (&bv)[6], float (&x)[6])
+{
+    double W[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         double sd = 0;
@@ -453,7 +484,8 @@ __device__ __forceinline__ void icp_cv_solve_svd6(const float (&A)[6][6], const 
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         double sd = W[i];
-        while (sd <= TF_FLT_MIN) {                 // a zero singular value: random completion
+#pragma unroll 1
+        for (int ii = 0; ii < 100 && sd <= TF_FLT_MIN; ii++) {   // a zero singular value: random completion
             const float val0 = (float)(1. / 6);
 #pragma unroll
             for (int k = 0; k < 6; k++) At[i][k] = (icp_cv_rng(rng) & 256) != 0 ? val0 : -val0;
@@ -480,7 +512,7 @@ __device__ __forceinline__ void icp_cv_solve_svd6(const float (&A)[6][6], const 
             for (int k = 0; k < 6; k++) sd += (double)At[i][k] * At[i][k];
             sd = sqrt(sd);
         }
-        const float s = (float)(1 / sd);
+        const float s = (float)(sd > TF_FLT_MIN ? 1 / sd : 0.);
 #pragma unroll
         for (int k = 0; k < 6; k++) At[i][k] *= s;
     }
@@ -503,6 +535,312 @@ __device__ __forceinline__ void icp_cv_solve_svd6(const float (&A)[6][6], const 
 #pragma unroll
         for (int j = 0; j < 6; j++) x[j] = (float)(x[j] + s * Vt[i][j]);
     }
+}
+
+// =============================================================================================
+// cv::solve(DECOMP_SVD) lane-parallel (round 6; IP_SVD_LANES).  The serial form above runs each
+// sweep's 15 rotations one after another on uniform data.  Here one wave holds the work matrix
+// one element per lane -- lane l = 8 r + k holds At[r][k], Vt[r][k] and |row r|^2 (rows 6, 7 and
+// columns 6, 7 are padding) -- and:
+//  * rotations on disjoint row pairs touch disjoint data, so the sweeps run in dependence order:
+//    a period of 6 levels of up to three concurrent rotations per sweep, sweep s + 1 starting
+//    while sweep s finishes (SV_PART; every row sees its rotations in the serial order, and a
+//    sweep that changed nothing is detected after its last rotation, (4, 5), exactly where the
+//    serial loop breaks -- the next sweep's rotations already issued then find the data they
+//    would have found and rotate nothing);
+//  * a rotation's sums (the dot product, the new |row|^2) keep the serial order: the six exact
+//    double products reach the row's lane 0 by DPP row_shl and are added there in order;
+//  * (c, s) come from a short sequence (v_rsq_f64 / v_rcp_f64 plus one refinement each,
+//    icp_sv_cs) whose double results are accepted only when they lie further from a float
+//    rounding boundary than the sequence's error bound -- then their float roundings are the
+//    exact sequence's -- and otherwise the exact sequence runs (a wave-uniform branch, about 1 in
+//    2000 rotations);
+//  * sort, normalisation and back substitution lane-parallel (a zero singular value takes the
+//    serial finish on the gathered matrices).
+// Every element sees the serial form's operations in the same order: the result is
+// icp_cv_solve_svd6's bit for bit (tools/micro/svd_lanes.hip; tools/svd_lanes_proto.c models the
+// schedule on the CPU against the oracle).
+// =============================================================================================
+// partner row of each row r (4-bit fields, 15 = idle) in level L of a period, and the rows whose
+// pair belongs to sweep s (the period's tail; the others are sweep s + 1's, its head)
+constexpr int SV_P[6][8] = {
+    { 1, 0, 5, 4, 3, 2, 15, 15 },        // (0,1)h (2,5)t (3,4)t
+    { 2, 15, 0, 5, 15, 3, 15, 15 },      // (0,2)h (3,5)t
+    { 3, 2, 1, 0, 5, 4, 15, 15 },        // (0,3)h (1,2)h (4,5)t   -- sweep s complete
+    { 4, 3, 15, 1, 0, 15, 15, 15 },      // (0,4)h (1,3)h
+    { 5, 4, 3, 2, 1, 0, 15, 15 },        // (0,5)h (1,4)h (2,3)h
+    { 15, 5, 4, 15, 2, 1, 15, 15 },      // (1,5)h (2,4)h
+};
+constexpr unsigned SV_TAIL_ROWS[6] = { 0x3cu, 0x28u, 0x30u, 0u, 0u, 0u };
+constexpr unsigned sv_pack(int L)
+{
+    unsigned v = 0;
+    for (int r = 0; r < 8; ++r) v |= (unsigned)SV_P[L][r] << (4 * r);
+    return v;
+}
+constexpr unsigned long long sv_row_lanes(unsigned rows)
+{
+    unsigned long long m = 0;
+    for (int r = 0; r < 8; ++r)
+        if ((rows >> r) & 1u) m |= 0xffull << (8 * r);
+    return m;
+}
+
+template <int CTRL>
+__device__ __forceinline__ double icp_dpp_d(double v)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xf, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ float icp_bperm_f(int src_lane, float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_lane << 2, __builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ double icp_bperm_d(int src_lane, double v)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(unsigned)u);
+    const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(unsigned)(u >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// sum over the row's columns k = 0..5 of q, in order (0 + q0 + q1 + ... + q5, as the serial
+// loops add), returned to every lane of the row: q1..q5 reach lane 0 of the 8-lane group by DPP
+// row_shl (within a 16-lane DPP row both groups' lanes 0 read in range), the sum is broadcast
+// back by row_newbcast:0 / :8
+__device__ __forceinline__ double icp_sv_rowsum(double q, int lane)
+{
+    const double q1 = icp_dpp_d<0x101>(q), q2 = icp_dpp_d<0x102>(q), q3 = icp_dpp_d<0x103>(q);
+    const double q4 = icp_dpp_d<0x104>(q), q5 = icp_dpp_d<0x105>(q);
+    double s = 0.0 + q;
+    s = s + q1;
+    s = s + q2;
+    s = s + q3;
+    s = s + q4;
+    s = s + q5;
+    const double b0 = icp_dpp_d<0x150>(s), b8 = icp_dpp_d<0x158>(s);
+    return (lane & 8) ? b8 : b0;
+}
+
+// RN_f(t) == RN_f(v) for every t within the fast sequence's error of v?  The 29 bits a float
+// drops from a double's mantissa must stay more than SV_MARGIN double ulps (2^-37 of a mantissa
+// in [1, 2), relative) from the midpoint pattern, and v must be a normal float.
+#define SV_MARGIN (1u << 16)
+__device__ __forceinline__ bool icp_sv_round_safe(double v)
+{
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned low = (unsigned)b & 0x1fffffffu;
+    const unsigned d = low > 0x10000000u ? low - 0x10000000u : 0x10000000u - low;
+    const unsigned e = (unsigned)(b >> 52) & 0x7ffu;            // biased exponent (sign dropped)
+    return (d > SV_MARGIN) & (e - (1023u - 125u) <= 251u);      // 2^-125 <= |v| < 2^127
+}
+// (c, s) of a rotation, the serial form's sequence (p already doubled, A = W[I], B = W[J])
+__device__ __forceinline__ void icp_sv_cs_exact(double p, double A, double B, float& c, float& s)
+{
+    const double beta = A - B, gamma = icp_cv_hypot(p, beta);
+    if (beta < 0) {
+        const double delta = (gamma - beta) * 0.5;
+        s = (float)sqrt(delta / gamma);
+        c = (float)(p / (gamma * s * 2));
+    } else {
+        c = (float)sqrt((gamma + beta) / (gamma * 2));
+        s = (float)(p / (gamma * c * 2));
+    }
+}
+// The same (c, s) by a short sequence.  Both branches of the serial form compute
+// u = RN_f(sqrt((gamma + |beta|) / (2 gamma))) and v = RN_f(p / (gamma u 2)), (c, s) = (u, v) or
+// (v, u) by the sign of beta.  gamma and 1 / (2 gamma) come from v_rsq_f64 and one Goldschmidt
+// step, u from v_rsq_f64 and one step, 1 / u from v_rcp_f64 and one Newton step; the relative
+// error of U and V against the exact sequence's doubles stays far below the margin
+// icp_sv_round_safe demands, so where both pass the check, (c, s) are the exact
+// sequence's.  Lanes that rotate and fail it take icp_sv_cs_exact (uniform branch).
+__device__ __forceinline__ void icp_sv_cs(double p, double A, double B, bool rot, float& c, float& s)
+{
+    const double beta = A - B;
+    const double X = fma(p, p, beta * beta);
+    const double y = __builtin_amdgcn_rsq(X);
+    double g = X * y, h = 0.5 * y;
+    const double r1 = fma(-g, h, 0.5);
+    g = fma(g, r1, g);
+    h = fma(h, r1, h);
+    const double q = (g + fabs(beta)) * h;
+    const double y2 = __builtin_amdgcn_rsq(q);
+    double U = q * y2;
+    const double h2 = 0.5 * y2, r2 = fma(-U, h2, 0.5);
+    U = fma(U, r2, U);
+    const float u = (float)U;
+    const double ud = u;
+    double z = __builtin_amdgcn_rcp(ud);
+    z = fma(fma(-ud, z, 1.0), z, z);
+    const double V = (p * h) * z;
+    const float v = (float)V;
+    const bool neg = beta < 0;
+    c = neg ? v : u;
+    s = neg ? u : v;
+    const bool bad = rot & !((int)icp_sv_round_safe(U) & (int)icp_sv_round_safe(V));     // (bitwise: no exec branches)
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+#ifdef TF_SV_STATS                                // (tools/micro/svd_lanes.hip: levels that fell back)
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_sv_stats[1], 1ull);
+#endif
+        float ce, se;
+        icp_sv_cs_exact(p, A, B, ce, se);
+        if (bad) { c = ce; s = se; }
+    }
+}
+
+// the serial form's rotation test, !(|p| <= eps sqrt(a b)) with eps = 2 FLT_EPSILON = 2^-22, without
+// its square root: p^2 against 2^-44 a b, decided there unless the two are within 2^-40
+// (relative) of each other -- then |p| and 2^-22 RN(sqrt(RN(a b))) are within 2^-41 and the exact
+// test runs (a wave-uniform branch).  p = 0 or ab = 0 decide exactly as the serial test does; a NaN
+// fails both comparisons and takes the exact test.
+__device__ __forceinline__ bool icp_sv_test(bool active, double p, double ab)
+{
+    const double p2 = p * p, t = ab * 5.684341886080802e-14;           // 2^-44 a b
+    const bool skip = p2 <= t * (1.0 - 9.094947017729282e-13);         // certainly |p| <= eps sqrt(ab)
+    const bool rot = !skip & (p2 >= t * (1.0 + 9.094947017729282e-13)); // certainly not (p = ab = 0: skip)
+    bool res = active & rot;
+    const bool unsure = active & !skip & !rot;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(unsure) != 0, 0)) {
+        if (unsure) res = !(fabs(p) <= (double)(TF_FLT_EPS * 2) * sqrt(ab));
+    }
+    return res;
+}
+
+// one level of a period: every row with a partner in an enabled sweep rotates with it
+template <int L>
+__device__ __forceinline__ void icp_sv_level(float& a, float& v, double& w, int lane, int r, bool tail_on,
+                                             bool head_on, bool& ch_tail, bool& ch_head)
+{
+    constexpr unsigned PK = sv_pack(L);
+    constexpr unsigned TR = SV_TAIL_ROWS[L];
+    constexpr unsigned long long TL = sv_row_lanes(TR);
+    const int P = (int)((PK >> (4 * r)) & 15u);
+    const bool tail = ((TR >> r) & 1u) != 0;
+    const bool active = P != 15 && (tail ? tail_on : head_on);
+    const int src = active ? 8 * P + (lane & 7) : lane;
+    const float xa = icp_bperm_f(src, a), xv = icp_bperm_f(src, v);
+    const double wp = icp_bperm_d(src, w);
+    // p = sum_k At[I][k] At[J][k] (exact double products, serial order); the lower row is I
+    const double p = icp_sv_rowsum((double)a * (double)xa, lane);
+    const bool lower = r < P;
+    const double A = lower ? w : wp, B = lower ? wp : w;
+    const bool rot = icp_sv_test(active, p, A * B);
+    float c, s;
+    icp_sv_cs(p * 2, A, B, rot, c, s);
+    // row I: c Ai + s Aj, Vi c + Vj s;  row J: -s Ai + c Aj, Vj c - Vi s (the same products and
+    // one addition each: a + b == b + a and x - y == x + (-y) bit for bit)
+    const float sc = lower ? s : -s;
+    const float na = c * a + sc * xa;
+    const float nv = v * c + xv * sc;
+    if (rot) { a = na; v = nv; }
+    w = icp_sv_rowsum((double)a * (double)a, lane);      // |row|^2 as the serial loop sums it
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(rot);
+#ifdef TF_SV_STATS                                // (tools/micro/svd_lanes.hip: rotations)
+    if (lane == 0) atomicAdd(&g_sv_stats[0], (unsigned long long)__builtin_popcountll(m & 0x0101010101010101ull) / 2);
+#endif
+    ch_tail = ch_tail || (m & TL) != 0;
+    ch_head = ch_head || (m & ~TL) != 0;
+}
+
+// tot: lane stride * q holds sum q of the system (StreamHelper layout, projective_icp.cpp:51-61);
+// x: the solution, uniform
+template <int ALG>
+__device__ __forceinline__ void icp_cv_solve_svd6_lanes(float tot, int stride, int lane, float (&x)[6])
+{
+    const int r = lane >> 3, k = lane & 7;
+    const bool valid = r < 6 && k < 6;
+    // At = transpose(A) = A (symmetric): element (r, k) is sum idx(min, max), idx(i, j) =
+    // i (15 - i) / 2 + j - i; b[k] = sum idx(k, 6)
+    const int lo = r < k ? r : k, hi = r < k ? k : r;
+    const int ia = valid ? ((lo * (15 - lo)) >> 1) + hi - lo : 0;
+    const int kb = k < 6 ? k : 0;
+    float a = icp_bperm_f(ia * stride, tot);
+    const float bk = icp_bperm_f((((kb * (15 - kb)) >> 1) + 6 - kb) * stride, tot);
+    if (!valid) a = 0.f;
+    float v = (valid && r == k) ? 1.f : 0.f;
+    double w = icp_sv_rowsum((double)a * (double)a, lane);
+    bool ch_tail = false, ch_head = false;
+#pragma unroll 1
+    for (int sw = -1; sw < 30; ++sw) {          // period: tail sweep sw, head sweep sw + 1 (max_iter 30)
+        const bool tail_on = sw >= 0, head_on = sw + 1 < 30;
+        icp_sv_level<0>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
+        icp_sv_level<1>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
+        icp_sv_level<2>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
+        if (sw >= 0 && (!ch_tail || sw == 29)) break;      // sweep sw done: the serial loop's exit
+        icp_sv_level<3>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
+        icp_sv_level<4>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
+        icp_sv_level<5>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
+        ch_tail = ch_head;
+        ch_head = false;
+    }
+    // ---- singular values, sorted descending (selection sort, strict <: the first maximum)
+    const double Wf = sqrt(w);
+    double Wu[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) Wu[i] = icp_rl_d(Wf, 8 * i);
+    bool zero = false;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) zero = zero || Wu[i] <= TF_FLT_MIN;
+    if (zero) {                                   // a zero singular value: the serial finish
+#ifdef TF_SV_STATS
+        if (lane == 0) atomicAdd(&g_sv_stats[2], 1ull);
+#endif
+        float At[6][6], Vt[6][6], bu[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) { At[i][j] = icp_rl_f(a, 8 * i + j); Vt[i][j] = icp_rl_f(v, 8 * i + j); }
+            bu[i] = icp_rl_f(bk, i);
+        }
+        icp_cv_svd_finish<ALG>(At, Vt, bu, x);
+        return;
+    }
+    unsigned perm = 0x543210u;                    // sorted position i <- row (perm >> 4 i) & 15
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        int j = i;
+        double wj = Wu[i];
+#pragma unroll
+        for (int kk = i + 1; kk < 6; kk++) if (wj < Wu[kk]) { j = kk; wj = Wu[kk]; }
+        j = __builtin_amdgcn_readfirstlane(j);
+        if (j != i) {
+#pragma unroll
+            for (int rr = i + 1; rr < 6; ++rr)
+                if (rr == j) {
+                    const double t = Wu[i]; Wu[i] = Wu[rr]; Wu[rr] = t;
+                    const unsigned pi = (perm >> (4 * i)) & 15u, pr = (perm >> (4 * rr)) & 15u;
+                    perm = (perm & ~((15u << (4 * i)) | (15u << (4 * rr)))) | (pr << (4 * i)) | (pi << (4 * rr));
+                }
+        }
+    }
+    const int sl = r < 6 ? 8 * (int)((perm >> (4 * r)) & 15u) + k : lane;
+    float as = icp_bperm_f(sl, a);
+    const float vs = icp_bperm_f(sl, v);
+    const double sd = icp_bperm_d(sl, Wf);        // W[r] after the sort
+    as *= (float)(1 / sd);                        // the row normalised
+    // ---- SVBkSbImpl_<float>: threshold = (sum of the float w[i], in order) * (float)(2 DBL_EPSILON)
+    double thr = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) thr += (float)Wu[i];
+    thr *= (double)(float)(2.220446049250313e-16 * 2);
+    const float wfl = (float)sd;
+    const bool live = !((double)fabs(wfl) <= thr);
+    double si = icp_sv_rowsum((double)(as * bk), lane);   // float products, double sum in order
+    double wi = wfl;
+    wi = 1 / wi;
+    si *= wi;
+    const double term = si * (double)vs;          // s * Vt[i][j]
+    const unsigned long long lm = __builtin_amdgcn_ballot_w64(live && k == 0);
+    double ti[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) ti[i] = icp_bperm_d(8 * i + k, term);
+    float xj = 0.f;                               // lane (0, j): x[j] over the rows in order
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+        if ((lm >> (8 * i)) & 1ull) xj = (float)((double)xj + ti[i]);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) x[j] = icp_rl_f(xj, j);
 }
 
 // cv::Affine3f(rvec, t)'s rotation: Affine3<float>::rotation(const Vec3f&) (affine.hpp), every
@@ -559,17 +897,6 @@ __device__ __forceinline__ void icp_cv_rodrigues(const float* rv, float* R)
 // sum {0, 7, 13, 18, 22, 25}[r] + c - r, bv[r] is Am[r][6]
 template <typename T>
 __device__ __forceinline__ T icp_sel3(int i, T a, T b, T c) { return i == 0 ? a : (i == 1 ? b : c); }
-__device__ __forceinline__ double icp_rl_d(double v, int src)
-{
-    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, src);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), src);
-    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ float icp_rl_f(float v, int src)
-{
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
-}
 // sm: the 27 sums (uniform); aff: the current affine (uniform); i: the lane (rows 0-2 used);
 // xs: 9 doubles of wave-private LDS.  Out: orow = row i of Tinc * aff, rv = the increment (uniform)
 __device__ __forceinline__ void icp_tail_rows(const float (&sm)[27], const float (&aff)[12], int i, double* xs,
@@ -719,7 +1046,7 @@ __device__ __forceinline__ void icp_solve_rodrigues(const float (&Am)[6][6], con
 #endif
         icp_rodrigues(rv, R);
     } else {
-        icp_cv_solve_svd6(Am, bv, rv);
+        icp_cv_solve_svd6<ALG>(Am, bv, rv);
         icp_cv_rodrigues<ALG>(rv, R);
     }
 }
