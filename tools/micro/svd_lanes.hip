@@ -12,6 +12,9 @@
 #ifdef TF_SV_STATS                               // (the svd_lanes_stats build: counts, not timing)
 __device__ unsigned long long g_sv_stats[4];     // rotations, fast-path fallback levels, zero-SV finishes
 #endif
+#ifdef TF_SV_TIMING                              // (the svd_lanes_timing build: cycles per level phase)
+__device__ long long g_sv_t[8];
+#endif
 #include "../../topfusion_amd/csrc/tf_icp_tail.h"
 
 extern "C" void tfo_cv_solve_svd6(const float A[36], const float b[6], float x[6]);
@@ -167,10 +170,27 @@ int main(int argc, char** argv)
     const int N = 2000, ns = ncap > 0 ? (ncap < 256 ? ncap : 256) : 256;
     hipLaunchKernelGGL(k_time<0>, dim3(1), dim3(64), 0, 0, dS, ns, 20, dC, dO);
     hipLaunchKernelGGL(k_time<0>, dim3(1), dim3(64), 0, 0, dS, ns, N, dC, dO);
+#ifdef TF_SV_TIMING
+    {
+        long long z8[8] = {};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_sv_t), z8, sizeof(z8));       // (the check kernels' stamps dropped)
+    }
+#endif
     hipLaunchKernelGGL(k_time<1>, dim3(1), dim3(64), 0, 0, dS, ns, 20, dC, dO);
     hipLaunchKernelGGL(k_time<1>, dim3(1), dim3(64), 0, 0, dS, ns, N, dC, dO);
     long long c[2];
     hipMemcpy(c, dC, sizeof(c), hipMemcpyDeviceToHost);
+#ifdef TF_SV_TIMING
+    {
+        long long t[8];
+        hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sv_t), sizeof(t));
+        const char* nm[8] = { "previous level end -> level start", "partner bpermute", "sums (DPP gather + fma)",
+                              "test + ballot", "(c, s) chain + checks", "broadcast + update",
+                              "after the sweeps: |row|, sort, gather", "normalise + back substitution" };
+        printf("per-phase cycles per solve (timing build, stamps included):\n");
+        for (int k = 0; k < 8; ++k) printf("  %-36s %9.1f\n", nm[k], (double)t[k] / (N + 20));
+    }
+#endif
     printf("latency over the first %d systems, one wave, dependent solves (s_memtime cycles per solve):\n", ns);
     printf("  serial  icp_cv_solve_svd6        %9.1f\n", (double)c[0] / N);
     printf("  lanes   icp_cv_solve_svd6_lanes  %9.1f   (%.2fx)\n", (double)c[1] / N, (double)c[0] / (double)c[1]);

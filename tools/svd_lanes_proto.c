@@ -91,19 +91,17 @@ static void cs_fast(double p, double a, double b, float* c, float* s)
     const double beta = a - b;
     const double X = fma(p, p, beta * beta);
     const double y = rsq_a(X);
-    double g = X * y, h = 0.5 * y;
-    const double r = fma(-g, h, 0.5);
-    g = fma(g, r, g); h = fma(h, r, h);
-    const double x1 = g + fabs(beta);
-    const double q = x1 * h;
+    const double e = fma(-(X * y), y, 1.0);
+    const double h = fma(0.25 * y, e, 0.5 * y);
+    const double q = fma(fabs(beta), h, 0.5);
     const double y2 = rsq_a(q);
     double U = q * y2;
     const double h2 = 0.5 * y2, r2 = fma(-U, h2, 0.5);
     U = fma(U, r2, U);
+    const double z0 = 2.0 * fma(h2, r2, h2);
     const float u = (float)U;
     const double ud = u;
-    double z = rcp_a(ud);
-    z = fma(fma(-ud, z, 1.0), z, z);
+    const double z = fma(fma(-ud, z0, 1.0), z0, z0);
     const double V = (p * h) * z;
     const float v = (float)V;
     if (!(safe_f(U) && safe_f(V))) {

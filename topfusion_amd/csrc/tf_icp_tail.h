@@ -586,6 +586,48 @@ constexpr unsigned long long sv_row_lanes(unsigned rows)
     return m;
 }
 
+// lanes of the rows that are the lower row (I) of their pair in level L; lane 0 of each row whose
+// pair is enabled (tail pairs when sweep s exists, head pairs when sweep s + 1 does)
+constexpr unsigned long long sv_lower_lanes(int L)
+{
+    unsigned long long m = 0;
+    for (int r = 0; r < 6; ++r)
+        if (SV_P[L][r] != 15 && r < SV_P[L][r]) m |= 0xffull << (8 * r);
+    return m;
+}
+constexpr unsigned long long sv_act_base(int L, bool tail_on, bool head_on)
+{
+    unsigned long long m = 0;
+    for (int r = 0; r < 6; ++r) {
+        const bool tail = ((SV_TAIL_ROWS[L] >> r) & 1u) != 0;
+        if (SV_P[L][r] != 15 && (tail ? tail_on : head_on)) m |= 1ull << (8 * r);
+    }
+    return m;
+}
+// per lane: bit `lane` of the wave-uniform mask selects t, else f (one v_cndmask_b32)
+__device__ __forceinline__ float icp_lsel(unsigned long long mask, float t, float f)
+{
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(mask));
+    return r;
+}
+__device__ __forceinline__ double icp_lsel_d(unsigned long long mask, double t, double f)
+{
+    const unsigned long long ut = __builtin_bit_cast(unsigned long long, t), uf = __builtin_bit_cast(unsigned long long, f);
+    const unsigned lo = __builtin_bit_cast(unsigned, icp_lsel(mask, __builtin_bit_cast(float, (unsigned)ut),
+                                                              __builtin_bit_cast(float, (unsigned)uf)));
+    const unsigned hi = __builtin_bit_cast(unsigned, icp_lsel(mask, __builtin_bit_cast(float, (unsigned)(ut >> 32)),
+                                                              __builtin_bit_cast(float, (unsigned)(uf >> 32))));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+// each set bit at a row's lane 0 spread over the row's 8 lanes
+__device__ __forceinline__ unsigned long long icp_sv_spread(unsigned long long m)
+{
+    m |= m << 1;
+    m |= m << 2;
+    return m | (m << 4);
+}
+
 template <int CTRL>
 __device__ __forceinline__ double icp_dpp_d(double v)
 {
@@ -625,20 +667,22 @@ __device__ __forceinline__ double icp_sv_rowsum(double q, int lane)
 
 // RN_f(t) == RN_f(v) for every t within the fast sequence's error of v?  The 29 bits a float
 // drops from a double's mantissa must stay more than SV_MARGIN double ulps (2^-37 of a mantissa
-// in [1, 2), relative) from the midpoint pattern, and v must be a normal float.
+// in [1, 2), relative) from the midpoint pattern (one add and one unsigned compare), and, where
+// the value's range does not already guarantee it (full = true), v must be a normal float.
 #define SV_MARGIN (1u << 16)
+template <bool full>
 __device__ __forceinline__ bool icp_sv_round_safe(double v)
 {
     const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
-    const unsigned low = (unsigned)b & 0x1fffffffu;
-    const unsigned d = low > 0x10000000u ? low - 0x10000000u : 0x10000000u - low;
+    const bool clear = (((unsigned)b & 0x1fffffffu) - (0x10000000u - SV_MARGIN)) > 2u * SV_MARGIN;
+    if constexpr (!full) return clear;
     const unsigned e = (unsigned)(b >> 52) & 0x7ffu;            // biased exponent (sign dropped)
-    return (d > SV_MARGIN) & (e - (1023u - 125u) <= 251u);      // 2^-125 <= |v| < 2^127
+    return clear & (e - (1023u - 125u) <= 251u);                 // 2^-125 <= |v| < 2^127
 }
-// (c, s) of a rotation, the serial form's sequence (p already doubled, A = W[I], B = W[J])
-__device__ __forceinline__ void icp_sv_cs_exact(double p, double A, double B, float& c, float& s)
+// (c, s) of a rotation, the serial form's sequence (p already doubled, beta = W[I] - W[J])
+__device__ __forceinline__ void icp_sv_cs_exact(double p, double beta, float& c, float& s)
 {
-    const double beta = A - B, gamma = icp_cv_hypot(p, beta);
+    const double gamma = icp_cv_hypot(p, beta);
     if (beta < 0) {
         const double delta = (gamma - beta) * 0.5;
         s = (float)sqrt(delta / gamma);
@@ -650,94 +694,143 @@ __device__ __forceinline__ void icp_sv_cs_exact(double p, double A, double B, fl
 }
 // The same (c, s) by a short sequence.  Both branches of the serial form compute
 // u = RN_f(sqrt((gamma + |beta|) / (2 gamma))) and v = RN_f(p / (gamma u 2)), (c, s) = (u, v) or
-// (v, u) by the sign of beta.  gamma and 1 / (2 gamma) come from v_rsq_f64 and one Goldschmidt
-// step, u from v_rsq_f64 and one step, 1 / u from v_rcp_f64 and one Newton step; the relative
-// error of U and V against the exact sequence's doubles stays far below the margin
-// icp_sv_round_safe demands, so where both pass the check, (c, s) are the exact
-// sequence's.  Lanes that rotate and fail it take icp_sv_cs_exact (uniform branch).
-__device__ __forceinline__ void icp_sv_cs(double p, double A, double B, bool rot, float& c, float& s)
+// (v, u) by the sign of beta, gamma = hypot(p, beta).  Here h ~ 1 / (2 gamma) from v_rsq_f64 and
+// one Newton step, q = 1/2 + |beta| h ~ (gamma + |beta|) / (2 gamma), U ~ sqrt(q) from v_rsq_f64
+// and one Goldschmidt step (which also refines 1 / (2 U)), 1 / u from that by one Newton step
+// on the rounded u, V = p h / u.  v_rsq_f64 is within 2^-24.2 (relative; all inputs checked,
+// profiles/r06/f64_approx.txt), so U and V are within ~2^-47 of the exact sequence's doubles,
+// 2^10 below the margin icp_sv_round_safe demands: where both pass it, (c, s)
+// are the exact sequence's.  Rotating lanes that fail take icp_sv_cs_exact (uniform branch).
+__device__ __forceinline__ void icp_sv_cs(double p, double beta, unsigned long long m, float& c, float& s)
 {
-    const double beta = A - B;
     const double X = fma(p, p, beta * beta);
     const double y = __builtin_amdgcn_rsq(X);
-    double g = X * y, h = 0.5 * y;
-    const double r1 = fma(-g, h, 0.5);
-    g = fma(g, r1, g);
-    h = fma(h, r1, h);
-    const double q = (g + fabs(beta)) * h;
+    const double e = fma(-(X * y), y, 1.0);
+    const double h = fma(0.25 * y, e, 0.5 * y);                 // 1 / (2 gamma)
+    const double q = fma(fabs(beta), h, 0.5);
     const double y2 = __builtin_amdgcn_rsq(q);
     double U = q * y2;
     const double h2 = 0.5 * y2, r2 = fma(-U, h2, 0.5);
     U = fma(U, r2, U);
+    const double z0 = 2.0 * fma(h2, r2, h2);                   // 1 / U
     const float u = (float)U;
     const double ud = u;
-    double z = __builtin_amdgcn_rcp(ud);
-    z = fma(fma(-ud, z, 1.0), z, z);
+    const double z = fma(fma(-ud, z0, 1.0), z0, z0);           // 1 / u
     const double V = (p * h) * z;
     const float v = (float)V;
     const bool neg = beta < 0;
     c = neg ? v : u;
     s = neg ? u : v;
-    const bool bad = rot & !((int)icp_sv_round_safe(U) & (int)icp_sv_round_safe(V));     // (bitwise: no exec branches)
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+    const unsigned long long bad =
+        m & ~__builtin_amdgcn_ballot_w64((int)icp_sv_round_safe<false>(U) & (int)icp_sv_round_safe<true>(V));
+    if (__builtin_expect(bad != 0, 0)) {
 #ifdef TF_SV_STATS                                // (tools/micro/svd_lanes.hip: levels that fell back)
         if ((threadIdx.x & 63) == 0) atomicAdd(&g_sv_stats[1], 1ull);
 #endif
         float ce, se;
-        icp_sv_cs_exact(p, A, B, ce, se);
-        if (bad) { c = ce; s = se; }
+        icp_sv_cs_exact(p, beta, ce, se);
+        c = icp_lsel(bad, ce, c);
+        s = icp_lsel(bad, se, s);
     }
 }
 
 // the serial form's rotation test, !(|p| <= eps sqrt(a b)) with eps = 2 FLT_EPSILON = 2^-22, without
-// its square root: p^2 against 2^-44 a b, decided there unless the two are within 2^-40
-// (relative) of each other -- then |p| and 2^-22 RN(sqrt(RN(a b))) are within 2^-41 and the exact
-// test runs (a wave-uniform branch).  p = 0 or ab = 0 decide exactly as the serial test does; a NaN
-// fails both comparisons and takes the exact test.
-__device__ __forceinline__ bool icp_sv_test(bool active, double p, double ab)
+// its square root: p^2 against 2^-44 ab (1 -+ 2^-40), decided there unless p^2 falls between the
+// two -- then |p| and 2^-22 RN(sqrt(RN(ab))) are within 2^-41 and the exact test runs (a rare
+// wave-uniform branch).  p = 0 or ab = 0 decide as the serial test does (skip, unless p != 0 =
+// ab); a NaN fails both comparisons and takes the exact test.  act: the lanes that test; the
+// result is the mask of those that rotate.
+__device__ __forceinline__ unsigned long long icp_sv_test(unsigned long long act, double p, double ab)
 {
-    const double p2 = p * p, t = ab * 5.684341886080802e-14;           // 2^-44 a b
-    const bool skip = p2 <= t * (1.0 - 9.094947017729282e-13);         // certainly |p| <= eps sqrt(ab)
-    const bool rot = !skip & (p2 >= t * (1.0 + 9.094947017729282e-13)); // certainly not (p = ab = 0: skip)
-    bool res = active & rot;
-    const bool unsure = active & !skip & !rot;
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(unsure) != 0, 0)) {
-        if (unsure) res = !(fabs(p) <= (double)(TF_FLT_EPS * 2) * sqrt(ab));
-    }
-    return res;
+    const double p2 = p * p;
+    const unsigned long long skip = __builtin_amdgcn_ballot_w64(p2 <= ab * 5.6843418860756883e-14);  // 2^-44 (1 - 2^-40)
+    const unsigned long long rot = __builtin_amdgcn_ballot_w64(p2 >= ab * 5.6843418860860254e-14);   // 2^-44 (1 + 2^-40)
+    unsigned long long m = act & rot & ~skip;
+    const unsigned long long unsure = act & ~rot & ~skip;
+    if (__builtin_expect(unsure != 0, 0))
+        m |= unsure & __builtin_amdgcn_ballot_w64(!(fabs(p) <= (double)(TF_FLT_EPS * 2) * sqrt(ab)));
+    return m;
 }
 
-// one level of a period: every row with a partner in an enabled sweep rotates with it
-template <int L>
-__device__ __forceinline__ void icp_sv_level(float& a, float& v, double& w, int lane, int r, bool tail_on,
-                                             bool head_on, bool& ch_tail, bool& ch_head)
+template <int CTRL>
+__device__ __forceinline__ float icp_dpp_f(float v)
 {
-    constexpr unsigned PK = sv_pack(L);
-    constexpr unsigned TR = SV_TAIL_ROWS[L];
-    constexpr unsigned long long TL = sv_row_lanes(TR);
-    const int P = (int)((PK >> (4 * r)) & 15u);
-    const bool tail = ((TR >> r) & 1u) != 0;
-    const bool active = P != 15 && (tail ? tail_on : head_on);
-    const int src = active ? 8 * P + (lane & 7) : lane;
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+// lane 0 of the lane's 8-lane row group (DPP row_newbcast:0 / :8)
+__device__ __forceinline__ float icp_row_bcast(float v, int lane)
+{
+    const float b0 = icp_dpp_f<0x150>(v), b8 = icp_dpp_f<0x158>(v);
+    return (lane & 8) ? b8 : b0;
+}
+
+#ifdef TF_SV_TIMING                               // (tools/micro/svd_lanes.hip timing build only)
+// a stamp after a value: its phase's cycles since the previous stamp accumulate in registers
+// (SvTimes), written to g_sv_t at the end of the solve
+struct SvTimes { long long t0, acc[8]; };
+#define SV_TPARAM , SvTimes& svt
+#define SV_TARG , svt
+#define SV_T(k, val_) do { const float d_ = (float)(val_); asm volatile("; sv dep %0" :: "v"(d_)); \
+    __builtin_amdgcn_sched_barrier(0); const long long t_ = (long long)__builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0); svt.acc[k] += t_ - svt.t0; svt.t0 = t_; } while (0)
+#else
+#define SV_TPARAM
+#define SV_TARG
+#define SV_T(k, val_) do { } while (0)
+#endif
+// one level of a period: every row with a partner in an enabled sweep rotates with it.  Lane 0
+// of each row group gathers its row and the partner row (DPP row_shl) and forms the three sums the
+// rotation needs in the serial order -- p = sum_k At[I][k] At[J][k] and both |row|^2, exact double
+// products added in order (as fma: the products are exact) -- then the test and (c, s); the row's
+// lanes apply (c, s) to their element.  src: the lane holding this lane's element of the partner
+// row (own lane when the row is idle); which pairs are enabled is a template argument.
+template <int L, bool TAIL_ON, bool HEAD_ON>
+__device__ __forceinline__ void icp_sv_level(float& a, float& v, int lane, int src, bool& ch_tail, bool& ch_head SV_TPARAM)
+{
+    constexpr unsigned long long ACT = sv_act_base(L, TAIL_ON, HEAD_ON);
+    constexpr unsigned long long LOW = sv_lower_lanes(L);
+    constexpr unsigned long long TL = sv_row_lanes(SV_TAIL_ROWS[L]);
+    if constexpr (ACT == 0) return;
+    SV_T(0, a);
     const float xa = icp_bperm_f(src, a), xv = icp_bperm_f(src, v);
-    const double wp = icp_bperm_d(src, w);
-    // p = sum_k At[I][k] At[J][k] (exact double products, serial order); the lower row is I
-    const double p = icp_sv_rowsum((double)a * (double)xa, lane);
-    const bool lower = r < P;
-    const double A = lower ? w : wp, B = lower ? wp : w;
-    const bool rot = icp_sv_test(active, p, A * B);
-    float c, s;
-    icp_sv_cs(p * 2, A, B, rot, c, s);
-    // row I: c Ai + s Aj, Vi c + Vj s;  row J: -s Ai + c Aj, Vj c - Vi s (the same products and
-    // one addition each: a + b == b + a and x - y == x + (-y) bit for bit)
-    const float sc = lower ? s : -s;
-    const float na = c * a + sc * xa;
-    const float nv = v * c + xv * sc;
-    if (rot) { a = na; v = nv; }
-    w = icp_sv_rowsum((double)a * (double)a, lane);      // |row|^2 as the serial loop sums it
-    const unsigned long long m = __builtin_amdgcn_ballot_w64(rot);
+    const float a1 = icp_dpp_f<0x101>(a), a2 = icp_dpp_f<0x102>(a), a3 = icp_dpp_f<0x103>(a);
+    const float a4 = icp_dpp_f<0x104>(a), a5 = icp_dpp_f<0x105>(a);
+    const double d0 = a, d1 = a1, d2 = a2, d3 = a3, d4 = a4, d5 = a5;
+    double wo = fma(d0, d0, 0.0);
+    wo = fma(d1, d1, wo); wo = fma(d2, d2, wo); wo = fma(d3, d3, wo); wo = fma(d4, d4, wo); wo = fma(d5, d5, wo);
+    SV_T(1, xa);
+    const float x1 = icp_dpp_f<0x101>(xa), x2 = icp_dpp_f<0x102>(xa), x3 = icp_dpp_f<0x103>(xa);
+    const float x4 = icp_dpp_f<0x104>(xa), x5 = icp_dpp_f<0x105>(xa);
+    const double e0 = xa, e1 = x1, e2 = x2, e3 = x3, e4 = x4, e5 = x5;
+    double wq = fma(e0, e0, 0.0), p = fma(d0, e0, 0.0);
+    wq = fma(e1, e1, wq); p = fma(d1, e1, p);
+    wq = fma(e2, e2, wq); p = fma(d2, e2, p);
+    wq = fma(e3, e3, wq); p = fma(d3, e3, p);
+    wq = fma(e4, e4, wq); p = fma(d4, e4, p);
+    wq = fma(e5, e5, wq); p = fma(d5, e5, p);
+    SV_T(2, p + wo + wq);
+    // beta = W[I] - W[J] on both rows' lanes (RN(y - x) = -RN(x - y)); ab = W[I] W[J]
+    const double dw = wo - wq;
+    const double beta = icp_lsel_d(LOW, dw, -dw);
+    const unsigned long long m = icp_sv_test(ACT, p, wo * wq);      // bits at the rotating rows' lanes 0
+    SV_T(3, (float)m);
+    if (m != 0) {                                               // (uniform: otherwise nothing changes)
+        float c, s;
+        icp_sv_cs(p * 2, beta, m, c, s);
+        SV_T(4, c + s);
+        const float cb = icp_row_bcast(c, lane), sb = icp_row_bcast(s, lane);
+        // row I: c Ai + s Aj, Vi c + Vj s;  row J: -s Ai + c Aj, Vj c - Vi s (the same products and
+        // one addition each: a + b == b + a and x - y == x + (-y) bit for bit)
+        const float sc = icp_lsel(LOW, sb, -sb);
+        const float na = cb * a + sc * xa;
+        const float nv = v * cb + xv * sc;
+        const unsigned long long mr = icp_sv_spread(m);
+        a = icp_lsel(mr, na, a);
+        v = icp_lsel(mr, nv, v);
+        SV_T(5, a + v);
+    }
 #ifdef TF_SV_STATS                                // (tools/micro/svd_lanes.hip: rotations)
-    if (lane == 0) atomicAdd(&g_sv_stats[0], (unsigned long long)__builtin_popcountll(m & 0x0101010101010101ull) / 2);
+    if (lane == 0) atomicAdd(&g_sv_stats[0], (unsigned long long)__builtin_popcountll(m) / 2);
 #endif
     ch_tail = ch_tail || (m & TL) != 0;
     ch_head = ch_head || (m & ~TL) != 0;
@@ -759,23 +852,47 @@ __device__ __forceinline__ void icp_cv_solve_svd6_lanes(float tot, int stride, i
     const float bk = icp_bperm_f((((kb * (15 - kb)) >> 1) + 6 - kb) * stride, tot);
     if (!valid) a = 0.f;
     float v = (valid && r == k) ? 1.f : 0.f;
-    double w = icp_sv_rowsum((double)a * (double)a, lane);
+    // partner lane of this lane's element in each level (own lane on an idle row)
+    int src[6];
+#pragma unroll
+    for (int L = 0; L < 6; ++L) {
+        const int P = (int)((sv_pack(L) >> (4 * r)) & 15u);
+        src[L] = P != 15 ? 8 * P + k : lane;
+    }
     bool ch_tail = false, ch_head = false;
+#ifdef TF_SV_TIMING
+    SvTimes svt = {};
+    svt.t0 = (long long)__builtin_amdgcn_s_memtime();
+#endif
+    // period -1: sweep 0's first levels (no tail)
+    icp_sv_level<0, false, true>(a, v, lane, src[0], ch_tail, ch_head SV_TARG);
+    icp_sv_level<1, false, true>(a, v, lane, src[1], ch_tail, ch_head SV_TARG);
+    icp_sv_level<2, false, true>(a, v, lane, src[2], ch_tail, ch_head SV_TARG);
+    icp_sv_level<3, false, true>(a, v, lane, src[3], ch_tail, ch_head SV_TARG);
+    icp_sv_level<4, false, true>(a, v, lane, src[4], ch_tail, ch_head SV_TARG);
+    icp_sv_level<5, false, true>(a, v, lane, src[5], ch_tail, ch_head SV_TARG);
+    ch_tail = ch_head;
+    ch_head = false;
+    bool done = false;
 #pragma unroll 1
-    for (int sw = -1; sw < 30; ++sw) {          // period: tail sweep sw, head sweep sw + 1 (max_iter 30)
-        const bool tail_on = sw >= 0, head_on = sw + 1 < 30;
-        icp_sv_level<0>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
-        icp_sv_level<1>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
-        icp_sv_level<2>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
-        if (sw >= 0 && (!ch_tail || sw == 29)) break;      // sweep sw done: the serial loop's exit
-        icp_sv_level<3>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
-        icp_sv_level<4>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
-        icp_sv_level<5>(a, v, w, lane, r, tail_on, head_on, ch_tail, ch_head);
+    for (int sw = 0; sw < 29; ++sw) {           // period sw: tail sweep sw, head sweep sw + 1
+        icp_sv_level<0, true, true>(a, v, lane, src[0], ch_tail, ch_head SV_TARG);
+        icp_sv_level<1, true, true>(a, v, lane, src[1], ch_tail, ch_head SV_TARG);
+        icp_sv_level<2, true, true>(a, v, lane, src[2], ch_tail, ch_head SV_TARG);
+        if (!ch_tail) { done = true; break; }   // sweep sw changed nothing: the serial loop's exit
+        icp_sv_level<3, true, true>(a, v, lane, src[3], ch_tail, ch_head SV_TARG);
+        icp_sv_level<4, true, true>(a, v, lane, src[4], ch_tail, ch_head SV_TARG);
+        icp_sv_level<5, true, true>(a, v, lane, src[5], ch_tail, ch_head SV_TARG);
         ch_tail = ch_head;
         ch_head = false;
     }
+    if (!done) {                                // sweep 29, the last (max_iter = 30): its tail only
+        icp_sv_level<0, true, false>(a, v, lane, src[0], ch_tail, ch_head SV_TARG);
+        icp_sv_level<1, true, false>(a, v, lane, src[1], ch_tail, ch_head SV_TARG);
+        icp_sv_level<2, true, false>(a, v, lane, src[2], ch_tail, ch_head SV_TARG);
+    }
     // ---- singular values, sorted descending (selection sort, strict <: the first maximum)
-    const double Wf = sqrt(w);
+    const double Wf = sqrt(icp_sv_rowsum((double)a * (double)a, lane));
     double Wu[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) Wu[i] = icp_rl_d(Wf, 8 * i);
@@ -818,6 +935,7 @@ __device__ __forceinline__ void icp_cv_solve_svd6_lanes(float tot, int stride, i
     float as = icp_bperm_f(sl, a);
     const float vs = icp_bperm_f(sl, v);
     const double sd = icp_bperm_d(sl, Wf);        // W[r] after the sort
+    SV_T(6, as + vs + sd);
     as *= (float)(1 / sd);                        // the row normalised
     // ---- SVBkSbImpl_<float>: threshold = (sum of the float w[i], in order) * (float)(2 DBL_EPSILON)
     double thr = 0;
@@ -841,6 +959,11 @@ __device__ __forceinline__ void icp_cv_solve_svd6_lanes(float tot, int stride, i
         if ((lm >> (8 * i)) & 1ull) xj = (float)((double)xj + ti[i]);
 #pragma unroll
     for (int j = 0; j < 6; ++j) x[j] = icp_rl_f(xj, j);
+#ifdef TF_SV_TIMING
+    SV_T(7, x[0] + x[5]);
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) g_sv_t[q] += svt.acc[q];
+#endif
 }
 
 // cv::Affine3f(rvec, t)'s rotation: Affine3<float>::rotation(const Vec3f&) (affine.hpp), every
