@@ -88,9 +88,11 @@ def parse():
                          "(an event pair is a few us of dispatch gap; 1 = every frame)")
     ap.add_argument("--breakdown-frames", type=int, default=64, help="frames of the per-stage timing pass")
     ap.add_argument("--pose-algebra", choices=["canonical", "opencv4", "opencv2"], default=None,
-                    help="the ICP iterations' det / solve / Rodrigues (tf_set_pose_algebra): canonical (LDL^T + sinc "
-                         "Rodrigues) or the reference's OpenCV algebra (cv::solve DECOMP_SVD, Affine3f), 3.x-4.x / "
-                         "2.4.9; default: the library's (TFUSION_ICP_SOLVE)")
+                    help="the ICP iterations' det / solve / Rodrigues (tf_set_pose_algebra): the reference's OpenCV "
+                         "algebra (cv::determinant, cv::solve DECOMP_SVD, Affine3f), 3.x-4.x or 2.4.9, or canonical (LU "
+                         "+ 2 x 2 block Schur + sinc Rodrigues); default: the library's (opencv4; TFUSION_ICP_SOLVE)")
+    ap.add_argument("--no-other-algebra", action="store_true",
+                    help="skip the canonical-algebra pass reported beside an OpenCV-algebra headline")
     ap.add_argument("--collective", choices=["rccl", "file"], default="rccl",
                     help="N > 1: how the ranks combine their numbers -- RCCL all-reduces (default) or the host-side "
                          "file group (topfusion_amd/replicas.py)")
@@ -191,6 +193,22 @@ def cpu_run(frames, params_kw, first, n, omp, start=None):
     for k in range(first, first + n):
         o(frames[k])
     return time.perf_counter() - t0
+
+
+def pose_algebra_gap_summary():
+    """What the canonical algebra changes against the reference's (OpenCV 4) on the C2 frames, one
+    step at a time (both from the same state before every frame): the committed measurement
+    tools/pose_algebra_gap.py --one-step made (profiles/r05/pose_algebra_onestep_C2.json)."""
+    path = os.path.join(ROOT, "profiles", "r05", "pose_algebra_onestep_C2.json")
+    try:
+        d = json.load(open(path))["modes"]["opencv4_portable"]
+    except Exception:
+        return None
+    return {"frames": 800, "frames_pose_rel_diff_over_1e-4": d.get("frames_pose_rel_diff_over_1e-4"),
+            "pose_rel_diff_p50_p99_tracked": d.get("pose_rel_diff_p50_p99_tracked"),
+            "frames_alloc_differs": d.get("frames_alloc_differs"), "alloc_xor_mean": d.get("alloc_xor_mean"),
+            "reset_flips": d.get("reset_flips"), "frames_iteration_count_differs": d.get("frames_iteration_count_differs"),
+            "source": os.path.relpath(path, ROOT)}
 
 
 def cpu_baseline_protocol(frames, first, params_kw, seconds, nt, algebra=0):
@@ -477,7 +495,8 @@ def c5e_bench(args):
     # steps whose frames all come after the first failure: the saturated-VBA rate
     sat_steps = [i for i in range(steps) if first_fail is not None and (warm + i) * F >= first_fail]
     sat_s = sum(step_s[i] for i in sat_steps)
-    elapsed_max, total_frames, multi = rep.summary(elapsed, steps * F)
+    elapsed_max, total_frames, multi = rep.summary(elapsed, steps * F, identity=rank_identity(args, local_rank, rank),
+                                                   extra={"frames_failed_alloc": int((fails[warm * F:] > 0).sum())})
     if rank == 0:
         late = timed[-min(len(timed), 10 * F):]
         allocated = nb - 1 - rec["lastFreeBlockId"]
@@ -513,6 +532,7 @@ def c5e_bench(args):
             "multi_gpu": multi if world > 1 else None,
         }
         print(json.dumps(out))
+        check_distinct_devices(multi if world > 1 else None)
     tf.close()
     stream.free()
     rep.close()
@@ -539,6 +559,23 @@ def rank_setup(args):
     return rank, local_rank, world, rep
 
 
+def rank_identity(args, local_rank, rank):
+    """This rank's device (PCI bus id) for the multi-GPU fields; the stand-in's placeholder."""
+    from topfusion_amd import replicas
+    if args.standin:      # (TFUSION_STANDIN_SAME_DEVICE=1, tests: every rank claims one device)
+        return replicas.device_identity(0 if os.environ.get("TFUSION_STANDIN_SAME_DEVICE") == "1" else rank, standin=True)
+    return replicas.device_identity(local_rank)
+
+
+def check_distinct_devices(multi):
+    """An N-GPU line must come from N distinct devices: exit non-zero (after the line is printed)
+    when two ranks report the same bus id, unless the tests' several-ranks-per-device mode
+    (TFUSION_RANK_DEVICE_MODULO=1) asked for exactly that."""
+    if multi and not multi.get("distinct_devices", True) and os.environ.get("TFUSION_RANK_DEVICE_MODULO") != "1":
+        sys.stdout.flush()
+        sys.exit(f"bench.py: two ranks ran on the same device: {multi.get('per_rank_device')}")
+
+
 def standin(args):
     """CPU stand-in for the launcher tests: each rank runs the oracle (test infrastructure; never a
     measured GPU number) over a few frames of its own 80x60 orbit stream (seed 7 + rank), then
@@ -555,7 +592,8 @@ def standin(args):
     ok = sum(bool(o(f)) for f in frames)
     rep.barrier()
     elapsed = time.perf_counter() - t0
-    emax, total, multi = rep.summary(elapsed, n)
+    emax, total, multi = rep.summary(elapsed, n, identity=rank_identity(args, local_rank, rank),
+                                     extra={"frames_ok": ok})
     if rank == 0:
         print(json.dumps({"metric": "stand-in: oracle frames/sec @80x60 (launcher test, not a GPU number)",
                           "value": round(total / emax, 4), "unit": "frames/s", "n_gpus": world, "steps": n,
@@ -564,6 +602,7 @@ def standin(args):
                           "config": {"workload": "standin", "parallelism": f"replicas{world}"},
                           "frames_ok_rank0": ok, "frame_sum_rank0": int(frames.astype(np.int64).sum()),
                           "multi_gpu": multi}))
+        check_distinct_devices(multi)
     rep.close()
 
 
@@ -625,24 +664,37 @@ def main():
             return tfx.process_frames(base + k0 * frame_bytes, n)
         return tfx.process_frames(base + k0 * frame_bytes, n, rgb_frames=rgb.ptr + k0 * rgb_bytes, rgb_stride=rgb_bytes)
 
-    tf = TopFu(default_params(**pkw), device=local_rank)
-    single = [k for k in SINGLE_KERNEL_STAGES if k != "icp" or tf.icp_persistent()]
+    # per-stage breakdown first (outside the timed region, a context of its own): a fresh context
+    # replays the warm-up and the first frames of the timed region with every stage timed; the
+    # dominant single-kernel stage -- by measured time per full launch -- is the one the timed
+    # region times and the roofline names
+    prof = {}
+    lanes_bd = nvis_bd = None
+    tb = TopFu(default_params(**pkw), device=local_rank)
+    single = [k for k in SINGLE_KERNEL_STAGES if k != "icp" or tb.icp_persistent()]
+    dominant = "icp" if tb.icp_persistent() else "raycast_icp"
+    if n_breakdown:
+        run(tb, 0, args.warmup * F)
+        tb.profile(True)
+        tb.reset_totals()
+        run(tb, args.warmup * F, n_breakdown)
+        prof = tb.profile_read()
+        tbt = tb.totals()
+        n_int = max(1, tbt["frames"] - tbt["resets"])
+        lanes_bd = (tbt["integrate_lanes_read"] / n_int, tbt["integrate_lanes_written"] / n_int)
+        nvis_bd = tbt["visible_sum"] / n_int
+        avg = {k: prof[k][0] / prof[k][1] for k in single if prof[k][1]}
+        if avg:
+            dominant = max(avg, key=avg.get)
+    tb.close()
     device_sync()
-    # warm-up (whole steps: full enqueue groups), every stage timed: picks the dominant
-    # single-kernel stage
-    dominant = "icp" if tf.icp_persistent() else "raycast_icp"
-    if args.warmup > 0:
-        tf.profile(not args.no_profile)
-        for w in range(args.warmup):
-            run(tf, w * F, F)
-        if not args.no_profile:
-            pw = tf.profile_read()
-            avg = {k: pw[k][0] / pw[k][1] for k in single if pw[k][1]}
-            if avg:
-                dominant = max(avg, key=avg.get)
+
+    tf = TopFu(default_params(**pkw), device=local_rank)
+    device_sync()
+    for w in range(args.warmup):                      # warm-up: whole steps (full enqueue groups)
+        run(tf, w * F, F)
     # timed region: HIP events only around the dominant kernel's stage, on every
-    # --profile-every-th frame (an event pair costs a few us of dispatch gap; the full per-stage
-    # breakdown comes from a separate pass below)
+    # --profile-every-th frame (an event pair costs a few us of dispatch gap)
     tf.profile(not args.no_profile, stages=[dominant], every=args.profile_every)
     tf.reset_totals()
     device_sync()
@@ -663,23 +715,35 @@ def main():
     # context's by a stream event (tf_capi.hip icp_order_*), a dispatch gap no single user sees
     tf_params, tf_alg, tf_persistent = tf.params(), tf.pose_algebra(), tf.icp_persistent()
     tf.close()
-    prof = {}
-    lanes_bd = nvis_bd = None
-    if n_breakdown:
-        # per-stage breakdown: a fresh context replays the warm-up and the first frames of the
-        # timed region with every stage timed (outside the timed region)
-        tb = TopFu(default_params(**pkw), device=local_rank)
-        run(tb, 0, args.warmup * F)
-        tb.profile(True)
-        tb.reset_totals()
-        run(tb, args.warmup * F, n_breakdown)
-        prof = tb.profile_read()
-        tbt = tb.totals()
-        n_int = max(1, tbt["frames"] - tbt["resets"])
-        lanes_bd = (tbt["integrate_lanes_read"] / n_int, tbt["integrate_lanes_written"] / n_int)
-        nvis_bd = tbt["visible_sum"] / n_int
-        tb.close()
+
+    # the other algebra beside the headline one: the same frames, warm-up and timed steps through
+    # a fresh context under the canonical algebra (when the headline ran the reference's) -- wall
+    # clock, and the ICP's full launches timed as in the timed region
+    other = None
+    if rgb is None and tf_alg != 0 and not args.no_other_algebra:
+        tc = TopFu(default_params(**pkw), device=local_rank)
+        tc.set_pose_algebra("canonical")
         device_sync()
+        for w in range(args.warmup):
+            run(tc, w * F, F)
+        tc.profile(not args.no_profile, stages=["icp"], every=args.profile_every)
+        tc.reset_totals()
+        device_sync()
+        tcs = time.perf_counter()
+        okc = np.concatenate([run(tc, (args.warmup + k) * F, F) for k in range(args.steps)])
+        device_sync()
+        el_c = time.perf_counter() - tcs
+        pc = tc.profile_read() if not args.no_profile else {}
+        totc = tc.totals()
+        tc.close()
+        other = {"pose_algebra": "canonical", "frames_per_sec": round(args.steps * F / el_c, 2),
+                 "icp_ms_full_launch": round(pc["icp"][0] / pc["icp"][1], 5) if pc and pc["icp"][1] else None,
+                 "frames_ok": int(okc.sum()), "resets": int(totc["resets"]),
+                 "is": "the same frames, warm-up and timed steps on one GPU through a fresh context under the "
+                       "canonical algebra (LU + 2 x 2 block Schur solve + sinc Rodrigues; not the reference's "
+                       "arithmetic: its trajectory and allocated blocks differ from the reference's)",
+                 "one_step_gap": pose_algebra_gap_summary()}
+
     # TopFu::operator() per call (one call per frame, returning on the frame's verdict) over the first
     # frames of the timed region, from a fresh context, and the batched rate of a fresh context on
     # the same frames beside it (the orbit's cost per frame varies along it: compare like with like)
@@ -710,7 +774,9 @@ def main():
             t1.close()
         c1_gpu = 1000.0 * sorted(c1[1:])[2]
     total_steps_frames = args.steps * F
-    elapsed_max, total_frames, multi = rep.summary(elapsed, total_steps_frames)
+    elapsed_max, total_frames, multi = rep.summary(
+        elapsed, total_steps_frames, identity=rank_identity(args, local_rank, rank),
+        extra={"frames_ok": int(ok.sum()), "icp_fallbacks": int(tot["icp_fallbacks"]), "resets": int(tot["resets"])})
 
     if rank == 0:
         value = total_frames / elapsed_max
@@ -761,7 +827,8 @@ def main():
                 roof_all["icp"]["occupancy"] = occ
             if "icp" in roof_all:
                 roof_all["icp"]["limit"] = ("latency, not HBM: 19 dependent iterations, each rows -> two cross-CU "
-                                            "hand-offs -> the serial 6x6 solve (DESIGN.md 5); the previous-frame "
+                                            "hand-offs -> the 6x6 solve on one wave (the reference's algebra: the "
+                                            "lane-parallel Jacobi SVD, ~20 k cycles; DESIGN.md 5); the previous-frame "
                                             "gathers hit L2, so PMC traffic is a fraction of the algorithmic bytes")
         stream_gbs = round(hbm_stream_copy(), 1)
         cpu = None
@@ -846,10 +913,16 @@ def main():
             "roofline_stages": roof_all,
             "icp_schedule": "persistent" if tf_persistent else "per_iteration",
             "pose_algebra": {0: "canonical", 2: "opencv2", 4: "opencv4"}[tf_alg],
+            "pose_algebra_is": ("the reference's own (cv::determinant, cv::solve DECOMP_SVD, Affine3f as OpenCV "
+                                "3.x-4.x / 2.4.9 publish them; projective_icp.cpp:197-209), bit-exact against the oracle's "
+                                "restatement") if tf_alg else "canonical (not the reference's arithmetic)",
+            "other_algebra": other,
+            "icp_fallbacks": int(tot["icp_fallbacks"]),
             "cpu_baseline": cpu,
             "multi_gpu": multi if world > 1 else None,
         }
         print(json.dumps(out))
+        check_distinct_devices(multi if world > 1 else None)
     dev.free()
     if rgb is not None:
         rgb.free()

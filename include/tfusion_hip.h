@@ -205,7 +205,9 @@ tf_status tf_get_schedule(tf_ctx* ctx, int* icp_persistent);
  *     with float rounding of every Matx operation; not checked against an OpenCV build, none is
  *     available) -- the reference's algebra (see DESIGN.md §2 for what the two algebras do to a
  *     sequence).
- * The environment variable TFUSION_ICP_SOLVE=svd|opencv4|opencv2 sets it at tf_create.
+ * Default: TF_POSE_ALGEBRA_OPENCV4 (the reference's algebra; the persistent ICP runs its Jacobi SVD
+ * lane-parallel).  The environment variable TFUSION_ICP_SOLVE=opencv4|opencv2|canonical sets it
+ * at tf_create.
  * TF_INVALID_ARG if the algebra's persistent ICP kernel would not fit the schedule chosen. */
 enum { TF_POSE_ALGEBRA_CANONICAL = 0, TF_POSE_ALGEBRA_OPENCV2 = 2, TF_POSE_ALGEBRA_OPENCV4 = 4 };
 tf_status tf_set_pose_algebra(tf_ctx* ctx, int algebra);

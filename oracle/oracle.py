@@ -135,9 +135,10 @@ POSE_MODES = {"canonical": POSE_CANONICAL, "opencv2": POSE_OPENCV2, "opencv4": P
 
 def set_pose_algebra(mode, libm=False, omp=None):
     """Test-only: the pose algebra estimateTransform's iterations use (tf_oracle.c, "The
-    reference's own pose algebra"): "canonical" (LDL^T + sinc Rodrigues, the GPU default),
-    "opencv2" / "opencv4" (cv::determinant, cv::solve DECOMP_SVD and Affine3f(rvec, t) as OpenCV
-    2.4.9 / 3.x-4.x publish them), with glibc's (libm=True) or the portable sin / cos / hypot.
+    reference's own pose algebra"): "opencv4" (the default, as the GPU's) / "opencv2"
+    (cv::determinant, cv::solve DECOMP_SVD and Affine3f(rvec, t) as OpenCV 3.x-4.x / 2.4.9 publish
+    them, restated: not checked against an OpenCV build) or "canonical" (LU + block Schur + sinc
+    Rodrigues), with glibc's (libm=True) or the portable sin / cos / hypot.
     Applies to the serial and (omp=None) the OpenMP build alike."""
     m = POSE_MODES[mode] if isinstance(mode, str) else int(mode)
     for o in ((False, True) if omp is None else (omp,)):

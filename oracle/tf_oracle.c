@@ -572,7 +572,7 @@ static void solve6(const float Af[36], const float bf[6], float x[6])
 /* either glibc's (use_libm = 1: what a host build of the reference calls) or portable           */
 /* restatements the GPU can run bit for bit (use_libm = 0: tfo_sincos and cv_hypot below).       */
 /* ------------------------------------------------------------------------- */
-static int g_pose_algebra = TFO_POSE_CANONICAL, g_pose_libm = 0;
+static int g_pose_algebra = TFO_POSE_OPENCV4, g_pose_libm = 0;   /* the reference's own by default */
 void tfo_set_pose_algebra(int mode, int use_libm) { g_pose_algebra = mode; g_pose_libm = use_libm; }
 int tfo_get_pose_algebra(void) { return g_pose_algebra; }
 

@@ -50,6 +50,10 @@ def _check_line(d, world):
     for fps, e, f in zip(m["per_rank_frames_per_sec"], m["per_rank_elapsed_s"], m["per_rank_frames"]):
         assert fps == pytest.approx(f / e, rel=1e-2)
     assert "efficiency" not in json.dumps(d)         # the driver computes scaling itself
+    # the line proves itself: every rank's device (distinct) and its own frame verdicts
+    assert len(m["per_rank_device"]) == world and m["distinct_devices"] is True
+    assert len(set(m["per_rank_device"])) == world
+    assert len(m["per_rank_frames_ok"]) == world and all(0 <= v <= d["steps"] for v in m["per_rank_frames_ok"])
 
 
 def test_bench_launches_its_own_ranks():
@@ -72,6 +76,24 @@ def test_bench_under_torchrun():
                        cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     _check_line(_line(r.stdout), 2)
+
+
+def test_duplicate_device_exits_nonzero():
+    """Two ranks that report the same device: rank 0 prints the line (distinct_devices false, both
+    bus ids) and the job exits non-zero -- an N-GPU number must come from N GPUs."""
+    env = _env()
+    env["TFUSION_STANDIN_SAME_DEVICE"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--standin", "--steps", "2"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    d = _line(r.stdout)
+    assert d["multi_gpu"]["distinct_devices"] is False and "same device" in r.stderr
+
+
+def test_bus_id_format():
+    from topfusion_amd import replicas
+    v = replicas.parse_bus_id("0000:c1:00.0")
+    assert v == [0, 0xc1, 0, 0] and replicas.format_bus_id(v) == "0000:c1:00.0"
 
 
 def test_world_mismatch_exits_nonzero():

@@ -106,3 +106,46 @@ def test_vis_build_lost_wait_is_sticky_on_engine_path(monkeypatch):
     assert (rec["noVisibleEntries"] > 0).all()
     g.close()
     dev.free()
+
+
+def test_engine_batch_no_ops_after_lost_wait(monkeypatch):
+    """once an engine batch's k_vis_build wait fails (TFUSION_VIS_FAULT=2: frame 1 of
+    the batch), the rest of the batch changes nothing -- frame 1 integrates nothing over its
+    unbuilt list, and frames 2.. allocate nothing (their records show frame 1's free-list top,
+    where a clean context on the same frames allocates new blocks) -- and the next call returns
+    TF_HIP_ERROR without enqueuing anything.  The records are read through the C-ABI, which fills
+    them before it reports the error."""
+    import ctypes
+    from topfusion_amd import TopFu, default_params, _lib as L
+    fx, fy, cx, cy = synth.intrinsics(W, H)
+    n = 4
+    frames = np.stack([synth.room_corner(W, H, seed=42 + k) for k in range(n)])
+    dev = DeviceFrames(frames)
+    poses = np.tile(np.eye(4, dtype=np.float32)[:3], (n, 1, 1))
+    poses[:, 0, 3] = 0.12 * np.arange(n)                    # each frame 12 cm further along x: new blocks
+
+    def batch(g):
+        rec = np.zeros(n, L.FUSE_RECORD_DTYPE)
+        P = np.ascontiguousarray(poses.reshape(n, 12))
+        st = L.load().tf_scene_fuse_frames(g._h, None, ctypes.c_void_p(dev.ptr), W * H * 2, 0,
+                                           P.ctypes.data_as(ctypes.c_void_p), n, rec.ctypes.data_as(ctypes.c_void_p))
+        return st, rec
+
+    clean = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy))
+    st0, rec0 = batch(clean)
+    assert st0 == L.TF_OK
+    assert rec0["lastFreeBlockId"][2] < rec0["lastFreeBlockId"][1]      # the clean run allocates at frame 2
+    clean.close()
+    monkeypatch.setenv("TFUSION_VIS_FAULT", "2")
+    g = TopFu(default_params(cols=W, rows=H, fx=fx, fy=fy, cx=cx, cy=cy))
+    st1, rec1 = batch(g)
+    assert st1 == L.TF_HIP_ERROR
+    assert rec1["lastFreeBlockId"][0] == rec0["lastFreeBlockId"][0]     # frame 0 as the clean run
+    assert (rec1["lastFreeBlockId"][2:] == rec1["lastFreeBlockId"][1]).all(), rec1["lastFreeBlockId"]
+    st2, rec2 = batch(g)
+    assert st2 == L.TF_HIP_ERROR and (rec2["lastFreeBlockId"] == 0).all()   # nothing enqueued, records untouched
+    g.reset()
+    st3, rec3 = batch(g)
+    assert st3 == L.TF_OK and (rec3["lastFreeBlockId"] == rec0["lastFreeBlockId"]).all()
+    g.close()
+    dev.free()

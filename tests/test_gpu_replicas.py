@@ -62,9 +62,14 @@ def test_bench_two_ranks_one_device_file_collective():
 def test_bench_two_ranks_one_device_rccl():
     """The same over RCCL.  RCCL refuses two ranks on one device ("Duplicate GPU detected", an
     invalid-usage error raised after the bootstrap exchange of the unique id succeeded), so on a
-    one-GPU box this reaches the communicator's duplicate check and skips; any other failure
-    (the unique id, the bootstrap network) fails the test."""
+    one-GPU box every rank falls back to the file collective and the line says why
+    (`rccl_error`); on a node with two devices the numbers go over RCCL."""
     r = _two_ranks("rccl")
-    if r.returncode != 0 and "Duplicate GPU detected" in r.stdout + r.stderr:   # (NCCL_DEBUG prints to stdout)
-        pytest.skip("RCCL: two ranks on one device (Duplicate GPU detected after a good bootstrap)")
-    _check(r, "rccl")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    m = d["multi_gpu"]
+    if m["collective"] == "file":
+        assert "Duplicate GPU" in m.get("rccl_error", "") or "ncclCommInitRank" in m.get("rccl_error", ""), m
+        _check(r, "file")
+    else:
+        _check(r, "rccl")

@@ -440,12 +440,13 @@ extern "C" tf_status tf_create(const tf_params* pin, tf_ctx** out)
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = tfk_check_div3(c, pin->mu, &c->mu_exact3);   // integrate: eta / mu
     if (e != hipSuccess) { ctx_free(c); return tf_from_hip(e); }
-    {   // the ICP iterations' pose algebra (tf_set_pose_algebra): TFUSION_ICP_SOLVE=svd / opencv4 (the
-        // reference's cv::solve DECOMP_SVD, OpenCV 3.x-4.x), opencv2 (OpenCV 2.4.9); default canonical
+    {   // the ICP iterations' pose algebra (tf_set_pose_algebra): by default the reference's own,
+        // cv::determinant / cv::solve(DECOMP_SVD) / Affine3f as OpenCV 3.x-4.x write them;
+        // TFUSION_ICP_SOLVE=opencv2 (OpenCV 2.4.9) or canonical (the short block-Schur tail)
         const char* env = getenv("TFUSION_ICP_SOLVE");
-        c->pose_alg = !env ? TF_POSE_ALGEBRA_CANONICAL
-                    : (!strcmp(env, "svd") || !strcmp(env, "opencv4")) ? TF_POSE_ALGEBRA_OPENCV4
-                    : !strcmp(env, "opencv2") ? TF_POSE_ALGEBRA_OPENCV2 : TF_POSE_ALGEBRA_CANONICAL;
+        c->pose_alg = !env ? TF_POSE_ALGEBRA_OPENCV4
+                    : !strcmp(env, "canonical") ? TF_POSE_ALGEBRA_CANONICAL
+                    : !strcmp(env, "opencv2") ? TF_POSE_ALGEBRA_OPENCV2 : TF_POSE_ALGEBRA_OPENCV4;
     }
     {   // ICP: one persistent launch per frame when all its workgroups fit at once; otherwise (or
         // with TFUSION_ICP_PERSISTENT=0) one k_icp_iter launch per iteration
@@ -1364,6 +1365,7 @@ extern "C" tf_status tf_scene_fuse_frames(tf_ctx* c, const float intr[4], const 
     if (!c || !dev_frames || !poses_rt || n < 0) return TF_INVALID_ARG;
     if (pitch == 0) pitch = (size_t)c->W * 2;
     if (pitch < (size_t)c->W * 2 || (n > 1 && stride < pitch * (size_t)c->H)) return TF_INVALID_ARG;
+    if (c->st_host->sticky_error) return TF_HIP_ERROR;     // (in error since an earlier call: nothing runs)
     if (n == 0) return TF_OK;
     if (n > c->fuse_cap) {              // the pose / record lists grow to the largest batch seen
         TF_CHECK(hipStreamSynchronize(c->stream));

@@ -1259,7 +1259,11 @@ __device__ __forceinline__ void fuse_head_part(int b, const FuseNext& f, const V
         float pose[12];
 #pragma unroll
         for (int i = 0; i < 12; ++i) pose[i] = f.pose[i];
-        const int halted = st->halt;                       // (only a frame end writes it)
+        // (only a frame end writes halt; sticky_error: an engine batch's failed wait, k_vis_build --
+        // every later frame of the batch no-ops, and the abort written here equals the one the
+        // failing frame's own head wrote unless that frame ran, so the write cannot change what a
+        // concurrent reader in this grid sees)
+        const int halted = st->halt | st->sticky_error;
         if (b == 0 && threadIdx.x == 0) {
             tf_set_pose_matrices(st, pose, 2);
             st->abort = halted ? 1 : 0;
@@ -1294,6 +1298,9 @@ k_fuse_tail(IntegArgs a, TfDevState* __restrict__ st, const TfHashEntry* __restr
 {
     const int b = (int)blockIdx.x;
     if (b < a.fuse_nwg) {
+        // frame k's visible list failed to build (sticky_error, written by its k_vis_build launch,
+        // ordered before this one): no integration over it
+        if (st->sticky_error) return;
         integ_body<false, false, true>(a, st, hash, visibleIds, vba, EdArgs{}, cnt);
         return;
     }

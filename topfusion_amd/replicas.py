@@ -252,17 +252,63 @@ class RcclGroup:
             self.comm = None
 
 
+def device_identity(device, standin=False):
+    """(domain, bus, device, function) of HIP device `device` (hipDeviceGetPCIBusId on the product's
+    runtime): what proves that the ranks of a job ran on distinct GPUs.  The CPU stand-in reports
+    (-1, rank-free placeholder) -- the caller passes its rank as `device`."""
+    if standin:
+        return [-1, int(device), 0, 0]
+    from topfusion_amd import _lib
+    _lib.load()
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipDeviceGetPCIBusId.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    hip.hipDeviceGetPCIBusId.restype = ctypes.c_int
+    buf = ctypes.create_string_buffer(64)
+    if hip.hipDeviceGetPCIBusId(buf, 64, int(device)) != 0:
+        return [-2, int(device), 0, 0]
+    return parse_bus_id(buf.value.decode())
+
+
+def parse_bus_id(text):
+    """"dddd:bb:dd.f" -> [domain, bus, device, function] (hex fields)."""
+    dom, bus, rest = text.strip().split(":")
+    dev, fn = rest.split(".")
+    return [int(dom, 16), int(bus, 16), int(dev, 16), int(fn, 16)]
+
+
+def format_bus_id(v):
+    if v[0] < 0:
+        return f"standin:{int(v[1])}" if v[0] == -1 else f"unknown:device{int(v[1])}"
+    return f"{int(v[0]):04x}:{int(v[1]):02x}:{int(v[2]):02x}.{int(v[3]):x}"
+
+
 class Replicas:
     """The collective a bench rank uses: RCCL for the numbers (`kind` "rccl"), the file group for
-    the unique id; or the file group alone ("file": the CPU stand-in, or world 1)."""
+    the unique id; or the file group alone ("file": the CPU stand-in, or world 1).  If RCCL cannot
+    be set up (a missing library, a communicator error) every rank falls back to the file group
+    and the line says so (`collective` "file", `rccl_error`)."""
 
     def __init__(self, rank, local_rank, world, kind="rccl"):
         self.rank, self.local_rank, self.world = rank, local_rank, world
         self.files = FileGroup(rank, world) if world > 1 else None
         self.rccl = None
+        self.rccl_error = None
         self.kind = kind if world > 1 else "none"
         if world > 1 and kind == "rccl":
-            self.rccl = RcclGroup(rank, world, local_rank, self.files)
+            try:
+                self.rccl = RcclGroup(rank, world, local_rank, self.files)
+            except (OSError, RuntimeError) as e:
+                self.rccl_error = f"rank {rank}: {e}"
+            # every rank learns whether every rank has a communicator (over the file group, which
+            # works either way); one failure sends all of them to the file group
+            errs = self.files.allgather(self.rccl_error)
+            bad = [e for e in errs if e]
+            if bad:
+                if self.rccl is not None:
+                    self.rccl.close()
+                    self.rccl = None
+                self.kind = "file"
+                self.rccl_error = bad[0]
 
     @property
     def group(self):
@@ -286,20 +332,34 @@ class Replicas:
         per = [tuple(v) for v in g.allgather([float(elapsed), float(frames)])]
         return emax, total, per
 
-    def summary(self, elapsed, frames):
+    def summary(self, elapsed, frames, identity=None, extra=None):
         """The multi-GPU fields of the bench line (rank 0): world, the communicator's own rank
-        count, per-rank frames/s and their spread.  The driver computes scaling efficiency
-        itself from the per-N values, so none is reported here."""
+        count, per-rank frames/s and their spread, and -- so that an N-GPU line proves itself --
+        each rank's device (PCI bus id, `identity` = device_identity()) and the per-rank numbers in
+        `extra` (name -> number, the same names on every rank, e.g. frames_ok, icp_fallbacks).
+        `distinct_devices` is false when two ranks report the same device.  The driver computes
+        scaling efficiency itself from the per-N values, so none is reported here."""
         emax, total, per = self.combine(elapsed, frames)
         fps = [f / e if e > 0 else 0.0 for e, f in per]
-        return emax, total, {
+        keys = sorted(extra or {})
+        vec = [float(v) for v in (identity or [-2, self.local_rank, 0, 0])] + [float(extra[k]) for k in keys]
+        rows = self.group.allgather(vec) if self.world > 1 else [vec]
+        devs = [format_bus_id(r[:4]) for r in rows]
+        out = {
             "world": self.world, "collective": self.kind,
             "collective_nranks": self.nranks(),
             "per_rank_frames_per_sec": [round(v, 2) for v in fps],
             "per_rank_elapsed_s": [round(e, 5) for e, _ in per],
             "per_rank_frames": [int(f) for _, f in per],
             "rank_spread": round(min(fps) / max(fps), 4) if fps and max(fps) > 0 else None,
+            "per_rank_device": devs,
+            "distinct_devices": len(set(devs)) == len(devs),
         }
+        for i, k in enumerate(keys):
+            out[f"per_rank_{k}"] = [int(r[4 + i]) if float(r[4 + i]).is_integer() else r[4 + i] for r in rows]
+        if self.rccl_error:
+            out["rccl_error"] = self.rccl_error
+        return emax, total, out
 
     def close(self):
         if self.rccl is not None:

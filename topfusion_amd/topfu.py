@@ -157,8 +157,9 @@ class TopFu:
     POSE_ALGEBRAS = {"canonical": 0, "opencv2": 2, "opencv4": 4, "svd": 4}
 
     def set_pose_algebra(self, algebra):
-        """The ICP iterations' det / solve / Rodrigues (tf_set_pose_algebra): "canonical" (default,
-        LDL^T + sinc Rodrigues) or the reference's OpenCV algebra, "opencv4" (= "svd") / "opencv2"."""
+        """The ICP iterations' det / solve / Rodrigues (tf_set_pose_algebra): the reference's OpenCV
+        algebra, "opencv4" (default; = "svd") or "opencv2" (2.4.9), or "canonical" (LU + 2 x 2 block
+        Schur solve + sinc Rodrigues: a shorter serial tail, not the reference's arithmetic)."""
         a = self.POSE_ALGEBRAS[algebra] if isinstance(algebra, str) else int(algebra)
         L.check(L.load().tf_set_pose_algebra(self._h, a), "tf_set_pose_algebra")
 
