@@ -4,6 +4,7 @@
 // tests/test_cpp_api.py::test_cv_types_alias_compiles instantiates.  Never used by the product.
 #pragma once
 #include <memory>
+#include <string>
 
 namespace cv
 {
@@ -34,5 +35,17 @@ namespace cv
     typedef Vec<double, 3> Vec3d;
     typedef Vec<int, 3> Vec3i;
 
-    struct Mat {};
+    typedef std::string String;
+    enum { CV_8U = 0, CV_16U = 2 };                                    // core/hal/interface.h depths
+    struct Mat {                                                       // core/mat.hpp: what demo.cpp uses
+        int rows = 0, cols = 0;
+        unsigned char* data = nullptr;
+        size_t step = 0;
+        void create(int r, int c, int type) { rows = r; cols = c; (void)type; }
+        template <typename T> T* ptr(int y = 0) { return reinterpret_cast<T*>(data + step * (size_t)y); }
+        void convertTo(Mat& m, int rtype, double alpha = 1, double beta = 0) const { (void)m; (void)rtype; (void)alpha; (void)beta; }
+    };
 }
+#define CV_8U 0
+#define CV_16U 2
+#define CV_8UC4 24

@@ -138,3 +138,20 @@ def test_cv_types_alias_compiles():
                         "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include", "-"],
                        input=probe, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+REF_DEMO = "/root/reference/apps/demo.cpp"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_DEMO), reason="the reference tree is not on this machine")
+def test_reference_demo_compiles():
+    """the reference's own apps/demo.cpp -- the file itself, read where it lies,
+    not an extract -- compiles against include/ (tfusion/topfu.hpp, tfusion/types.hpp,
+    io/capture.hpp) with TFUSION_OPENCV_TYPES on.  Compile-only (-fsyntax-only), against the
+    stand-in OpenCV headers of tests/cvstub (core, highgui, imgproc, viz: the declarations demo.cpp
+    uses, with OpenCV's public signatures; OpenCV is absent from this image)."""
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-DTFUSION_OPENCV_TYPES=1", "-D__HIP_PLATFORM_AMD__",
+                        "-I", os.path.join(ROOT, "tests", "cvstub"), "-I", os.path.join(ROOT, "include"),
+                        "-I", "/opt/rocm/include", REF_DEMO],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]

@@ -670,6 +670,9 @@ __device__ __forceinline__ double icp_sv_rowsum(double q, int lane)
 // in [1, 2), relative) from the midpoint pattern (one add and one unsigned compare), and, where
 // the value's range does not already guarantee it (full = true), v must be a normal float.
 #define SV_MARGIN (1u << 16)
+#ifndef SV_WQ_BPERM
+#define SV_WQ_BPERM 0          // 1: |partner row|^2 fetched from the partner's lane 0 (A/B: 0.6% slower)
+#endif
 template <bool full>
 __device__ __forceinline__ bool icp_sv_round_safe(double v)
 {
@@ -802,12 +805,19 @@ __device__ __forceinline__ void icp_sv_level(float& a, float& v, int lane, int s
     const float x1 = icp_dpp_f<0x101>(xa), x2 = icp_dpp_f<0x102>(xa), x3 = icp_dpp_f<0x103>(xa);
     const float x4 = icp_dpp_f<0x104>(xa), x5 = icp_dpp_f<0x105>(xa);
     const double e0 = xa, e1 = x1, e2 = x2, e3 = x3, e4 = x4, e5 = x5;
+#if SV_WQ_BPERM
+    // |partner row|^2: the partner row's lane 0 formed it (its wo), fetched while p is summed
+    const double wq = icp_bperm_d(src & ~7, wo);
+    double p = fma(d0, e0, 0.0);
+    p = fma(d1, e1, p); p = fma(d2, e2, p); p = fma(d3, e3, p); p = fma(d4, e4, p); p = fma(d5, e5, p);
+#else
     double wq = fma(e0, e0, 0.0), p = fma(d0, e0, 0.0);
     wq = fma(e1, e1, wq); p = fma(d1, e1, p);
     wq = fma(e2, e2, wq); p = fma(d2, e2, p);
     wq = fma(e3, e3, wq); p = fma(d3, e3, p);
     wq = fma(e4, e4, wq); p = fma(d4, e4, p);
     wq = fma(e5, e5, wq); p = fma(d5, e5, p);
+#endif
     SV_T(2, p + wo + wq);
     // beta = W[I] - W[J] on both rows' lanes (RN(y - x) = -RN(x - y)); ab = W[I] W[J]
     const double dw = wo - wq;
