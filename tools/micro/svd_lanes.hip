@@ -125,6 +125,19 @@ int main(int argc, char** argv)
             sys.insert(sys.end(), sm, sm + 27);
             ++ndeg;
         }
+    // equal singular values (the sort's tie path): scaled identities, diagonals with repeated
+    // entries, permuted diagonals
+    for (int rep = 0; rep < 60; ++rep) {
+        float sm[27] = {};
+        float d[6];
+        for (int i = 0; i < 6; ++i) d[i] = 1.f + (float)((rep + i * (rep % 4)) % 3);
+        if (rep % 5 == 0) for (int i = 0; i < 6; ++i) d[i] = 0.5f * (1 + rep);
+        int s2 = 0;
+        for (int a = 0; a < 6; ++a)
+            for (int c = a; c < 7; ++c) sm[s2++] = c == 6 ? frand() : (a == c ? d[a] : 0.f);
+        sys.insert(sys.end(), sm, sm + 27);
+        ++ndeg;
+    }
     const int n = (int)(sys.size() / 27);
     float *dS, *dX, *dO; int* dB; long long* dC;
     hipMalloc(&dS, sys.size() * 4); hipMalloc(&dX, (size_t)n * 6 * 4); hipMalloc(&dB, 4); hipMalloc(&dC, 16 * 8); hipMalloc(&dO, 64);

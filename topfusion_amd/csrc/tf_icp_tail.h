@@ -647,6 +647,18 @@ __device__ __forceinline__ double icp_bperm_d(int src_lane, double v)
     const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(unsigned)(u >> 32));
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
+// forward permute: this lane's value lands in lane dst_lane (a permutation of the lanes)
+__device__ __forceinline__ float icp_fperm_f(int dst_lane, float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_permute(dst_lane << 2, __builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ double icp_fperm_d(int dst_lane, double v)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_ds_permute(dst_lane << 2, (int)(unsigned)u);
+    const unsigned hi = (unsigned)__builtin_amdgcn_ds_permute(dst_lane << 2, (int)(unsigned)(u >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 // sum over the row's columns k = 0..5 of q, in order (0 + q0 + q1 + ... + q5, as the serial
 // loops add), returned to every lane of the row: q1..q5 reach lane 0 of the 8-lane group by DPP
 // row_shl (within a 16-lane DPP row both groups' lanes 0 read in range), the sum is broadcast
@@ -903,13 +915,8 @@ __device__ __forceinline__ void icp_cv_solve_svd6_lanes(float tot, int stride, i
     }
     // ---- singular values, sorted descending (selection sort, strict <: the first maximum)
     const double Wf = sqrt(icp_sv_rowsum((double)a * (double)a, lane));
-    double Wu[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) Wu[i] = icp_rl_d(Wf, 8 * i);
-    bool zero = false;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) zero = zero || Wu[i] <= TF_FLT_MIN;
-    if (zero) {                                   // a zero singular value: the serial finish
+    if (__builtin_amdgcn_ballot_w64((r < 6) & (k == 0) & (Wf <= TF_FLT_MIN)) != 0) {
+        // a zero singular value: the serial finish (random completion) on the gathered matrices
 #ifdef TF_SV_STATS
         if (lane == 0) atomicAdd(&g_sv_stats[2], 1ull);
 #endif
@@ -923,34 +930,67 @@ __device__ __forceinline__ void icp_cv_solve_svd6_lanes(float tot, int stride, i
         icp_cv_svd_finish<ALG>(At, Vt, bu, x);
         return;
     }
-    unsigned perm = 0x543210u;                    // sorted position i <- row (perm >> 4 i) & 15
+    double Wu[6];
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
-        int j = i;
-        double wj = Wu[i];
+    for (int i = 0; i < 6; ++i) Wu[i] = icp_rl_d(Wf, 8 * i);
+    // Six distinct values: the selection sort's result is the descending order, so row r goes to
+    // position #{j : W_j > W_r} -- counted on every lane of the row, moved by one forward permute.
+    // Equal values (or a NaN) leave the order to the selection sort's swaps: run it (uniform).
+    int rank = 0, eq = 0;
 #pragma unroll
-        for (int kk = i + 1; kk < 6; kk++) if (wj < Wu[kk]) { j = kk; wj = Wu[kk]; }
-        j = __builtin_amdgcn_readfirstlane(j);
-        if (j != i) {
+    for (int j = 0; j < 6; ++j) { rank += Wu[j] > Wf ? 1 : 0; eq += Wu[j] == Wf ? 1 : 0; }
+    float as, vs;
+    double sd, Ws[6];
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64((r < 6) & (eq != 1)) == 0, 1)) {
+        const int dst = r < 6 ? 8 * rank + k : lane;
+        as = icp_fperm_f(dst, a);
+        vs = icp_fperm_f(dst, v);
+        sd = icp_fperm_d(dst, Wf);                // W[r] after the sort
 #pragma unroll
-            for (int rr = i + 1; rr < 6; ++rr)
-                if (rr == j) {
-                    const double t = Wu[i]; Wu[i] = Wu[rr]; Wu[rr] = t;
-                    const unsigned pi = (perm >> (4 * i)) & 15u, pr = (perm >> (4 * rr)) & 15u;
-                    perm = (perm & ~((15u << (4 * i)) | (15u << (4 * rr)))) | (pr << (4 * i)) | (pi << (4 * rr));
-                }
+        for (int i = 0; i < 6; ++i) Ws[i] = icp_rl_d(sd, 8 * i);
+    } else {
+        unsigned perm = 0x543210u;                // sorted position i <- row (perm >> 4 i) & 15
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            int j = i;
+            double wj = Wu[i];
+#pragma unroll
+            for (int kk = i + 1; kk < 6; kk++) if (wj < Wu[kk]) { j = kk; wj = Wu[kk]; }
+            j = __builtin_amdgcn_readfirstlane(j);
+            if (j != i) {
+#pragma unroll
+                for (int rr = i + 1; rr < 6; ++rr)
+                    if (rr == j) {
+                        const double t = Wu[i]; Wu[i] = Wu[rr]; Wu[rr] = t;
+                        const unsigned pi = (perm >> (4 * i)) & 15u, pr = (perm >> (4 * rr)) & 15u;
+                        perm = (perm & ~((15u << (4 * i)) | (15u << (4 * rr)))) | (pr << (4 * i)) | (pi << (4 * rr));
+                    }
+            }
         }
+        const int sl = r < 6 ? 8 * (int)((perm >> (4 * r)) & 15u) + k : lane;
+        as = icp_bperm_f(sl, a);
+        vs = icp_bperm_f(sl, v);
+        sd = icp_bperm_d(sl, Wf);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Ws[i] = Wu[i];
     }
-    const int sl = r < 6 ? 8 * (int)((perm >> (4 * r)) & 15u) + k : lane;
-    float as = icp_bperm_f(sl, a);
-    const float vs = icp_bperm_f(sl, v);
-    const double sd = icp_bperm_d(sl, Wf);        // W[r] after the sort
     SV_T(6, as + vs + sd);
-    as *= (float)(1 / sd);                        // the row normalised
+    // the row normalised: RN_f(1 / sd) from v_rcp_f64 and one Newton step (within 2^-48) where that
+    // double is clear of a float rounding boundary, else the IEEE division
+    {
+        const double r0 = __builtin_amdgcn_rcp(sd);
+        const double rq = fma(fma(-sd, r0, 1.0), r0, r0);
+        float scl = (float)rq;
+        const bool exact = icp_sv_round_safe<true>(rq);
+        if (__builtin_amdgcn_ballot_w64(!exact) != 0) {
+            if (!exact) scl = (float)(1 / sd);
+        }
+        as *= scl;
+    }
     // ---- SVBkSbImpl_<float>: threshold = (sum of the float w[i], in order) * (float)(2 DBL_EPSILON)
     double thr = 0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) thr += (float)Wu[i];
+    for (int i = 0; i < 6; ++i) thr += (float)Ws[i];
     thr *= (double)(float)(2.220446049250313e-16 * 2);
     const float wfl = (float)sd;
     const bool live = !((double)fabs(wfl) <= thr);
