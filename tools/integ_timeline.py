@@ -50,3 +50,11 @@ for p_ in sorted(set(passes.tolist())):
     print(f"  {p_} passes: n={m.sum()} dur p50/max {np.median(d[m]):.2f}/{d[m].max():.2f}")
 edges = np.arange(0, en[used].max() + 1, 1.0)
 print("resident every 1 us:", [int(((st[used] <= e) & (en[used] > e)).sum()) for e in edges])
+# by XCD (blockIdx.x mod 8 under round-robin dispatch; TFUSION_INTEG_BANDS: band x on XCD x)
+xs = sel % 8
+print("integrate end by XCD (p50/max us), workgroups: " +
+      " ".join(f"x{x}:{np.median(en[sel][xs == x]):.1f}/{en[sel][xs == x].max():.1f}" for x in range(8)))
+cnt = (ctypes.c_int * 9)()
+edg = (ctypes.c_float * 18)()
+_lib.load().tf_debug_bands(tf._h, cnt, edg)
+print("band_on", cnt[0], "counts", list(cnt[1:]), "edges", [round(x, 1) for x in edg[0:9]], [round(x, 1) for x in edg[9:18]])
