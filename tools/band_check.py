@@ -1,6 +1,7 @@
 """XCD bands (k_vis_build, TFUSION_INTEG_BANDS): the visible blocks' centre columns after the C2 orbit
 and one tracked frame, recomputed on the host from the hash, the visible list and the pose, against
-the device's band counts and edges (tf_debug_bands; diagnostic).  On the GPU box:
+the device's band counts and edges (tf_debug_bands; diagnostic builds of the experiment in
+tools/experiments/integ_xcd_bands.patch only).  On the GPU box:
   python tools/band_check.py"""
 import ctypes, os, sys
 import numpy as np

@@ -54,7 +54,9 @@ print("resident every 1 us:", [int(((st[used] <= e) & (en[used] > e)).sum()) for
 xs = sel % 8
 print("integrate end by XCD (p50/max us), workgroups: " +
       " ".join(f"x{x}:{np.median(en[sel][xs == x]):.1f}/{en[sel][xs == x].max():.1f}" for x in range(8)))
-cnt = (ctypes.c_int * 9)()
-edg = (ctypes.c_float * 18)()
-_lib.load().tf_debug_bands(tf._h, cnt, edg)
-print("band_on", cnt[0], "counts", list(cnt[1:]), "edges", [round(x, 1) for x in edg[0:9]], [round(x, 1) for x in edg[9:18]])
+# (the XCD-band experiment's builds, tools/experiments/integ_xcd_bands.patch: its band counts and edges)
+if hasattr(_lib.load(), "tf_debug_bands"):
+    cnt = (ctypes.c_int * 9)()
+    edg = (ctypes.c_float * 18)()
+    _lib.load().tf_debug_bands(tf._h, cnt, edg)
+    print("band_on", cnt[0], "counts", list(cnt[1:]), "edges", [round(x, 1) for x in edg[0:9]], [round(x, 1) for x in edg[9:18]])
