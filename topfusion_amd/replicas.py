@@ -349,7 +349,7 @@ class Replicas:
             "world": self.world, "collective": self.kind,
             "collective_nranks": self.nranks(),
             "per_rank_frames_per_sec": [round(v, 2) for v in fps],
-            "per_rank_elapsed_s": [round(e, 5) for e, _ in per],
+            "per_rank_elapsed_s": [float(f"{e:.6g}") for e, _ in per],   # (6 significant digits: short runs too)
             "per_rank_frames": [int(f) for _, f in per],
             "rank_spread": round(min(fps) / max(fps), 4) if fps and max(fps) > 0 else None,
             "per_rank_device": devs,
