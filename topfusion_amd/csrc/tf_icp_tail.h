@@ -793,6 +793,66 @@ struct SvTimes { long long t0, acc[8]; };
 #define SV_TARG
 #define SV_T(k, val_) do { } while (0)
 #endif
+// The partner row's element by lane swaps (SV_XOR_PARTNER): in every level each row's partner is
+// its index XOR one or two masks, and a row-index XOR of 1 / 2 / 4 is a lane XOR of 8 / 16 / 32 --
+// DPP row_ror:8, v_permlane16_swap, v_permlane32_swap (+ one v_cndmask each) -- instead of one
+// ds_bpermute round trip.  Rows without a partner (and the padding rows) get some other row's
+// element; nothing of theirs is used.  A/B (round 6, tools/micro/svd_lanes.hip, bit-exact): 21 708
+// against 20 254 cycles per solve -- the swap chains (up to three deep, each with its select) take
+// longer than the one round trip; off.
+#ifndef SV_XOR_PARTNER
+#define SV_XOR_PARTNER 0
+#endif
+__device__ __forceinline__ float icp_x8(float x) { return icp_dpp_f<0x128>(x); }
+__device__ __forceinline__ float icp_x16(float x)
+{
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return icp_lsel(0xffff0000ffff0000ull, __uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float icp_x32(float x)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return icp_lsel(0xffffffff00000000ull, __uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+template <int L>
+__device__ __forceinline__ float icp_sv_partner(float x)
+{
+    // level L's pairs as row-index XOR masks (SV_P): rows of mask A take a, the rest b
+    if constexpr (L == 0) {                 // (0,1) ^1; (2,5) (3,4) ^7
+        const float a1 = icp_x8(x), a7 = icp_x32(icp_x16(a1));
+        return icp_lsel(sv_row_lanes(0x03u), a1, a7);
+    } else if constexpr (L == 1) {          // (0,2) ^2; (3,5) ^6
+        const float a2 = icp_x16(x), a6 = icp_x32(a2);
+        return icp_lsel(sv_row_lanes(0x05u), a2, a6);
+    } else if constexpr (L == 2) {          // (0,3) (1,2) ^3; (4,5) ^1
+        const float a1 = icp_x8(x), a3 = icp_x16(a1);
+        return icp_lsel(sv_row_lanes(0x0fu), a3, a1);
+    } else if constexpr (L == 3) {          // (0,4) ^4; (1,3) ^2
+        const float a4 = icp_x32(x), a2 = icp_x16(x);
+        return icp_lsel(sv_row_lanes(0x11u), a4, a2);
+    } else if constexpr (L == 4) {          // (0,5) (1,4) ^5; (2,3) ^1
+        const float a1 = icp_x8(x), a5 = icp_x32(a1);
+        return icp_lsel(sv_row_lanes(0x33u), a5, a1);
+    } else {                                // (1,5) ^4; (2,4) ^6
+        const float a4 = icp_x32(x), a6 = icp_x16(a4);
+        return icp_lsel(sv_row_lanes(0x22u), a4, a6);
+    }
+}
+// the partner masks above, checked against SV_P at compile time
+constexpr bool sv_xor_ok()
+{
+    const unsigned A[6] = { 0x03u, 0x05u, 0x0fu, 0x11u, 0x33u, 0x22u };
+    const int ma[6] = { 1, 2, 3, 4, 5, 4 }, mb[6] = { 7, 6, 1, 2, 1, 6 };
+    for (int L = 0; L < 6; ++L)
+        for (int r = 0; r < 6; ++r) {
+            if (SV_P[L][r] == 15) continue;
+            const int m = ((A[L] >> r) & 1u) ? ma[L] : mb[L];
+            if ((r ^ m) != SV_P[L][r]) return false;
+        }
+    return true;
+}
+static_assert(sv_xor_ok(), "icp_sv_partner: masks must match SV_P");
+
 // one level of a period: every row with a partner in an enabled sweep rotates with it.  Lane 0
 // of each row group gathers its row and the partner row (DPP row_shl) and forms the three sums the
 // rotation needs in the serial order -- p = sum_k At[I][k] At[J][k] and both |row|^2, exact double
@@ -807,7 +867,12 @@ __device__ __forceinline__ void icp_sv_level(float& a, float& v, int lane, int s
     constexpr unsigned long long TL = sv_row_lanes(SV_TAIL_ROWS[L]);
     if constexpr (ACT == 0) return;
     SV_T(0, a);
+#if SV_XOR_PARTNER
+    const float xa = icp_sv_partner<L>(a), xv = icp_sv_partner<L>(v);
+    (void)src;
+#else
     const float xa = icp_bperm_f(src, a), xv = icp_bperm_f(src, v);
+#endif
     const float a1 = icp_dpp_f<0x101>(a), a2 = icp_dpp_f<0x102>(a), a3 = icp_dpp_f<0x103>(a);
     const float a4 = icp_dpp_f<0x104>(a), a5 = icp_dpp_f<0x105>(a);
     const double d0 = a, d1 = a1, d2 = a2, d3 = a3, d4 = a4, d5 = a5;
