@@ -331,7 +331,9 @@ k_icp_iter(IcpLevel L, TfDevState* __restrict__ st, float* __restrict__ T, unsig
 #define IP_SREG 1                       // CTA slots kept in registers per wave (8 per WG; larger images use k_icp_iter)
 #define IP_SPIN_LIMIT (1u << 21)
 #ifndef IP_SLEEP
-#define IP_SLEEP 1                      // s_sleep between hand-off polls (x 64 cycles)
+#define IP_SLEEP 0                      // s_sleep between hand-off polls (x 64 cycles); round 6 A/B under the
+                                        // OpenCV 4 algebra: 0 vs 1 = 2829 / 2825 vs 2816 / 2819 frames/s, ICP
+                                        // 0.304 vs 0.306 ms (profiles/r06/ab_icp_poll_sleep.txt); 2 = as 1
 #endif
 #define IP_PART (2 * ICP_NWG * ICP_T_STRIDE + 16)   // column slots (double-buffered by generation parity), then
                                                  // the 8 residue-class partials, double-buffered
